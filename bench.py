@@ -1,0 +1,269 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident RS encode + decode of 1 MiB chunks on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-seconds S]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (per rank; weak scaling — every rank owns its own 1024 chunks, no collective on the
+data path): BASELINE configs[1]+[2] — 1024 x 1 MiB chunks, RS(k=4, m=2) (zfec Encoder(4, 6)):
+one step = encode all 1024 chunks + decode/reassemble all 1024 chunks with data shards
+{1, 3} erased (read from the surviving data + parity blocks in HBM).  Inputs are resident in
+HBM before the timed region.  value = (chunk bytes encoded + chunk bytes decoded) by all
+ranks / max-over-ranks wall time, in GiB/s (2^30 B).
+
+Also reported on the same line:
+  roofline      the encode kernel (the dominant, BASELINE-target kernel): algorithmic bytes
+                per launch (n read + (m-k)*B written = 1.5 MiB per chunk) / average launch
+                time from HIP events on the launch stream, vs 8 TB/s HBM peak; `traffic` =
+                rocprofv3 PMC bytes per launch from profiles/ (FETCH_SIZE x2 + WRITE_SIZE,
+                gfx950 correction) when a matching summary is committed, else null
+  cpu_baseline  oracle/fec_oracle.c (C restatement of zfec's fec.c: 64 KiB LUT, 8 KiB
+                strides), 1 thread, on a bounded sample of the same workload, rank 0 at N=1
+  e2e           host-buffer encode+decode through the C ABI incl. pinned staging + PCIe
+                (reported beside `value`, never as it)
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+N_CHUNKS = 1024
+CHUNK = 1 << 20
+K, M = 4, 6  # RS(k=4, m=2) == zfec Encoder(4, 6)
+ERASED = (1, 3)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    return ap.parse_args()
+
+
+def enc_descs(nchunks, n, k, m):
+    from storb_amd._lib import ENC_DTYPE
+
+    B = -(-n // k)
+    d = np.zeros(nchunks, dtype=ENC_DTYPE)
+    d["in_off"] = np.arange(nchunks, dtype=np.uint64) * n
+    d["n"] = n
+    d["parity_off"] = np.arange(nchunks, dtype=np.uint64) * (m - k) * B
+    d["parity_stride"] = B
+    d["k"] = k
+    d["m"] = m
+    return d, B
+
+
+def dec_descs(nchunks, n, k, m, B, data_base, par_base, erased):
+    from storb_amd._lib import DEC_DTYPE
+
+    keep = [s for s in range(m) if s not in erased][:k]
+    d = np.zeros(nchunks, dtype=DEC_DTYPE)
+    d["out_off"] = np.arange(nchunks, dtype=np.uint64) * n
+    d["B"] = B
+    d["padlen"] = B * k - n
+    d["slot0"] = np.arange(nchunks, dtype=np.uint64) * k
+    d["k"] = k
+    d["m"] = m
+    sn = np.tile(np.array(keep, np.int32), nchunks)
+    offs = np.zeros(nchunks * k, np.uint64)
+    ci = np.arange(nchunks, dtype=np.uint64)
+    for j, s in enumerate(keep):
+        offs[j::k] = (data_base + ci * n + s * B) if s < k else (par_base + ci * (m - k) * B + (s - k) * B)
+    return d, sn, offs
+
+
+def load_traffic():
+    """Per-launch HBM bytes of the encode kernel from a committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_encode_c2.json")
+    try:
+        with open(path) as f:
+            j = json.load(f)
+        if j.get("workload") == "c2" and j.get("hbm_bytes_per_launch"):
+            return float(j["hbm_bytes_per_launch"])
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(seconds: float) -> dict:
+    """oracle/fec_oracle.c, 1 thread: encode + decode ({1,3} erased) of 1 MiB chunks, RS(4,2)."""
+    from oracle import cfec
+
+    lib = cfec.lib()
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    rng = np.random.default_rng(0)
+    nsample = 8
+    chunks = [rng.integers(0, 256, CHUNK, dtype=np.uint8).tobytes() for _ in range(nsample)]
+    B = CHUNK // K
+    blocks = (ctypes.c_uint8 * (M * B))()
+    out = (ctypes.c_uint8 * CHUNK)()
+    keep = [s for s in range(M) if s not in ERASED]
+    sn = (ctypes.c_int * K)(*keep)
+    done = 0
+    t0 = time.perf_counter()
+    while True:
+        c = chunks[done % nsample]
+        if lib.fo_easy_encode(K, M, c, CHUNK, ctypes.cast(blocks, u8p)) != B:
+            raise RuntimeError("oracle encode failed")
+        base = ctypes.addressof(blocks)
+        ptrs = (ctypes.c_char_p * K)(*[ctypes.c_char_p(base + s * B) for s in keep])
+        if lib.fo_easy_decode(K, M, ptrs, sn, B, 0, ctypes.cast(out, u8p)):
+            raise RuntimeError("oracle decode failed")
+        if done == 0 and bytes(out) != c:
+            raise RuntimeError("oracle round trip mismatch")
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": round(2 * done * CHUNK / el / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{done} x (encode + decode {{1,3}} erased) of 1 MiB RS(4,2) chunks, {nsample} distinct "
+                      f"chunks cycled, {el:.1f} s, oracle/fec_oracle.c (zfec fec.c restatement, 1 thread)"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    from storb_amd import dist as D
+    from storb_amd.engine import Engine
+
+    rank, local, world = D.rank_env()
+    torch.cuda.set_device(local)
+    dmod = D.init()
+    eng = Engine(local)
+
+    n, k, m = CHUNK, K, M
+    g = torch.Generator(device=f"cuda:{local}")
+    g.manual_seed(1000 + rank)
+    src = torch.randint(0, 256, (N_CHUNKS * n,), dtype=torch.uint8, device=f"cuda:{local}", generator=g)
+    ed, B = enc_descs(N_CHUNKS, n, k, m)
+    par = torch.empty(N_CHUNKS * (m - k) * B, dtype=torch.uint8, device=f"cuda:{local}")
+    out = torch.empty_like(src)
+    dd, sn, offs = dec_descs(N_CHUNKS, n, k, m, B, src.data_ptr(), par.data_ptr(), ERASED)
+
+    def step():
+        eng.encode_batch(ed, src, par, asynchronous=True)
+        eng.decode_batch(dd, sn, offs, 0, out, asynchronous=True)
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    if not torch.equal(out, src):
+        raise SystemExit("bench: decode round trip mismatch")
+
+    eng.set_timing(True)
+    D.barrier(dmod, local)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
+    torch.cuda.synchronize()
+    D.barrier(dmod, local)
+    el = time.perf_counter() - t0
+    eng.set_timing(False)
+    enc_ms, enc_n = eng.collect_timing("encode")
+    dec_ms, dec_n = eng.collect_timing("decode")
+    el_max = D.max_over_ranks(dmod, el, local)
+
+    bytes_per_step = 2 * N_CHUNKS * n  # encoded + decoded chunk bytes
+    value = world * args.steps * bytes_per_step / el_max / GIB
+
+    enc_alg = N_CHUNKS * (n + (m - k) * B)  # bytes per encode launch
+    dec_alg = N_CHUNKS * (k * B + n)  # reassemble: k blocks read + n written
+    enc_avg_s = enc_ms / 1e3 / max(enc_n, 1)
+    dec_avg_s = dec_ms / 1e3 / max(dec_n, 1)
+    enc_gbs = enc_alg / enc_avg_s / 1e9
+    traffic = load_traffic()
+
+    res = None
+    if rank == 0:
+        res = {
+            "metric": "GiB/s device-resident RS encode+decode, 1 MiB chunks, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (torch.randint uniform bytes, seeded per rank), HBM-resident",
+            "config": {"workload": "1024 x 1 MiB chunks per GPU, RS(k=4,m=2)=zfec(4,6): encode + "
+                                   "decode/reassemble with data shards {1,3} erased",
+                       "chunks_per_gpu": N_CHUNKS, "chunk_bytes": n, "k": k, "m_total": m,
+                       "bytes_per_step_per_gpu": bytes_per_step, "parallelism": f"chunk-partition x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(enc_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(enc_gbs / PEAK_HBM_GBS, 4),
+                         "traffic": traffic,
+                         "kernel": "sec_encode_kernel<2,4,false>",
+                         "algorithmic_bytes_per_launch": enc_alg,
+                         "avg_launch_ms": round(enc_avg_s * 1e3, 4), "launches": enc_n},
+            "decode_kernel": {"achieved": round(dec_alg / dec_avg_s / 1e9, 1), "unit": "GB/s",
+                              "algorithmic_bytes_per_launch": dec_alg, "avg_launch_ms": round(dec_avg_s * 1e3, 4),
+                              "launches": dec_n},
+            "encode_gibs": round(N_CHUNKS * n / enc_avg_s / GIB, 2),
+            "decode_gibs": round(N_CHUNKS * n / dec_avg_s / GIB, 2),
+        }
+
+    # host-buffer (PCIe-inclusive) rate: reported, never `value`
+    if rank == 0 and world == 1 and not args.no_e2e:
+        res["e2e"] = e2e_rate(eng)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    elif rank == 0:
+        res["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    eng.close()
+    if dmod is not None:
+        dmod.destroy_process_group()
+
+
+def e2e_rate(eng, nchunks=256, steps=3) -> dict:
+    """Encode + decode of host-resident 1 MiB chunks through SEC_F_HOST (pinned staging, PCIe)."""
+    rng = np.random.default_rng(7)
+    host = rng.integers(0, 256, nchunks * CHUNK, dtype=np.uint8)
+    ed, B = enc_descs(nchunks, CHUNK, K, M)
+    par = np.empty(nchunks * (M - K) * B, dtype=np.uint8)
+    out = np.empty_like(host)
+    dd, sn, offs = dec_descs(nchunks, CHUNK, K, M, B, host.ctypes.data, par.ctypes.data, ERASED)
+    eng.encode_batch(ed, host, par, host=True)
+    eng.decode_batch(dd, sn, offs, 0, out, host=True)
+    if not np.array_equal(out, host):
+        raise SystemExit("bench: host e2e mismatch")
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.encode_batch(ed, host, par, host=True)
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        eng.decode_batch(dd, sn, offs, 0, out, host=True)
+    t2 = time.perf_counter()
+    tot = nchunks * CHUNK * steps
+    return {"encode_gibs": round(tot / (t1 - t0) / GIB, 3), "decode_gibs": round(tot / (t2 - t1) / GIB, 3),
+            "sample": f"{nchunks} x 1 MiB RS(4,2), host buffers, {steps} calls each"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,149 @@
+/*
+ * storb_ec.h — C ABI of libstorbec.so, the MI355X (gfx950) Reed–Solomon engine
+ * behind storb's chunk-and-shard path.
+ *
+ * Boundary.  In the reference the path crosses into native code at zfec's
+ * CPython extension:
+ *   zfec.easyfec.Encoder(k, m).encode(chunk)         /root/reference/storb/util/piece.py:129-130
+ *   zfec.easyfec.Decoder(k, m).decode(b, s, padlen)  /root/reference/storb/util/piece.py:196-197
+ * (zfec 1.6.0.0, /root/reference/uv.lock:1088-1091; import at piece.py:8).
+ * This header replaces that extension with plain C entry points (no torch or
+ * HIP types in any signature) that a ctypes / cffi / cgo binding can bind
+ * directly; storb_amd/_lib.py is the ctypes binding, INTEGRATION.md shows it.
+ *
+ * Conventions (zfec's, kept on purpose):
+ *   k = data blocks, m = TOTAL blocks (data + parity), 1 <= k <= m <= 256
+ *   B = ceil(n / k) bytes per block; padlen = k*B - n; the last data block
+ *   is zero-padded to B (easyfec).  Block numbers 0..k-1 are primaries
+ *   (systematic: the chunk bytes themselves), k..m-1 are secondaries.
+ *
+ * Ownership.  The caller owns every buffer passed in; the library never frees
+ * caller memory.  Device scratch, coefficient tables, pinned staging and
+ * streams belong to the sec_ctx and are reused across calls.
+ *
+ * Threading.  One sec_ctx per (device, host thread).  Calls on different
+ * contexts are independent; a context must not be used from two threads at
+ * once.
+ *
+ * Errors.  Every int-returning function returns SEC_OK (0) or a negative
+ * SEC_E* code; sec_strerror() names it.  The zfec preconditions map as
+ * follows (zfec raises zfec.Error for each; storb_amd.easyfec raises
+ * storb_amd.easyfec.Error with the same message text).
+ */
+#ifndef STORB_EC_H
+#define STORB_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SEC_ABI_VERSION 1
+
+enum sec_status {
+    SEC_OK = 0,
+    SEC_EINVAL = -1,     /* NULL pointer / negative count / bad flag                  */
+    SEC_EKM = -2,        /* 1 <= k <= m <= 256 violated (zfec Encoder/Decoder init)    */
+    SEC_EBLOCKLEN = -3,  /* blocks not all the same length (easyfec short middle slice) */
+    SEC_ENBLOCKS = -4,   /* decode given other than exactly k blocks                   */
+    SEC_ESHARENUM = -5,  /* sharenum < 0 or >= m                                       */
+    SEC_EDUPSHARE = -6,  /* duplicate sharenum                                         */
+    SEC_EPADLEN = -7,    /* padlen > k*B                                               */
+    SEC_ESIZE = -8,      /* block size B >= 2^31 bytes                                 */
+    SEC_ENODEV = -9,     /* no HIP device / bad device ordinal                         */
+    SEC_EHIP = -10,      /* HIP runtime error; sec_last_hip_error() has the text       */
+    SEC_ENOMEM = -11,    /* device / pinned allocation failed                          */
+    SEC_ESINGULAR = -12  /* decode matrix singular (cannot happen for valid inputs)    */
+};
+
+/* flags for sec_encode_batch / sec_decode_batch */
+#define SEC_F_HOST 1u  /* in/out/blocks are HOST pointers; the library stages through
+                          pinned buffers and device scratch and returns when the
+                          results are back in host memory                            */
+#define SEC_F_ASYNC 2u /* device pointers only: return once enqueued on the context
+                          stream (sec_sync() waits)                                  */
+
+typedef struct sec_ctx sec_ctx;
+
+/* One chunk to encode: the easyfec.Encoder(k, m).encode(chunk) of piece.py:129-130. */
+typedef struct sec_enc_chunk {
+    uint64_t in_off;        /* byte offset of the chunk in `in`                       */
+    uint64_t n;             /* chunk bytes (EncodedChunk.original_chunk_size)         */
+    uint64_t parity_off;    /* byte offset in `parity` of block k (first secondary)   */
+    uint64_t parity_stride; /* bytes from one secondary block to the next (>= B)      */
+    int32_t k;              /* data blocks                                            */
+    int32_t m;              /* total blocks                                           */
+} sec_enc_chunk;
+
+/* One chunk to reassemble: the easyfec.Decoder(k, m).decode(blocks, sharenums,
+ * padlen) of piece.py:196-197.  The chunk's k blocks are entries
+ * slot0 .. slot0+k-1 of the call's sharenums[] / block_offs[] arrays. */
+typedef struct sec_dec_chunk {
+    uint64_t out_off; /* byte offset in `out` of the k*B - padlen reassembled bytes    */
+    uint64_t B;       /* block size (EncodedChunk.chunk_size)                          */
+    uint64_t padlen;  /* EncodedChunk.padlen                                           */
+    uint64_t slot0;   /* first index into sharenums[] / block_offs[]                   */
+    int32_t k;
+    int32_t m;
+} sec_dec_chunk;
+
+/* ---- library / device ------------------------------------------------- */
+int sec_abi_version(void);
+const char *sec_strerror(int status);
+const char *sec_last_hip_error(void);          /* thread-local text of the last SEC_EHIP */
+int sec_device_count(int *count);              /* SEC_ENODEV when the HIP runtime has none */
+
+/* ---- context ------------------------------------------------------------ */
+int sec_ctx_create(int device, sec_ctx **out);
+void sec_ctx_destroy(sec_ctx *ctx);
+/* Launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int sec_ctx_set_stream(sec_ctx *ctx, void *hip_stream);
+int sec_sync(sec_ctx *ctx);
+/* HIP-event timing of the hot kernels: when enabled every batch call records an
+ * event pair around its encode / decode kernels on the launch stream. */
+int sec_ctx_set_timing(sec_ctx *ctx, int enable);
+/* Waits for recorded pairs, returns the summed milliseconds and launch count of
+ * kind 0 = encode, 1 = decode, and clears them. */
+int sec_timing_collect(sec_ctx *ctx, int kind, double *total_ms, int64_t *launches);
+
+/* ---- matrices (host arithmetic, no device needed) ------------------------ */
+/* Rows k..m-1 of zfec's systematic encode matrix ((m-k)*k bytes, row-major). */
+int sec_encode_matrix(int k, int m, uint8_t *out_rows);
+/* zfec decode matrix for the given k sharenums: slots normalised as
+ * _fecmodule.c does (each primary moved to its own slot), rows built, inverted.
+ * out: k*k bytes of the inverse; out_index (nullable): k normalised sharenums. */
+int sec_decode_matrix(int k, int m, const int32_t *sharenums, uint8_t *out, int32_t *out_index);
+
+/* ---- the hot path ----------------------------------------------------------
+ * Encode: for every chunk, parity block r (r = k..m-1) is written at
+ * parity + parity_off + (r-k)*parity_stride, B bytes.  Data blocks are not
+ * written: they are the chunk bytes themselves (systematic code); the zero
+ * padding of the last data block is synthesised, never read from `in`.
+ */
+int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
+                     const uint8_t *in, uint8_t *parity, unsigned flags);
+
+/* Decode + reassemble: for every chunk, its k blocks are at
+ * blocks + block_offs[slot0 + i] (B bytes each) with block numbers
+ * sharenums[slot0 + i]; the chunk's k*B - padlen bytes are written at
+ * out + out_off.  Present primaries are copied, missing ones recovered. */
+int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
+                     const int32_t *sharenums, const uint64_t *block_offs,
+                     const uint8_t *blocks, uint8_t *out, unsigned flags);
+
+/* ---- memory helpers for hosts without a device allocator ----------------- */
+int sec_malloc(sec_ctx *ctx, size_t bytes, void **dptr);
+int sec_free(sec_ctx *ctx, void *dptr);
+int sec_host_alloc(sec_ctx *ctx, size_t bytes, void **hptr); /* pinned */
+int sec_host_free(sec_ctx *ctx, void *hptr);
+/* kind: 0 host->device, 1 device->host, 2 device->device; synchronous on the ctx stream */
+int sec_memcpy(sec_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
+int sec_memset(sec_ctx *ctx, void *dptr, int value, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STORB_EC_H */

@@ -1,0 +1,58 @@
+"""Builds libstorbec.so in-tree with hipcc for gfx950 (no JIT cache, no pip install).
+
+The .so lands in storb_amd/lib/ (git-ignored) so it travels with the repo snapshot to the
+GPU box.  A stamp of the source hashes skips rebuilds when nothing changed.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIBDIR, "libstorbec.so")
+INCLUDE = os.path.join(ROOT, "include")
+SOURCES = ["kernels.hip", "api.cpp"]
+HEADERS = ["kernels.hpp", "gf_host.hpp"]
+ARCH = os.environ.get("STORB_EC_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _digest() -> str:
+    h = hashlib.sha256()
+    for name in SOURCES + HEADERS:
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(name.encode() + f.read())
+    with open(os.path.join(INCLUDE, "storb_ec.h"), "rb") as f:
+        h.update(f.read())
+    h.update(ARCH.encode())
+    return h.hexdigest()
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    stamp = LIB + ".stamp"
+    dig = _digest()
+    if not force and os.path.exists(LIB) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == dig:
+                return LIB
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", "-o", tmp]
+    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    with open(stamp, "w") as f:
+        f.write(dig)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

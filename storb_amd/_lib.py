@@ -1,0 +1,112 @@
+"""ctypes binding of libstorbec.so (include/storb_ec.h).
+
+This is the binding a storb maintainer would add in place of ``from zfec.easyfec import
+Decoder, Encoder`` (/root/reference/storb/util/piece.py:8).  It fails loudly: if the
+library is missing or cannot be loaded there is no CPU fallback, the import raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from ._build import LIB
+
+SEC_OK = 0
+SEC_EINVAL = -1
+SEC_EKM = -2
+SEC_EBLOCKLEN = -3
+SEC_ENBLOCKS = -4
+SEC_ESHARENUM = -5
+SEC_EDUPSHARE = -6
+SEC_EPADLEN = -7
+SEC_ESIZE = -8
+SEC_ENODEV = -9
+SEC_EHIP = -10
+SEC_ENOMEM = -11
+SEC_ESINGULAR = -12
+
+SEC_F_HOST = 1
+SEC_F_ASYNC = 2
+
+# zfec precondition failures (raised by zfec as zfec.Error)
+PRECONDITION_CODES = {SEC_EKM, SEC_EBLOCKLEN, SEC_ENBLOCKS, SEC_ESHARENUM, SEC_EDUPSHARE, SEC_EPADLEN, SEC_ESIZE}
+
+
+class sec_enc_chunk(ctypes.Structure):
+    _fields_ = [("in_off", ctypes.c_uint64), ("n", ctypes.c_uint64), ("parity_off", ctypes.c_uint64),
+                ("parity_stride", ctypes.c_uint64), ("k", ctypes.c_int32), ("m", ctypes.c_int32)]
+
+
+class sec_dec_chunk(ctypes.Structure):
+    _fields_ = [("out_off", ctypes.c_uint64), ("B", ctypes.c_uint64), ("padlen", ctypes.c_uint64),
+                ("slot0", ctypes.c_uint64), ("k", ctypes.c_int32), ("m", ctypes.c_int32)]
+
+
+# numpy mirrors of the descriptor structs (same layout: 4 x u64 + 2 x i32 = 40 B)
+ENC_DTYPE = np.dtype([("in_off", "<u8"), ("n", "<u8"), ("parity_off", "<u8"), ("parity_stride", "<u8"),
+                      ("k", "<i4"), ("m", "<i4")], align=True)
+DEC_DTYPE = np.dtype([("out_off", "<u8"), ("B", "<u8"), ("padlen", "<u8"), ("slot0", "<u8"),
+                      ("k", "<i4"), ("m", "<i4")], align=True)
+assert ENC_DTYPE.itemsize == ctypes.sizeof(sec_enc_chunk) == 40
+assert DEC_DTYPE.itemsize == ctypes.sizeof(sec_dec_chunk) == 40
+
+# every symbol include/storb_ec.h declares: name -> (restype, argtypes)
+_vp = ctypes.c_void_p
+_SIGS = {
+    "sec_abi_version": (ctypes.c_int, []),
+    "sec_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "sec_last_hip_error": (ctypes.c_char_p, []),
+    "sec_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "sec_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "sec_ctx_destroy": (None, [_vp]),
+    "sec_ctx_set_stream": (ctypes.c_int, [_vp, _vp]),
+    "sec_sync": (ctypes.c_int, [_vp]),
+    "sec_ctx_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "sec_timing_collect": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(ctypes.c_int64)]),
+    "sec_encode_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp]),
+    "sec_decode_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
+    "sec_encode_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint]),
+    "sec_decode_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_uint]),
+    "sec_malloc": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "sec_free": (ctypes.c_int, [_vp, _vp]),
+    "sec_host_alloc": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "sec_host_free": (ctypes.c_int, [_vp, _vp]),
+    "sec_memcpy": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_int]),
+    "sec_memset": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t]),
+}
+SYMBOLS = tuple(_SIGS)
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libstorbec.so from the package tree; raise if it is absent (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = os.environ.get("STORB_EC_LIB", LIB)
+    if not os.path.exists(path):
+        raise ImportError(
+            f"libstorbec.so not found at {path}: build it with `python -m storb_amd._build` "
+            "(or __graft_entry__.build()); storb_amd has no CPU fallback")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.sec_abi_version() != 1:
+        raise ImportError("libstorbec.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def strerror(code: int) -> str:
+    lib = load()
+    msg = lib.sec_strerror(code).decode()
+    if code == SEC_EHIP:
+        msg += ": " + lib.sec_last_hip_error().decode()
+    return msg

@@ -1,0 +1,1053 @@
+// api.cpp — the C ABI of libstorbec.so (declared in include/storb_ec.h).
+//
+// Replaces zfec's CPython extension on storb's path
+// (/root/reference/storb/util/piece.py:8,129-130,196-197).  Responsibilities:
+//   * validate exactly the preconditions zfec / easyfec enforce, returning
+//     SEC_E* codes the Python layer maps to the same exceptions;
+//   * build the per-batch launch plan (descriptors + tiles) on the host and
+//     cache it, so a caller that repeats a batch shape (the validator's
+//     steady state, bench.py) pays no host work or metadata upload;
+//   * keep the coefficient tables device-resident, expanded on the GPU from
+//     coefficient bytes (encode tables per (k, m), decode tables per erasure
+//     pattern);
+//   * stage host buffers for SEC_F_HOST calls.
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "gf_host.hpp"
+#include "kernels.hpp"
+#include "storb_ec.h"
+
+namespace {
+
+thread_local std::string g_hip_err;
+
+int hip_fail(hipError_t e, const char *what)
+{
+    g_hip_err = std::string(what) + ": " + hipGetErrorString(e);
+    return SEC_EHIP;
+}
+
+#define CK(x)                                   \
+    do {                                        \
+        hipError_t e_ = (x);                    \
+        if (e_ != hipSuccess)                   \
+            return hip_fail(e_, #x);            \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes)
+    {
+        if (bytes <= cap)
+            return SEC_OK;
+        if (p)
+            CK(hipFree(p));
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max(bytes, (size_t)1 << 16);
+        if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
+            return SEC_ENOMEM;
+        }
+        cap = want;
+        return SEC_OK;
+    }
+    void release()
+    {
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T *as(size_t off = 0) const { return reinterpret_cast<T *>((char *)p + off); }
+};
+
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes)
+    {
+        if (bytes <= cap)
+            return SEC_OK;
+        if (p)
+            CK(hipHostFree(p));
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max(bytes, (size_t)1 << 16);
+        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return SEC_ENOMEM;
+        }
+        cap = want;
+        return SEC_OK;
+    }
+    void release()
+    {
+        if (p)
+            (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct Group {
+    int rows, U;
+    bool edge;
+    uint32_t first, count;
+};
+
+// Device-resident GF coefficient tables (5 dwords per coefficient), keyed by
+// matrix identity.  Reset (and generation bumped) when it outgrows its buffer.
+struct TableCache {
+    DevBuf buf;
+    size_t used = 0;  // dwords
+    uint64_t gen = 1;
+    std::map<std::string, uint32_t> index;
+};
+
+struct Plan {
+    std::vector<uint8_t> key;
+    uint64_t gen_enc = 0, gen_dec = 0;
+    std::vector<Group> groups;
+    DevBuf meta;  // device copy of descriptors, tiles, slot arrays
+    size_t off_desc = 0, off_tiles = 0, off_soff = 0, off_srow = 0, off_mrow = 0;
+    // host-mode bookkeeping
+    size_t dev_in_bytes = 0, dev_out_bytes = 0;
+    bool valid = false;
+};
+
+// Picks the u-steps (4 KiB each) a lane covers per tile.  Larger U = more
+// bytes in flight per lane but more registers; SEC_TILE_U overrides.
+int pick_u(uint64_t B, int rows)
+{
+    static int forced = [] {
+        const char *s = getenv("SEC_TILE_U");
+        return s ? atoi(s) : 0;
+    }();
+    if (forced == 1 || forced == 2 || forced == 4)
+        return forced;
+    if (B >= 4 * (uint64_t)sec::kStepBytes * 4 && rows <= 2)
+        return 4;
+    if (B >= 2 * (uint64_t)sec::kStepBytes * 4 && rows <= 4)
+        return 2;
+    return 1;
+}
+
+// Tiles for one chunk: full tiles over [0, valid) in steps of 4 KiB * U,
+// U=1 edge tiles over the rest of [0, B).  `valid` = positions where every
+// block (incl. the zero-padded last data block) is readable in full.
+void add_tiles(std::map<std::tuple<int, int, bool>, std::vector<sec::Tile>> &bins, uint32_t chunk, uint64_t B,
+               int64_t valid, int rows_total)
+{
+    if (B == 0)
+        return;
+    valid = std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)B));
+    const int ngroups = rows_total == 0 ? 1 : (rows_total + sec::kMaxRows - 1) / sec::kMaxRows;
+    for (int g = 0; g < ngroups; ++g) {
+        const int r0 = g * sec::kMaxRows;
+        const int rows = std::min(sec::kMaxRows, rows_total - r0);
+        const int U = pick_u(B, rows);
+        const uint64_t step = (uint64_t)sec::kStepBytes * U;
+        const uint64_t nfull = (uint64_t)valid / step;
+        auto &full = bins[std::make_tuple(rows, U, false)];
+        for (uint64_t i = 0; i < nfull; ++i)
+            full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
+        auto &edge = bins[std::make_tuple(rows, 1, true)];
+        for (uint64_t t0 = nfull * step; t0 < B; t0 += sec::kStepBytes)
+            edge.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
+    }
+}
+
+}  // namespace
+
+struct sec_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t ext = nullptr;
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[2];
+    std::vector<hipEvent_t> ev_pool;
+    PinBuf pin;  // metadata / host-data staging
+    hipEvent_t pin_ev = nullptr;
+    TableCache enc_tabs, dec_tabs;
+    Plan enc_plan, dec_plan;
+    DevBuf d_in, d_out;  // host-mode device copies
+
+    hipStream_t stream() const { return ext ? ext : own; }
+    hipEvent_t ev()
+    {
+        if (!ev_pool.empty()) {
+            hipEvent_t e = ev_pool.back();
+            ev_pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+};
+
+namespace {
+
+int set_dev(const sec_ctx *ctx)
+{
+    CK(hipSetDevice(ctx->device));
+    return SEC_OK;
+}
+
+// Make sure the pinned staging is no longer read by an in-flight copy.
+int pin_wait(sec_ctx *ctx)
+{
+    CK(hipEventSynchronize(ctx->pin_ev));
+    return SEC_OK;
+}
+
+// Adds the tables for one coefficient matrix (ncoef bytes, layout [slot][row])
+// unless present; returns the dword offset in *off.  New coefficients are
+// appended to `upload` with their destination.
+struct PendingExpand {
+    std::vector<uint8_t> coef;
+    uint32_t dst;  // dword offset in the cache buffer
+};
+
+int table_ensure(TableCache &tc, const std::string &key, const std::vector<uint8_t> &coef,
+                 std::vector<PendingExpand> &pending, uint32_t *off)
+{
+    auto it = tc.index.find(key);
+    if (it != tc.index.end()) {
+        *off = it->second;
+        return SEC_OK;
+    }
+    const size_t need = coef.size() * sec::kTabDwords;
+    if ((tc.used + need) * 4 > tc.buf.cap)
+        return 1;  // caller resets the cache and retries
+    *off = (uint32_t)tc.used;
+    tc.index.emplace(key, *off);
+    pending.push_back(PendingExpand{coef, *off});
+    tc.used += need;
+    return SEC_OK;
+}
+
+int table_reset(sec_ctx *ctx, TableCache &tc, size_t need_dwords)
+{
+    CK(hipStreamSynchronize(ctx->stream()));
+    size_t want = std::max<size_t>(tc.buf.cap * 2, std::max<size_t>(need_dwords * 4 * 2, (size_t)1 << 20));
+    tc.buf.release();
+    int rc = tc.buf.ensure(want);
+    if (rc)
+        return rc;
+    tc.used = 0;
+    tc.index.clear();
+    ++tc.gen;
+    return SEC_OK;
+}
+
+// Upload one contiguous metadata image (built in the pinned buffer) into
+// plan.meta and launch the pending table expansions whose coefficient bytes
+// sit at `coef_base` within the image.
+int upload_meta(sec_ctx *ctx, Plan &plan, size_t bytes)
+{
+    int rc = plan.meta.ensure(bytes);
+    if (rc)
+        return rc;
+    CK(hipMemcpyAsync(plan.meta.p, ctx->pin.p, bytes, hipMemcpyHostToDevice, ctx->stream()));
+    CK(hipEventRecord(ctx->pin_ev, ctx->stream()));
+    return SEC_OK;
+}
+
+int launch_expansions(sec_ctx *ctx, TableCache &tc, const Plan &plan, size_t coef_off,
+                      const std::vector<PendingExpand> &pending)
+{
+    size_t o = coef_off;
+    for (const auto &pe : pending) {
+        int e = sec_launch_expand(plan.meta.as<uint8_t>(o), (uint32_t)pe.coef.size(), tc.buf.as<uint32_t>() + pe.dst,
+                                  ctx->stream());
+        if (e)
+            return hip_fail((hipError_t)e, "sec_expand_tables");
+        o += pe.coef.size();
+    }
+    return SEC_OK;
+}
+
+int timing_begin(sec_ctx *ctx, hipEvent_t *a)
+{
+    *a = nullptr;
+    if (!ctx->timing)
+        return SEC_OK;
+    *a = ctx->ev();
+    CK(hipEventRecord(*a, ctx->stream()));
+    return SEC_OK;
+}
+
+int timing_end(sec_ctx *ctx, hipEvent_t a, int kind)
+{
+    if (!a)
+        return SEC_OK;
+    hipEvent_t b = ctx->ev();
+    CK(hipEventRecord(b, ctx->stream()));
+    ctx->pending[kind].emplace_back(a, b);
+    return SEC_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+extern "C" {
+
+int sec_abi_version(void) { return SEC_ABI_VERSION; }
+
+const char *sec_strerror(int s)
+{
+    switch (s) {
+    case SEC_OK: return "ok";
+    case SEC_EINVAL: return "invalid argument";
+    case SEC_EKM: return "Precondition violation: 1 <= k <= m <= 256 required";
+    case SEC_EBLOCKLEN: return "Precondition violation: Input blocks are required to be all the same length.";
+    case SEC_ENBLOCKS: return "Precondition violation: exactly k blocks and k sharenums are required";
+    case SEC_ESHARENUM: return "Precondition violation: sharenum is required to be in [0, m)";
+    case SEC_EDUPSHARE: return "Precondition violation: duplicate sharenum";
+    case SEC_EPADLEN: return "padlen larger than k * blocksize";
+    case SEC_ESIZE: return "block size must be < 2^31 bytes";
+    case SEC_ENODEV: return "no HIP device available";
+    case SEC_EHIP: return "HIP runtime error";
+    case SEC_ENOMEM: return "out of device or pinned memory";
+    case SEC_ESINGULAR: return "decode matrix is singular";
+    default: return "unknown error";
+    }
+}
+
+const char *sec_last_hip_error(void) { return g_hip_err.c_str(); }
+
+int sec_device_count(int *count)
+{
+    if (!count)
+        return SEC_EINVAL;
+    *count = 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return SEC_ENODEV;
+    *count = n;
+    return SEC_OK;
+}
+
+int sec_ctx_create(int device, sec_ctx **out)
+{
+    if (!out)
+        return SEC_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return SEC_ENODEV;
+    sec_ctx *ctx = new sec_ctx();
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&ctx->pin_ev, hipEventDisableTiming);
+    if (e == hipSuccess)
+        e = hipEventRecord(ctx->pin_ev, ctx->own);
+    if (e != hipSuccess) {
+        sec_ctx_destroy(ctx);
+        return hip_fail(e, "sec_ctx_create");
+    }
+    *out = ctx;
+    return SEC_OK;
+}
+
+void sec_ctx_destroy(sec_ctx *ctx)
+{
+    if (!ctx)
+        return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->own)
+        (void)hipStreamSynchronize(ctx->own);
+    if (ctx->ext)
+        (void)hipStreamSynchronize(ctx->ext);
+    for (auto &v : ctx->pending)
+        for (auto &pr : v) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+    for (auto e : ctx->ev_pool)
+        (void)hipEventDestroy(e);
+    if (ctx->pin_ev)
+        (void)hipEventDestroy(ctx->pin_ev);
+    ctx->pin.release();
+    ctx->enc_tabs.buf.release();
+    ctx->dec_tabs.buf.release();
+    ctx->enc_plan.meta.release();
+    ctx->dec_plan.meta.release();
+    ctx->d_in.release();
+    ctx->d_out.release();
+    if (ctx->own)
+        (void)hipStreamDestroy(ctx->own);
+    delete ctx;
+}
+
+int sec_ctx_set_stream(sec_ctx *ctx, void *stream)
+{
+    if (!ctx)
+        return SEC_EINVAL;
+    int rc = set_dev(ctx);
+    if (rc)
+        return rc;
+    // order the switch: work queued so far completes before the new stream runs
+    CK(hipStreamSynchronize(ctx->stream()));
+    ctx->ext = (hipStream_t)stream;
+    CK(hipEventRecord(ctx->pin_ev, ctx->stream()));
+    return SEC_OK;
+}
+
+int sec_sync(sec_ctx *ctx)
+{
+    if (!ctx)
+        return SEC_EINVAL;
+    int rc = set_dev(ctx);
+    if (rc)
+        return rc;
+    CK(hipStreamSynchronize(ctx->stream()));
+    return SEC_OK;
+}
+
+int sec_ctx_set_timing(sec_ctx *ctx, int enable)
+{
+    if (!ctx)
+        return SEC_EINVAL;
+    ctx->timing = enable != 0;
+    return SEC_OK;
+}
+
+int sec_timing_collect(sec_ctx *ctx, int kind, double *total_ms, int64_t *launches)
+{
+    if (!ctx || kind < 0 || kind > 1 || !total_ms || !launches)
+        return SEC_EINVAL;
+    int rc = set_dev(ctx);
+    if (rc)
+        return rc;
+    double tot = 0;
+    for (auto &pr : ctx->pending[kind]) {
+        CK(hipEventSynchronize(pr.second));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, pr.first, pr.second));
+        tot += ms;
+        ctx->ev_pool.push_back(pr.first);
+        ctx->ev_pool.push_back(pr.second);
+    }
+    *launches = (int64_t)ctx->pending[kind].size();
+    *total_ms = tot;
+    ctx->pending[kind].clear();
+    return SEC_OK;
+}
+
+int sec_encode_matrix(int k, int m, uint8_t *out)
+{
+    if (!out)
+        return SEC_EINVAL;
+    if (k < 1 || m < k || m > 256)
+        return SEC_EKM;
+    std::vector<uint8_t> enc = sec::encode_matrix(k, m);
+    memcpy(out, enc.data() + (size_t)k * k, (size_t)(m - k) * k);
+    return SEC_OK;
+}
+
+static int check_sharenums(int k, int m, const int32_t *s)
+{
+    bool seen[256] = {false};
+    for (int i = 0; i < k; ++i) {
+        if (s[i] < 0 || s[i] >= m)
+            return SEC_ESHARENUM;
+        if (seen[s[i]])
+            return SEC_EDUPSHARE;
+        seen[s[i]] = true;
+    }
+    return SEC_OK;
+}
+
+int sec_decode_matrix(int k, int m, const int32_t *sharenums, uint8_t *out, int32_t *out_index)
+{
+    if (!sharenums || !out)
+        return SEC_EINVAL;
+    if (k < 1 || m < k || m > 256)
+        return SEC_EKM;
+    int rc = check_sharenums(k, m, sharenums);
+    if (rc)
+        return rc;
+    std::vector<int> idx(sharenums, sharenums + k), perm;
+    sec::normalise_slots(k, idx, perm);
+    std::vector<uint8_t> minv;
+    if (!sec::decode_matrix(k, m, idx, minv))
+        return SEC_ESINGULAR;
+    memcpy(out, minv.data(), (size_t)k * k);
+    if (out_index)
+        for (int i = 0; i < k; ++i)
+            out_index[i] = idx[i];
+    return SEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
+                     uint8_t *parity, unsigned flags)
+{
+    if (!ctx || nchunks < 0 || (nchunks > 0 && !chunks) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC)))
+        return SEC_EINVAL;
+    if (nchunks == 0)
+        return SEC_OK;
+    if (nchunks >= (int64_t)UINT32_MAX)
+        return SEC_EINVAL;
+    const bool host = flags & SEC_F_HOST;
+    int rc = set_dev(ctx);
+    if (rc)
+        return rc;
+
+    // ---- validate (easyfec.Encoder.encode / _fec.Encoder preconditions) ----
+    uint64_t in_dense = 0, total_par = 0;
+    for (int64_t i = 0; i < nchunks; ++i) {
+        const sec_enc_chunk &c = chunks[i];
+        if (c.k < 1 || c.m < c.k || c.m > 256)
+            return SEC_EKM;
+        const uint64_t B = (c.n + c.k - 1) / c.k;
+        if (c.k > 1 && (uint64_t)(c.k - 1) * B > c.n)
+            return SEC_EBLOCKLEN;
+        if (B >= (1ull << 31))
+            return SEC_ESIZE;
+        const uint64_t p = (uint64_t)(c.m - c.k);
+        if (p > 0 && B > 0 && c.parity_stride < B)
+            return SEC_EINVAL;
+        in_dense += c.n;
+        total_par += p * B;
+    }
+    if (total_par == 0)
+        return SEC_OK;  // nothing to compute (m == k, or empty chunks)
+    if ((!in && !host) || !parity)
+        return SEC_EINVAL;
+
+    Plan &plan = ctx->enc_plan;
+    std::vector<uint8_t> key(sizeof(sec_enc_chunk) * (size_t)nchunks + sizeof(unsigned));
+    memcpy(key.data(), chunks, sizeof(sec_enc_chunk) * (size_t)nchunks);
+    memcpy(key.data() + sizeof(sec_enc_chunk) * (size_t)nchunks, &flags, sizeof(unsigned));
+    const bool reuse = plan.valid && plan.gen_enc == ctx->enc_tabs.gen && plan.key == key;
+
+    if (!reuse) {
+        plan.valid = false;
+        // tables for every distinct (k, m)
+        std::vector<PendingExpand> pending;
+        std::vector<uint32_t> tab_of((size_t)nchunks, 0);
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            pending.clear();
+            size_t need = 0;
+            bool overflow = false;
+            std::map<std::pair<int, int>, uint32_t> local;
+            for (int64_t i = 0; i < nchunks && !overflow; ++i) {
+                const int k = chunks[i].k, m = chunks[i].m;
+                if (m == k)
+                    continue;
+                auto lk = local.find({k, m});
+                if (lk != local.end()) {
+                    tab_of[i] = lk->second;
+                    continue;
+                }
+                std::vector<uint8_t> enc = sec::encode_matrix(k, m);
+                const int p = m - k;
+                std::vector<uint8_t> coef((size_t)k * p);
+                for (int j = 0; j < k; ++j)
+                    for (int r = 0; r < p; ++r)
+                        coef[(size_t)j * p + r] = enc[(size_t)(k + r) * k + j];
+                need += coef.size() * sec::kTabDwords;
+                uint32_t off = 0;
+                const std::string tk = std::to_string(k) + "/" + std::to_string(m);
+                int st = table_ensure(ctx->enc_tabs, tk, coef, pending, &off);
+                if (st == 1) {
+                    overflow = true;
+                    break;
+                }
+                local[{k, m}] = off;
+                tab_of[i] = off;
+            }
+            if (!overflow)
+                break;
+            if (attempt == 1)
+                return SEC_ENOMEM;
+            rc = table_reset(ctx, ctx->enc_tabs, need);
+            if (rc)
+                return rc;
+        }
+
+        // descriptors + tiles
+        std::vector<sec::EncDesc> descs((size_t)nchunks);
+        std::map<std::tuple<int, int, bool>, std::vector<sec::Tile>> bins;
+        uint64_t dense = 0, idense = 0;
+        for (int64_t i = 0; i < nchunks; ++i) {
+            const sec_enc_chunk &c = chunks[i];
+            const uint64_t B = (c.n + c.k - 1) / c.k;
+            const int p = c.m - c.k;
+            sec::EncDesc &d = descs[i];
+            d.in_off = host ? idense : c.in_off;
+            idense += c.n;
+            d.par_off = host ? dense : c.parity_off;
+            d.par_stride = host ? B : c.parity_stride;
+            d.n = c.n;
+            d.B = (uint32_t)B;
+            d.k = (uint32_t)c.k;
+            d.p = (uint32_t)p;
+            d.tab = tab_of[i];
+            dense += (uint64_t)p * B;
+            if (p > 0)
+                add_tiles(bins, (uint32_t)i, B, (int64_t)c.n - (int64_t)(c.k - 1) * (int64_t)B, p);
+        }
+        plan.groups.clear();
+        std::vector<sec::Tile> tiles;
+        for (auto &kv : bins) {
+            if (kv.second.empty())
+                continue;
+            plan.groups.push_back(Group{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first),
+                                        (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
+            tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
+        }
+        // metadata image: [descs][tiles][coefs]
+        size_t coef_bytes = 0;
+        for (auto &pe : pending)
+            coef_bytes += pe.coef.size();
+        plan.off_desc = 0;
+        plan.off_tiles = align_up(descs.size() * sizeof(sec::EncDesc), 256);
+        const size_t off_coef = align_up(plan.off_tiles + tiles.size() * sizeof(sec::Tile), 256);
+        const size_t bytes = off_coef + coef_bytes;
+        rc = pin_wait(ctx);
+        if (!rc)
+            rc = ctx->pin.ensure(bytes);
+        if (rc)
+            return rc;
+        char *img = (char *)ctx->pin.p;
+        memcpy(img + plan.off_desc, descs.data(), descs.size() * sizeof(sec::EncDesc));
+        memcpy(img + plan.off_tiles, tiles.data(), tiles.size() * sizeof(sec::Tile));
+        size_t o = off_coef;
+        for (auto &pe : pending) {
+            memcpy(img + o, pe.coef.data(), pe.coef.size());
+            o += pe.coef.size();
+        }
+        rc = upload_meta(ctx, plan, bytes);
+        if (!rc)
+            rc = launch_expansions(ctx, ctx->enc_tabs, plan, off_coef, pending);
+        if (rc)
+            return rc;
+        plan.key.swap(key);
+        plan.gen_enc = ctx->enc_tabs.gen;
+        plan.dev_in_bytes = in_dense;
+        plan.dev_out_bytes = dense;
+        plan.valid = true;
+    }
+
+    // ---- data movement (host mode) ----
+    const uint8_t *d_in = in;
+    uint8_t *d_par = parity;
+    if (host) {
+        // gather every chunk (arbitrary host addresses) into pinned staging, one H2D
+        rc = ctx->d_in.ensure(plan.dev_in_bytes);
+        if (!rc)
+            rc = ctx->d_out.ensure(plan.dev_out_bytes);
+        if (!rc)
+            rc = pin_wait(ctx);
+        if (!rc)
+            rc = ctx->pin.ensure(plan.dev_in_bytes);
+        if (rc)
+            return rc;
+        char *stage = (char *)ctx->pin.p;
+        uint64_t o = 0;
+        for (int64_t i = 0; i < nchunks; ++i) {
+            memcpy(stage + o, in + chunks[i].in_off, chunks[i].n);
+            o += chunks[i].n;
+        }
+        CK(hipMemcpyAsync(ctx->d_in.p, stage, plan.dev_in_bytes, hipMemcpyHostToDevice, ctx->stream()));
+        CK(hipEventRecord(ctx->pin_ev, ctx->stream()));
+        d_in = ctx->d_in.as<uint8_t>();
+        d_par = ctx->d_out.as<uint8_t>();
+    }
+
+    // ---- launches ----
+    hipEvent_t t0 = nullptr;
+    rc = timing_begin(ctx, &t0);
+    if (rc)
+        return rc;
+    const sec::EncDesc *dd = plan.meta.as<sec::EncDesc>(plan.off_desc);
+    const sec::Tile *dt = plan.meta.as<sec::Tile>(plan.off_tiles);
+    for (const Group &g : plan.groups) {
+        int e = sec_launch_encode(g.rows, g.U, g.edge, d_in, d_par, dd, dt + g.first, g.count,
+                                  ctx->enc_tabs.buf.as<uint32_t>(), ctx->stream());
+        if (e)
+            return hip_fail((hipError_t)e, "sec_encode_kernel");
+    }
+    rc = timing_end(ctx, t0, 0);
+    if (rc)
+        return rc;
+
+    if (host) {
+        uint64_t dense = 0;
+        for (int64_t i = 0; i < nchunks; ++i) {
+            const sec_enc_chunk &c = chunks[i];
+            const uint64_t B = (c.n + c.k - 1) / c.k;
+            const uint64_t p = (uint64_t)(c.m - c.k);
+            if (p == 0 || B == 0)
+                continue;
+            CK(hipMemcpy2DAsync(parity + c.parity_off, c.parity_stride, d_par + dense, B, B, p,
+                                hipMemcpyDeviceToHost, ctx->stream()));
+            dense += p * B;
+        }
+        CK(hipStreamSynchronize(ctx->stream()));
+    } else if (!(flags & SEC_F_ASYNC)) {
+        CK(hipStreamSynchronize(ctx->stream()));
+    }
+    return SEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const int32_t *sharenums,
+                     const uint64_t *block_offs, const uint8_t *blocks, uint8_t *out, unsigned flags)
+{
+    if (!ctx || nchunks < 0 || (nchunks > 0 && (!chunks || !sharenums || !block_offs)) ||
+        (flags & ~(SEC_F_HOST | SEC_F_ASYNC)))
+        return SEC_EINVAL;
+    if (nchunks == 0)
+        return SEC_OK;
+    if (nchunks >= (int64_t)UINT32_MAX)
+        return SEC_EINVAL;
+    const bool host = flags & SEC_F_HOST;
+    int rc = set_dev(ctx);
+    if (rc)
+        return rc;
+
+    // ---- validate (_fec.Decoder.decode / easyfec.Decoder.decode) ----
+    uint64_t total_slots = 0, total_out = 0;
+    for (int64_t i = 0; i < nchunks; ++i) {
+        const sec_dec_chunk &c = chunks[i];
+        if (c.k < 1 || c.m < c.k || c.m > 256)
+            return SEC_EKM;
+        if (c.B >= (1ull << 31))
+            return SEC_ESIZE;
+        if (c.padlen > (uint64_t)c.k * c.B)
+            return SEC_EPADLEN;
+        rc = check_sharenums(c.k, c.m, sharenums + c.slot0);
+        if (rc)
+            return rc;
+        total_slots = std::max<uint64_t>(total_slots, c.slot0 + (uint64_t)c.k);
+        total_out += (uint64_t)c.k * c.B - c.padlen;
+    }
+    if (total_out == 0)
+        return SEC_OK;
+    if (!out || (!blocks && !host))
+        return SEC_EINVAL;
+
+    Plan &plan = ctx->dec_plan;
+    const size_t kc = sizeof(sec_dec_chunk) * (size_t)nchunks;
+    std::vector<uint8_t> key(kc + total_slots * (4 + 8) + sizeof(unsigned) + sizeof(void *));
+    {
+        size_t o = 0;
+        memcpy(key.data() + o, chunks, kc);
+        o += kc;
+        memcpy(key.data() + o, sharenums, total_slots * 4);
+        o += total_slots * 4;
+        memcpy(key.data() + o, block_offs, total_slots * 8);
+        o += total_slots * 8;
+        memcpy(key.data() + o, &flags, sizeof(unsigned));
+        o += sizeof(unsigned);
+        const void *b = host ? (const void *)blocks : nullptr;
+        memcpy(key.data() + o, &b, sizeof(void *));
+    }
+    const bool reuse = plan.valid && plan.gen_dec == ctx->dec_tabs.gen && plan.key == key;
+
+    // normalised slot order per chunk (needed for host gather even on reuse)
+    std::vector<int> perm_all;  // caller position for each normalised slot
+    std::vector<int> idx_all;
+    perm_all.reserve((size_t)nchunks * 4);
+    std::vector<uint64_t> chunk_slot((size_t)nchunks);
+    {
+        std::vector<int> idx, perm;
+        for (int64_t i = 0; i < nchunks; ++i) {
+            const sec_dec_chunk &c = chunks[i];
+            idx.assign(sharenums + c.slot0, sharenums + c.slot0 + c.k);
+            sec::normalise_slots(c.k, idx, perm);
+            chunk_slot[i] = perm_all.size();
+            perm_all.insert(perm_all.end(), perm.begin(), perm.end());
+            idx_all.insert(idx_all.end(), idx.begin(), idx.end());
+        }
+    }
+
+    if (!reuse) {
+        plan.valid = false;
+        std::vector<PendingExpand> pending;
+        std::vector<uint32_t> tab_of((size_t)nchunks, 0), e_of((size_t)nchunks, 0);
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            pending.clear();
+            size_t need = 0;
+            bool overflow = false;
+            for (int64_t i = 0; i < nchunks && !overflow; ++i) {
+                const sec_dec_chunk &c = chunks[i];
+                const int k = c.k;
+                const int *idx = &idx_all[chunk_slot[i]];
+                std::vector<int> miss;
+                for (int s = 0; s < k; ++s)
+                    if (idx[s] >= k)
+                        miss.push_back(s);
+                e_of[i] = (uint32_t)miss.size();
+                if (miss.empty())
+                    continue;
+                std::string tk = std::to_string(k) + "/" + std::to_string(c.m) + ":";
+                for (int s = 0; s < k; ++s)
+                    tk += std::to_string(idx[s]) + ",";
+                auto it = ctx->dec_tabs.index.find(tk);
+                if (it != ctx->dec_tabs.index.end()) {
+                    tab_of[i] = it->second;
+                    continue;
+                }
+                std::vector<int> iv(idx, idx + k);
+                std::vector<uint8_t> minv;
+                if (!sec::decode_matrix(k, c.m, iv, minv))
+                    return SEC_ESINGULAR;
+                const int e = (int)miss.size();
+                std::vector<uint8_t> coef((size_t)k * e);
+                for (int s = 0; s < k; ++s)
+                    for (int r = 0; r < e; ++r)
+                        coef[(size_t)s * e + r] = minv[(size_t)miss[r] * k + s];
+                need += coef.size() * sec::kTabDwords;
+                uint32_t off = 0;
+                if (table_ensure(ctx->dec_tabs, tk, coef, pending, &off) == 1) {
+                    overflow = true;
+                    break;
+                }
+                tab_of[i] = off;
+            }
+            if (!overflow)
+                break;
+            if (attempt == 1)
+                return SEC_ENOMEM;
+            rc = table_reset(ctx, ctx->dec_tabs, need * 2 + ((size_t)1 << 18));
+            if (rc)
+                return rc;
+        }
+
+        std::vector<sec::DecDesc> descs((size_t)nchunks);
+        std::vector<uint64_t> soff(perm_all.size());
+        std::vector<uint32_t> srow(perm_all.size()), mrow(perm_all.size(), 0);
+        std::map<std::tuple<int, int, bool>, std::vector<sec::Tile>> bins;
+        uint64_t in_dense = 0, out_dense = 0;
+        for (int64_t i = 0; i < nchunks; ++i) {
+            const sec_dec_chunk &c = chunks[i];
+            const uint64_t base = chunk_slot[i];
+            const int *idx = &idx_all[base];
+            uint32_t nm = 0;
+            for (int s = 0; s < c.k; ++s) {
+                const int from = perm_all[base + s];
+                soff[base + s] = host ? in_dense + (uint64_t)s * c.B : block_offs[c.slot0 + from];
+                srow[base + s] = idx[s] < c.k ? (uint32_t)idx[s] : 0xFFFFFFFFu;
+                if (idx[s] >= c.k)
+                    mrow[base + nm++] = (uint32_t)s;
+            }
+            const uint64_t nout = (uint64_t)c.k * c.B - c.padlen;
+            sec::DecDesc &d = descs[i];
+            d.out_off = host ? out_dense : c.out_off;
+            d.n = nout;
+            d.B = (uint32_t)c.B;
+            d.k = (uint32_t)c.k;
+            d.e = e_of[i];
+            d.tab = tab_of[i];
+            d.slot0 = (uint32_t)base;
+            d.pad = 0;
+            in_dense += (uint64_t)c.k * c.B;
+            out_dense += nout;
+            if (nout > 0)
+                add_tiles(bins, (uint32_t)i, c.B, (int64_t)nout - (int64_t)(c.k - 1) * (int64_t)c.B, (int)e_of[i]);
+        }
+        plan.groups.clear();
+        std::vector<sec::Tile> tiles;
+        for (auto &kv : bins) {
+            if (kv.second.empty())
+                continue;
+            plan.groups.push_back(Group{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first),
+                                        (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
+            tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
+        }
+        size_t coef_bytes = 0;
+        for (auto &pe : pending)
+            coef_bytes += pe.coef.size();
+        plan.off_desc = 0;
+        plan.off_tiles = align_up(descs.size() * sizeof(sec::DecDesc), 256);
+        plan.off_soff = align_up(plan.off_tiles + tiles.size() * sizeof(sec::Tile), 256);
+        plan.off_srow = align_up(plan.off_soff + soff.size() * 8, 256);
+        plan.off_mrow = align_up(plan.off_srow + srow.size() * 4, 256);
+        const size_t off_coef = align_up(plan.off_mrow + mrow.size() * 4, 256);
+        const size_t bytes = off_coef + coef_bytes;
+        rc = pin_wait(ctx);
+        if (!rc)
+            rc = ctx->pin.ensure(bytes);
+        if (rc)
+            return rc;
+        char *img = (char *)ctx->pin.p;
+        memcpy(img + plan.off_desc, descs.data(), descs.size() * sizeof(sec::DecDesc));
+        memcpy(img + plan.off_tiles, tiles.data(), tiles.size() * sizeof(sec::Tile));
+        memcpy(img + plan.off_soff, soff.data(), soff.size() * 8);
+        memcpy(img + plan.off_srow, srow.data(), srow.size() * 4);
+        memcpy(img + plan.off_mrow, mrow.data(), mrow.size() * 4);
+        size_t o = off_coef;
+        for (auto &pe : pending) {
+            memcpy(img + o, pe.coef.data(), pe.coef.size());
+            o += pe.coef.size();
+        }
+        rc = upload_meta(ctx, plan, bytes);
+        if (!rc)
+            rc = launch_expansions(ctx, ctx->dec_tabs, plan, off_coef, pending);
+        if (rc)
+            return rc;
+        plan.key.swap(key);
+        plan.gen_dec = ctx->dec_tabs.gen;
+        plan.dev_in_bytes = in_dense;
+        plan.dev_out_bytes = out_dense;
+        plan.valid = true;
+    }
+
+    // ---- data movement (host mode): gather blocks in normalised slot order ----
+    const uint8_t *d_blocks = blocks;
+    uint8_t *d_out = out;
+    if (host) {
+        rc = ctx->d_in.ensure(plan.dev_in_bytes);
+        if (!rc)
+            rc = ctx->d_out.ensure(plan.dev_out_bytes);
+        if (!rc)
+            rc = pin_wait(ctx);
+        if (!rc)
+            rc = ctx->pin.ensure(plan.dev_in_bytes);
+        if (rc)
+            return rc;
+        char *stage = (char *)ctx->pin.p;
+        uint64_t o = 0;
+        for (int64_t i = 0; i < nchunks; ++i) {
+            const sec_dec_chunk &c = chunks[i];
+            for (int s = 0; s < c.k; ++s) {
+                const int from = perm_all[chunk_slot[i] + s];
+                memcpy(stage + o, blocks + block_offs[c.slot0 + from], c.B);
+                o += c.B;
+            }
+        }
+        CK(hipMemcpyAsync(ctx->d_in.p, stage, plan.dev_in_bytes, hipMemcpyHostToDevice, ctx->stream()));
+        CK(hipEventRecord(ctx->pin_ev, ctx->stream()));
+        d_blocks = ctx->d_in.as<uint8_t>();
+        d_out = ctx->d_out.as<uint8_t>();
+    }
+
+    hipEvent_t t0 = nullptr;
+    rc = timing_begin(ctx, &t0);
+    if (rc)
+        return rc;
+    const sec::DecDesc *dd = plan.meta.as<sec::DecDesc>(plan.off_desc);
+    const sec::Tile *dt = plan.meta.as<sec::Tile>(plan.off_tiles);
+    for (const Group &g : plan.groups) {
+        int e = sec_launch_decode(g.rows, g.U, g.edge, d_blocks, d_out, dd, dt + g.first, g.count,
+                                  ctx->dec_tabs.buf.as<uint32_t>(), plan.meta.as<uint64_t>(plan.off_soff),
+                                  plan.meta.as<uint32_t>(plan.off_srow), plan.meta.as<uint32_t>(plan.off_mrow),
+                                  ctx->stream());
+        if (e)
+            return hip_fail((hipError_t)e, "sec_decode_kernel");
+    }
+    rc = timing_end(ctx, t0, 1);
+    if (rc)
+        return rc;
+
+    if (host) {
+        uint64_t dense = 0;
+        for (int64_t i = 0; i < nchunks; ++i) {
+            const sec_dec_chunk &c = chunks[i];
+            const uint64_t nout = (uint64_t)c.k * c.B - c.padlen;
+            if (nout)
+                CK(hipMemcpyAsync(out + c.out_off, d_out + dense, nout, hipMemcpyDeviceToHost, ctx->stream()));
+            dense += nout;
+        }
+        CK(hipStreamSynchronize(ctx->stream()));
+    } else if (!(flags & SEC_F_ASYNC)) {
+        CK(hipStreamSynchronize(ctx->stream()));
+    }
+    return SEC_OK;
+}
+
+// ---------------------------------------------------------------------------
+int sec_malloc(sec_ctx *ctx, size_t bytes, void **dptr)
+{
+    if (!ctx || !dptr)
+        return SEC_EINVAL;
+    int rc = set_dev(ctx);
+    if (rc)
+        return rc;
+    if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess)
+        return SEC_ENOMEM;
+    return SEC_OK;
+}
+
+int sec_free(sec_ctx *ctx, void *dptr)
+{
+    if (!ctx)
+        return SEC_EINVAL;
+    int rc = set_dev(ctx);
+    if (rc)
+        return rc;
+    CK(hipFree(dptr));
+    return SEC_OK;
+}
+
+int sec_host_alloc(sec_ctx *ctx, size_t bytes, void **hptr)
+{
+    if (!ctx || !hptr)
+        return SEC_EINVAL;
+    int rc = set_dev(ctx);
+    if (rc)
+        return rc;
+    if (hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
+        return SEC_ENOMEM;
+    return SEC_OK;
+}
+
+int sec_host_free(sec_ctx *ctx, void *hptr)
+{
+    if (!ctx)
+        return SEC_EINVAL;
+    CK(hipHostFree(hptr));
+    return SEC_OK;
+}
+
+int sec_memcpy(sec_ctx *ctx, void *dst, const void *src, size_t bytes, int kind)
+{
+    if (!ctx || (bytes && (!dst || !src)) || kind < 0 || kind > 2)
+        return SEC_EINVAL;
+    int rc = set_dev(ctx);
+    if (rc)
+        return rc;
+    static const hipMemcpyKind kinds[3] = {hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice};
+    if (bytes) {
+        CK(hipMemcpyAsync(dst, src, bytes, kinds[kind], ctx->stream()));
+        CK(hipStreamSynchronize(ctx->stream()));
+    }
+    return SEC_OK;
+}
+
+int sec_memset(sec_ctx *ctx, void *dptr, int value, size_t bytes)
+{
+    if (!ctx || (bytes && !dptr))
+        return SEC_EINVAL;
+    int rc = set_dev(ctx);
+    if (rc)
+        return rc;
+    if (bytes) {
+        CK(hipMemsetAsync(dptr, value, bytes, ctx->stream()));
+        CK(hipStreamSynchronize(ctx->stream()));
+    }
+    return SEC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,371 @@
+// kernels.hip — CDNA4 (gfx950) kernels for GF(2^8) Reed–Solomon encode / decode.
+//
+// What they compute is zfec's fec_encode / fec_decode (restated in
+// oracle/fec_oracle.c; called from /root/reference/storb/util/piece.py:129-130
+// and :196-197 through zfec.easyfec):
+//     out_r[t] = XOR_j  c_rj * in_j[t]        over GF(2^8) / 0x11D
+//
+// How.  The work is byte-wise and HBM-bound (a few VALU ops per byte, no
+// matrix shape), so there is no MFMA and no LDS in the hot loop:
+//   * multiplication by a constant c is GF(2)-linear in the byte x, so with
+//     x = lo3 | mid3 << 3 | hi2 << 6
+//         c*x = c*lo3  ^  c*(mid3 << 3)  ^  c*(hi2 << 6)
+//     and each term is an 8- (or 4-) entry byte table: exactly what one
+//     v_perm_b32 looks up for 4 bytes at once (its 8-byte source = the table,
+//     its selector = the 3-bit fields).  So one coefficient costs 3 v_perm +
+//     2 XOR per dword, and the 3 selectors of an input dword are shared by all
+//     output rows.  The tables (5 dwords per coefficient) are wave-uniform and
+//     arrive through scalar loads.
+//   * the tables themselves are expanded on the device from the coefficient
+//     bytes by sec_expand_tables, which stages the GF(2^8) exp/log tables in
+//     LDS and forms every product as exp[log c + log v].
+//   * each lane streams 16 B (global_load_dwordx4) per block per u-step, so a
+//     wave reads one coalesced 1 KiB run from each of the k blocks; block
+//     starts that are not 16 B aligned (B % 16 != 0) use the hardware's
+//     unaligned dwordx4 access; the last data block's zero padding is
+//     synthesised for the few edge lanes, never read.
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+
+using u8 = uint8_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_u __attribute__((aligned(1)));  // byte-aligned 16 B access
+
+namespace {
+
+struct GfTables {
+    u8 exp[512];
+    u8 log[256];
+};
+
+constexpr GfTables make_gf()
+{
+    GfTables t{};
+    u32 v = 1;
+    for (int e = 0; e < 255; ++e) {
+        t.exp[e] = (u8)v;
+        t.exp[e + 255] = (u8)v;
+        t.log[v] = (u8)e;
+        v <<= 1;
+        if (v & 0x100)
+            v ^= 0x11D;
+    }
+    t.exp[510] = t.exp[0];
+    t.exp[511] = t.exp[1];
+    t.log[0] = 255;  // sentinel; products with 0 are special-cased
+    return t;
+}
+
+__constant__ GfTables c_gf = make_gf();
+
+// ---- table expansion: coefficient byte -> 5 v_perm tables ---------------
+__global__ __launch_bounds__(256) void sec_expand_tables(const u8 *__restrict__ coef, u32 ncoef,
+                                                         u32 *__restrict__ tabs)
+{
+    __shared__ u8 s_exp[512];
+    __shared__ u8 s_log[256];
+    for (u32 i = threadIdx.x; i < 512; i += blockDim.x)
+        s_exp[i] = c_gf.exp[i];
+    for (u32 i = threadIdx.x; i < 256; i += blockDim.x)
+        s_log[i] = c_gf.log[i];
+    __syncthreads();
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ncoef)
+        return;
+    const u32 c = coef[i];
+    const u32 lc = s_log[c];
+    auto mul = [&](u32 v) -> u32 { return (c && v) ? (u32)s_exp[lc + s_log[v]] : 0u; };
+    auto pack = [&](u32 a, u32 b, u32 cc, u32 d) { return mul(a) | mul(b) << 8 | mul(cc) << 16 | mul(d) << 24; };
+    u32 *o = tabs + (u64)i * sec::kTabDwords;
+    o[0] = pack(0, 1, 2, 3);                      // c * lo3,        lo3 = 0..3
+    o[1] = pack(4, 5, 6, 7);                      //                 lo3 = 4..7
+    o[2] = pack(0 << 3, 1 << 3, 2 << 3, 3 << 3);  // c * (mid3<<3), mid3 = 0..3
+    o[3] = pack(4 << 3, 5 << 3, 6 << 3, 7 << 3);  //                 mid3 = 4..7
+    o[4] = pack(0 << 6, 1 << 6, 2 << 6, 3 << 6);  // c * (hi2<<6),   hi2 = 0..3
+}
+
+// ---- the multiply-accumulate ------------------------------------------------
+template <int R, int U>
+__device__ __forceinline__ void gf_mac(u32x4 (&acc)[R][U], const u32x4 (&x)[U], const u32 *__restrict__ t)
+{
+    u32 s0[U][4], s1[U][4], s2[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const u32 v = x[u][w];
+            s0[u][w] = v & 0x07070707u;
+            s1[u][w] = (v >> 3) & 0x07070707u;
+            s2[u][w] = (v >> 6) & 0x03030303u;
+        }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const u32 a0 = t[r * 5 + 0], a1 = t[r * 5 + 1];
+        const u32 b0 = t[r * 5 + 2], b1 = t[r * 5 + 3];
+        const u32 c0 = t[r * 5 + 4];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                acc[r][u][w] ^= __builtin_amdgcn_perm(a1, a0, s0[u][w]) ^ __builtin_amdgcn_perm(b1, b0, s1[u][w]) ^
+                                __builtin_amdgcn_perm(c0, c0, s2[u][w]);
+    }
+}
+
+__device__ __forceinline__ u32x4 load16(const u8 *p) { return *reinterpret_cast<const u32x4_u *>(p); }
+__device__ __forceinline__ void store16(u8 *p, u32x4 v) { *reinterpret_cast<u32x4_u *>(p) = v; }
+
+// bytes [pos, pos+16) of a row, zero at and beyond `lim`
+__device__ __forceinline__ u32x4 load_edge(const u8 *row, u32 pos, int64_t lim)
+{
+    u32x4 v = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        if ((int64_t)pos + b < lim)
+            v[b >> 2] |= (u32)row[pos + b] << (8 * (b & 3));
+    return v;
+}
+
+__device__ __forceinline__ void store_edge(u8 *row, u32 pos, int64_t lim, u32x4 v)
+{
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        if ((int64_t)pos + b < lim)
+            row[pos + b] = (u8)(v[b >> 2] >> (8 * (b & 3)));
+}
+
+__device__ __forceinline__ int64_t row_limit(uint64_t n, u32 B, u32 row)
+{
+    const int64_t l = (int64_t)n - (int64_t)row * B;
+    return l < 0 ? 0 : (l > (int64_t)B ? (int64_t)B : l);
+}
+
+// ---- encode ----------------------------------------------------------------
+// grid = tiles of one row-group size R; tile = (chunk, t0, r0).
+template <int R, int U, bool EDGE>
+__global__ __launch_bounds__(256) void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+                                                         const sec::EncDesc *__restrict__ descs,
+                                                         const sec::Tile *__restrict__ tiles,
+                                                         const u32 *__restrict__ tabs)
+{
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::EncDesc d = descs[tl.chunk];
+    const u32 B = d.B, k = d.k;
+    const u32 tbase = tl.t0 + threadIdx.x * sec::kLaneBytes;
+    if (tbase >= B)
+        return;
+    const u8 *src = in + d.in_off;
+    u8 *dst = par + d.par_off + (u64)tl.r0 * d.par_stride;
+    const u32 *tj = tabs + d.tab + tl.r0 * sec::kTabDwords;
+    const u32 tstep = d.p * sec::kTabDwords;
+
+    u32x4 acc[R][U];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc[r][u] = u32x4{0u, 0u, 0u, 0u};
+
+    const u32 tlast = tbase + (U - 1) * sec::kStepBytes + sec::kLaneBytes;
+    const bool full = !EDGE || (tlast <= B && (u64)(k - 1) * B + tlast <= d.n);
+    if (full) {
+        for (u32 j = 0; j < k; ++j, tj += tstep) {
+            const u8 *row = src + (u64)j * B + tbase;
+            u32x4 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                x[u] = load16(row + u * sec::kStepBytes);
+            gf_mac<R, U>(acc, x, tj);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                store16(dst + (u64)r * d.par_stride + tbase + u * sec::kStepBytes, acc[r][u]);
+    } else if constexpr (EDGE) {
+        for (u32 j = 0; j < k; ++j, tj += tstep) {
+            const u8 *row = src + (u64)j * B;
+            const int64_t lim = row_limit(d.n, B, j);
+            u32x4 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                x[u] = load_edge(row, tbase + u * sec::kStepBytes, lim);
+            gf_mac<R, U>(acc, x, tj);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                store_edge(dst + (u64)r * d.par_stride, tbase + u * sec::kStepBytes, B, acc[r][u]);
+    }
+}
+
+// ---- decode + reassemble -----------------------------------------------------
+// Slot c of a chunk holds block number idx[c]; primaries sit in their own slot
+// (zfec's normalisation).  Present primaries are copied to their output row;
+// the R missing rows of this tile's row group are XOR_c Minv[row][c] * slot_c.
+template <int R, int U, bool EDGE>
+__global__ __launch_bounds__(256) void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+                                                         const sec::DecDesc *__restrict__ descs,
+                                                         const sec::Tile *__restrict__ tiles,
+                                                         const u32 *__restrict__ tabs,
+                                                         const u64 *__restrict__ slot_off,
+                                                         const u32 *__restrict__ slot_row,
+                                                         const u32 *__restrict__ miss_row)
+{
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::DecDesc d = descs[tl.chunk];
+    const u32 B = d.B, k = d.k;
+    const u32 tbase = tl.t0 + threadIdx.x * sec::kLaneBytes;
+    if (tbase >= B)
+        return;
+    u8 *dst = out + d.out_off;
+    const bool copies = tl.r0 == 0;  // row group 0 also copies the present primaries
+    const u32 *tj = tabs + d.tab + tl.r0 * sec::kTabDwords;
+    const u32 tstep = d.e * sec::kTabDwords;
+
+    u32x4 acc[R > 0 ? R : 1][U];
+#pragma unroll
+    for (int r = 0; r < (R > 0 ? R : 1); ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc[r][u] = u32x4{0u, 0u, 0u, 0u};
+
+    const u32 tlast = tbase + (U - 1) * sec::kStepBytes + sec::kLaneBytes;
+    const bool full = !EDGE || (tlast <= B && (u64)(k - 1) * B + tlast <= d.n);
+    for (u32 c = 0; c < k; ++c, tj += tstep) {
+        const u32 orow = slot_row[d.slot0 + c];
+        const bool copy = copies && orow != 0xFFFFFFFFu;
+        if (R == 0 && !copy)
+            continue;
+        const u8 *s = blocks + slot_off[d.slot0 + c] + tbase;
+        u32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            x[u] = (!EDGE || full) ? load16(s + u * sec::kStepBytes) : load_edge(s, u * sec::kStepBytes, (int64_t)B - tbase);
+        if (copy) {
+            u8 *o = dst + (u64)orow * B;
+            const int64_t lim = row_limit(d.n, B, orow);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!EDGE || full)
+                    store16(o + tbase + u * sec::kStepBytes, x[u]);
+                else
+                    store_edge(o, tbase + u * sec::kStepBytes, lim, x[u]);
+            }
+        }
+        if constexpr (R > 0)
+            gf_mac<R, U>(acc, x, tj);
+    }
+    if constexpr (R > 0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const u32 orow = miss_row[d.slot0 + tl.r0 + r];
+            u8 *o = dst + (u64)orow * B;
+            const int64_t lim = row_limit(d.n, B, orow);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!EDGE || full)
+                    store16(o + tbase + u * sec::kStepBytes, acc[r][u]);
+                else
+                    store_edge(o, tbase + u * sec::kStepBytes, lim, acc[r][u]);
+            }
+        }
+    }
+}
+
+template <int R, int U, bool EDGE>
+hipError_t launch_enc(const u8 *in, u8 *par, const sec::EncDesc *descs, const sec::Tile *tiles, u32 ntiles,
+                      const u32 *tabs, hipStream_t s)
+{
+    hipLaunchKernelGGL((sec_encode_kernel<R, U, EDGE>), dim3(ntiles), dim3(sec::kLanes), 0, s, in, par, descs, tiles,
+                       tabs);
+    return hipGetLastError();
+}
+
+template <int R, int U, bool EDGE>
+hipError_t launch_dec(const u8 *blocks, u8 *out, const sec::DecDesc *descs, const sec::Tile *tiles, u32 ntiles,
+                      const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, hipStream_t s)
+{
+    hipLaunchKernelGGL((sec_decode_kernel<R, U, EDGE>), dim3(ntiles), dim3(sec::kLanes), 0, s, blocks, out, descs, tiles,
+                       tabs, so, sr, mr);
+    return hipGetLastError();
+}
+
+template <int U, bool EDGE>
+hipError_t dispatch_enc(int rows, const u8 *in, u8 *par, const sec::EncDesc *d, const sec::Tile *t, u32 nt,
+                        const u32 *tabs, hipStream_t s)
+{
+    switch (rows) {
+    case 1: return launch_enc<1, U, EDGE>(in, par, d, t, nt, tabs, s);
+    case 2: return launch_enc<2, U, EDGE>(in, par, d, t, nt, tabs, s);
+    case 3: return launch_enc<3, U, EDGE>(in, par, d, t, nt, tabs, s);
+    case 4: return launch_enc<4, U, EDGE>(in, par, d, t, nt, tabs, s);
+    case 5: return launch_enc<5, U, EDGE>(in, par, d, t, nt, tabs, s);
+    case 6: return launch_enc<6, U, EDGE>(in, par, d, t, nt, tabs, s);
+    case 7: return launch_enc<7, U, EDGE>(in, par, d, t, nt, tabs, s);
+    case 8: return launch_enc<8, U, EDGE>(in, par, d, t, nt, tabs, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int U, bool EDGE>
+hipError_t dispatch_dec(int rows, const u8 *b, u8 *o, const sec::DecDesc *d, const sec::Tile *t, u32 nt,
+                        const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, hipStream_t s)
+{
+    switch (rows) {
+    case 0: return launch_dec<0, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 1: return launch_dec<1, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 2: return launch_dec<2, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 3: return launch_dec<3, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 4: return launch_dec<4, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 5: return launch_dec<5, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 6: return launch_dec<6, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 7: return launch_dec<7, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 8: return launch_dec<8, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void *stream)
+{
+    if (ncoef == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_expand_tables, dim3((ncoef + 255) / 256), dim3(256), 0, (hipStream_t)stream, coef, ncoef,
+                       tabs);
+    return hipGetLastError();
+}
+
+int sec_launch_encode(int rows, int U, bool edge, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
+                      const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, void *stream)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    hipStream_t s = (hipStream_t)stream;
+    switch (U) {
+    case 1: return edge ? dispatch_enc<1, true>(rows, in, par, descs, tiles, ntiles, tabs, s) : dispatch_enc<1, false>(rows, in, par, descs, tiles, ntiles, tabs, s);
+    case 2: return edge ? dispatch_enc<2, true>(rows, in, par, descs, tiles, ntiles, tabs, s) : dispatch_enc<2, false>(rows, in, par, descs, tiles, ntiles, tabs, s);
+    case 4: return edge ? dispatch_enc<4, true>(rows, in, par, descs, tiles, ntiles, tabs, s) : dispatch_enc<4, false>(rows, in, par, descs, tiles, ntiles, tabs, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+int sec_launch_decode(int rows, int U, bool edge, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
+                      const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, const uint64_t *slot_off,
+                      const uint32_t *slot_row, const uint32_t *miss_row, void *stream)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    hipStream_t s = (hipStream_t)stream;
+    switch (U) {
+    case 1: return edge ? dispatch_dec<1, true>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s) : dispatch_dec<1, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
+    case 2: return edge ? dispatch_dec<2, true>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s) : dispatch_dec<2, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
+    case 4: return edge ? dispatch_dec<4, true>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s) : dispatch_dec<4, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
+    default: return hipErrorInvalidValue;
+    }
+}

@@ -1,0 +1,62 @@
+// kernels.hpp — device-side descriptors shared by kernels.hip and api.cpp.
+//
+// Work decomposition.  A "tile" is one workgroup of 256 lanes over a run of
+// 256*16*U consecutive byte positions t of ONE chunk's blocks (U = 1 or 4), and
+// a group of up to 8 output rows (parity rows for encode, missing data rows
+// for decode).  Each lane owns 16 consecutive positions per u-step, so every
+// wave reads one coalesced 1 KiB run from each of the k input blocks and
+// writes one 1 KiB run per output row.
+#pragma once
+#include <stdint.h>
+
+namespace sec {
+
+constexpr int kLanes = 256;         // threads per workgroup
+constexpr int kLaneBytes = 16;      // bytes per lane per u-step (dwordx4)
+constexpr int kStepBytes = kLanes * kLaneBytes;  // 4 KiB per u-step
+constexpr int kMaxRows = 8;         // output rows per tile (accumulator groups)
+constexpr int kTabDwords = 5;       // v_perm tables per GF coefficient
+
+// One encode chunk, device copy (48 B).
+struct EncDesc {
+    uint64_t in_off;      // chunk start in `in`
+    uint64_t par_off;     // first parity block in `parity`
+    uint64_t par_stride;  // bytes between parity blocks
+    uint64_t n;           // chunk bytes
+    uint32_t B;           // block bytes = ceil(n/k)
+    uint32_t k;           // data blocks
+    uint32_t p;           // parity blocks (m - k)
+    uint32_t tab;         // dword offset of this chunk's tables, layout [j][r][5]
+};
+
+// One decode chunk, device copy (40 B).
+struct DecDesc {
+    uint64_t out_off;  // reassembled chunk start in `out`
+    uint64_t n;        // bytes to write = k*B - padlen
+    uint32_t B;
+    uint32_t k;
+    uint32_t e;        // missing primaries (rows recovered)
+    uint32_t tab;      // dword offset of tables, layout [slot][missing][5]
+    uint32_t slot0;    // first entry in slot_off / slot_row / miss_row
+    uint32_t pad;
+};
+
+struct Tile {
+    uint32_t chunk;  // descriptor index
+    uint32_t t0;     // first byte position within the block
+    uint32_t r0;     // first output row of this tile's row group
+    uint32_t pad;
+};
+
+}  // namespace sec
+
+// launchers (kernels.hip); all enqueue on `stream` and return hipError_t as int
+extern "C++" {
+int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void *stream);
+int sec_launch_encode(int rows, int U, bool edge, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
+                      const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, void *stream);
+int sec_launch_decode(int rows, int U, bool edge, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
+                      const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
+                      const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,
+                      void *stream);
+}

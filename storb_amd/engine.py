@@ -1,0 +1,228 @@
+"""Host-side engine over libstorbec.so: one HIP context per (device, thread).
+
+Two ways in:
+  * device-resident batches (``encode_batch`` / ``decode_batch``): descriptor arrays +
+    device addresses (torch tensors, or any integer address) — the bench and the GPU parity
+    tests use these;
+  * host batches (``encode_host`` / ``decode_host``): lists of bytes-like objects; the
+    library gathers them into pinned staging, runs the kernels and copies results back —
+    this is what the easyfec-compatible layer and the ``piece`` drop-in use.
+
+There is no CPU compute path: every call goes to the HIP kernels; construction raises
+``ECRuntimeError`` when no device is present.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from . import _lib
+from ._lib import DEC_DTYPE, ENC_DTYPE, SEC_F_ASYNC, SEC_F_HOST
+
+
+class Error(Exception):
+    """A zfec precondition violation (zfec raises ``zfec.Error`` for the same cases)."""
+
+
+class ECRuntimeError(RuntimeError):
+    """Device / runtime failure (no GPU, HIP error, out of memory)."""
+
+
+def check(rc: int) -> None:
+    if rc == 0:
+        return
+    msg = _lib.strerror(rc)
+    if rc in _lib.PRECONDITION_CODES:
+        raise Error(msg)
+    raise ECRuntimeError(f"libstorbec: {msg} (status {rc})")
+
+
+def addr(obj) -> tuple[int, object]:
+    """(address, keep-alive) of a buffer: int, torch tensor, numpy array or bytes-like."""
+    if obj is None:
+        return 0, None
+    if isinstance(obj, int):
+        return obj, None
+    if hasattr(obj, "data_ptr"):  # torch.Tensor (device or host)
+        return int(obj.data_ptr()), obj
+    if isinstance(obj, np.ndarray):
+        return int(obj.ctypes.data), obj
+    arr = np.frombuffer(obj, dtype=np.uint8)
+    return (int(arr.ctypes.data) if arr.size else 0), arr
+
+
+def _ptr(a: np.ndarray) -> int:
+    return int(a.ctypes.data) if a.size else 0
+
+
+def default_device() -> int:
+    for var in ("STORB_EC_DEVICE", "LOCAL_RANK"):
+        v = os.environ.get(var)
+        if v is not None and v.strip().lstrip("-").isdigit():
+            return int(v)
+    return 0
+
+
+def device_count() -> int:
+    lib = _lib.load()
+    n = ctypes.c_int(0)
+    rc = lib.sec_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+class Engine:
+    """A libstorbec context on one device.  Not thread-safe; use ``get_engine()`` per thread."""
+
+    def __init__(self, device: int | None = None):
+        self.lib = _lib.load()
+        self.device = default_device() if device is None else int(device)
+        h = ctypes.c_void_p()
+        rc = self.lib.sec_ctx_create(self.device, ctypes.byref(h))
+        if rc:
+            raise ECRuntimeError(f"cannot create HIP context on device {self.device}: {_lib.strerror(rc)}")
+        self._ctx = h
+
+    # -- lifecycle / stream / timing ----------------------------------------
+    def close(self) -> None:
+        if self._ctx:
+            self.lib.sec_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream) -> None:
+        """Launch on an external hipStream_t (int handle or torch.cuda.Stream); None = own."""
+        h = getattr(stream, "cuda_stream", stream)
+        check(self.lib.sec_ctx_set_stream(self._ctx, h or None))
+
+    def sync(self) -> None:
+        check(self.lib.sec_sync(self._ctx))
+
+    def set_timing(self, enable: bool) -> None:
+        check(self.lib.sec_ctx_set_timing(self._ctx, int(bool(enable))))
+
+    def collect_timing(self, kind: str) -> tuple[float, int]:
+        """(summed kernel ms, launch count) recorded since the last collect; kind 'encode'|'decode'."""
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int64(0)
+        check(self.lib.sec_timing_collect(self._ctx, {"encode": 0, "decode": 1}[kind], ctypes.byref(ms),
+                                          ctypes.byref(n)))
+        return ms.value, n.value
+
+    # -- device-resident batches --------------------------------------------
+    def encode_batch(self, descs: np.ndarray, src, parity, *, host: bool = False, asynchronous: bool = False) -> None:
+        descs = np.ascontiguousarray(descs, dtype=ENC_DTYPE)
+        s, _ks = addr(src)
+        p, _kp = addr(parity)
+        flags = (SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0)
+        check(self.lib.sec_encode_batch(self._ctx, _ptr(descs), len(descs), s or None, p or None, flags))
+
+    def decode_batch(self, descs: np.ndarray, sharenums: np.ndarray, block_offs: np.ndarray, blocks, out, *,
+                     host: bool = False, asynchronous: bool = False) -> None:
+        descs = np.ascontiguousarray(descs, dtype=DEC_DTYPE)
+        sn = np.ascontiguousarray(sharenums, dtype=np.int32)
+        bo = np.ascontiguousarray(block_offs, dtype=np.uint64)
+        b, _kb = addr(blocks)
+        o, _ko = addr(out)
+        flags = (SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0)
+        check(self.lib.sec_decode_batch(self._ctx, _ptr(descs), len(descs), _ptr(sn), _ptr(bo), b or None,
+                                        o or None, flags))
+
+    # -- host batches ---------------------------------------------------------
+    def encode_host(self, chunks, shapes) -> list[list[bytes]]:
+        """Parity blocks for each chunk.  chunks: bytes-like list; shapes: [(k, m)] per chunk.
+
+        Returns, per chunk, the m-k secondary blocks (block numbers k..m-1) as bytes.
+        """
+        n = len(chunks)
+        descs = np.zeros(n, dtype=ENC_DTYPE)
+        keep = []
+        blocks = []
+        total = 0
+        for i, (c, (k, m)) in enumerate(zip(chunks, shapes)):
+            a, kp = addr(c)
+            keep.append(kp)
+            ln = len(kp) if isinstance(kp, np.ndarray) else len(c)
+            B = -(-ln // k) if ln else 0
+            descs[i] = (a, ln, total, max(B, 1), k, m)
+            blocks.append((total, B, m - k))
+            total += (m - k) * B
+        out = np.empty(max(total, 1), dtype=np.uint8)
+        self.encode_batch(descs, 0, out, host=True)
+        mv = memoryview(out)
+        return [[bytes(mv[o + r * B:o + (r + 1) * B]) for r in range(p)] for (o, B, p) in blocks]
+
+    def decode_host(self, items, out=None) -> bytes:
+        """Reassemble chunks from host blocks, concatenated in order.
+
+        items: [(k, m, blocks, sharenums, padlen)] with exactly k equal-length blocks each.
+        Returns the concatenation of every chunk's k*B - padlen bytes.
+        """
+        n = len(items)
+        descs = np.zeros(n, dtype=DEC_DTYPE)
+        nslots = sum(it[0] for it in items)
+        sn = np.zeros(nslots, dtype=np.int32)
+        bo = np.zeros(nslots, dtype=np.uint64)
+        keep = []
+        slot = 0
+        total = 0
+        for i, (k, m, blocks, sharenums, padlen) in enumerate(items):
+            if len(blocks) != k or len(sharenums) != k:
+                raise Error(_lib.strerror(_lib.SEC_ENBLOCKS))
+            B = len(blocks[0])
+            for j, b in enumerate(blocks):
+                if len(b) != B:
+                    raise Error(_lib.strerror(_lib.SEC_EBLOCKLEN))
+                a, kp = addr(b)
+                keep.append(kp)
+                bo[slot + j] = a
+                sn[slot + j] = int(sharenums[j])
+            descs[i] = (total, B, padlen, slot, k, m)
+            slot += k
+            total += k * B - padlen
+        buf = np.empty(max(total, 1), dtype=np.uint8) if out is None else out
+        self.decode_batch(descs, sn, bo, 0, buf, host=True)
+        return bytes(memoryview(buf)[:total])
+
+
+# -- matrices (host arithmetic; no device needed) ------------------------------
+def encode_matrix(k: int, m: int) -> bytes:
+    """Rows k..m-1 of zfec's systematic encode matrix, as produced by libstorbec."""
+    lib = _lib.load()
+    out = np.zeros(max((m - k) * k, 1), dtype=np.uint8)
+    check(lib.sec_encode_matrix(k, m, _ptr(out)))
+    return out[: (m - k) * k].tobytes()
+
+
+def decode_matrix(k: int, m: int, sharenums) -> tuple[bytes, list[int]]:
+    lib = _lib.load()
+    sn = np.ascontiguousarray(sharenums, dtype=np.int32)
+    if sn.size != k:
+        raise Error(_lib.strerror(_lib.SEC_ENBLOCKS))
+    out = np.zeros(k * k, dtype=np.uint8)
+    idx = np.zeros(k, dtype=np.int32)
+    check(lib.sec_decode_matrix(k, m, _ptr(sn), _ptr(out), _ptr(idx)))
+    return out.tobytes(), idx.tolist()
+
+
+_tls = threading.local()
+
+
+def get_engine(device: int | None = None) -> Engine:
+    """The calling thread's engine for `device` (default: STORB_EC_DEVICE / LOCAL_RANK / 0)."""
+    dev = default_device() if device is None else int(device)
+    engines = getattr(_tls, "engines", None)
+    if engines is None:
+        engines = _tls.engines = {}
+    eng = engines.get(dev)
+    if eng is None:
+        eng = engines[dev] = Engine(dev)
+    return eng

@@ -1,0 +1,239 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the CPU oracle, bit-exact.
+
+* golden fixtures (tests/golden/golden.json) and oracle/fec_oracle.c on seeded inputs at sizes
+  the oracle finishes in seconds, covering aligned and unaligned block sizes, the zero-padded
+  last block, tiny chunks, m == k, and row groups beyond 8 (p > 8, e > 8);
+* BASELINE.json's full sizes (1024 x 1 MiB RS(4,2); RS(10,4) 64 KiB chunks; mixed RS(8,3))
+  through size-independent properties — encode -> erase -> decode round trips over every
+  chunk — plus oracle comparison on a sample of chunks.
+"""
+
+import hashlib
+import itertools
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import cfec
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+
+from storb_amd._lib import DEC_DTYPE, ENC_DTYPE  # noqa: E402
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def oracle_parity(data, k, m):
+    return cfec.easy_encode(bytes(data), k, m)[k:]
+
+
+# ---------------------------------------------------------------- host-mode path
+def test_encode_golden(engine):
+    ents = GOLDEN["encode"]
+    chunks = [random.Random(e["seed"]).randbytes(e["n"]) for e in ents]
+    par = engine.encode_host(chunks, [(e["k"], e["m"]) for e in ents])
+    for e, p in zip(ents, par):
+        assert [sha(b) for b in p] == e["blocks_sha256"][e["k"]:], (e["k"], e["m"], e["n"])
+
+
+def test_decode_golden(engine):
+    for e in GOLDEN["decode"]:
+        k, m, sn = e["k"], e["m"], e["sharenums"]
+        data = random.Random(e["seed"]).randbytes(e["n"])
+        blocks = cfec.easy_encode(data, k, m)
+        pad = len(blocks[0]) * k - len(data)
+        got = engine.decode_host([(k, m, [blocks[s] for s in sn], sn, pad)])
+        assert sha(got) == e["out_sha256"]
+
+
+@pytest.mark.parametrize("k,m", [(1, 2), (2, 3), (3, 4), (4, 6), (5, 8), (8, 11), (10, 14), (8, 16), (12, 20),
+                                 (16, 24), (20, 30), (32, 48), (64, 96), (4, 4), (7, 256)])
+def test_encode_random_sizes_vs_oracle(engine, k, m):
+    rng = random.Random(k * 1000 + m)
+    sizes = [k, k * k, 4095, 4096 * k, 4096 * k + 1, 65536, 65536 + 7, 6554 * k - 3, 262144 + 13, 1 << 20]
+    sizes += [rng.randrange(k * k, 300000) for _ in range(6)]
+    sizes = [n for n in sizes if -(-n // k) * (k - 1) <= n]
+    chunks = [rng.randbytes(n) for n in sizes]
+    par = engine.encode_host(chunks, [(k, m)] * len(chunks))
+    for c, p in zip(chunks, par):
+        assert p == oracle_parity(c, k, m), (k, m, len(c))
+
+
+def test_encode_mixed_shapes_one_batch(engine):
+    rng = random.Random(5)
+    shapes = [(1, 2), (2, 3), (4, 6), (8, 11), (10, 14), (16, 24), (3, 12)]
+    chunks, km = [], []
+    for i in range(60):
+        k, m = shapes[i % len(shapes)]
+        n = rng.randrange(max(k * k, 1), 200000)
+        chunks.append(rng.randbytes(n))
+        km.append((k, m))
+    par = engine.encode_host(chunks, km)
+    for c, (k, m), p in zip(chunks, km, par):
+        assert p == oracle_parity(c, k, m)
+
+
+@pytest.mark.parametrize("k,m", [(2, 3), (4, 6), (8, 11), (10, 14), (16, 24), (16, 40), (32, 48)])
+def test_decode_erasures_vs_oracle(engine, k, m):
+    rng = random.Random(k + 100 * m)
+    items, expect = [], []
+    for n in [k * k, 4096 * k - 5, 65536 + 3, 6554 * k, 300001]:
+        if -(-n // k) * (k - 1) > n:
+            continue
+        data = rng.randbytes(n)
+        blocks = cfec.easy_encode(data, k, m)
+        B = len(blocks[0])
+        for _ in range(4):
+            sn = rng.sample(range(m), k)
+            items.append((k, m, [blocks[s] for s in sn], sn, B * k - n))
+            expect.append(data)
+    got = engine.decode_host(items)
+    assert got == b"".join(expect)
+    # each case also equals the oracle's own decode (same bytes by construction)
+    k0, m0, bl, sn, pad = items[-1]
+    assert cfec.easy_decode(bl, sn, pad, k0, m0) == expect[-1]
+
+
+def test_decode_every_pattern_rs42(engine):
+    data = random.Random(9).randbytes(1 << 20)
+    blocks = cfec.easy_encode(data, 4, 6)
+    items = []
+    for sub in itertools.combinations(range(6), 4):
+        for order in (list(sub), list(reversed(sub))):
+            items.append((4, 6, [blocks[s] for s in order], order, 0))
+    got = engine.decode_host(items)
+    assert got == data * len(items)
+
+
+def test_empty_and_degenerate(engine):
+    assert engine.encode_host([b""], [(4, 6)]) == [[b"", b""]]
+    assert engine.encode_host([b"\x07"], [(1, 2)]) == [[b"\x07"]]  # zfec(1,2) parity = copy
+    assert engine.encode_host([b"abcdefgh"], [(4, 4)]) == [[]]
+    assert engine.decode_host([(1, 2, [b"\x07"], [1], 0)]) == b"\x07"
+
+
+# ---------------------------------------------------------------- device-resident path
+def _dev(nbytes, seed):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
+
+
+def _enc_descs(nchunks, n, k, m):
+    B = -(-n // k)
+    d = np.zeros(nchunks, dtype=ENC_DTYPE)
+    d["in_off"] = np.arange(nchunks, dtype=np.uint64) * n
+    d["n"] = n
+    d["parity_off"] = np.arange(nchunks, dtype=np.uint64) * (m - k) * B
+    d["parity_stride"] = B
+    d["k"] = k
+    d["m"] = m
+    return d, B
+
+
+def _dec_inputs(nchunks, n, k, m, B, erased, data_base, par_base):
+    """Descriptors reading the surviving blocks straight from the encoded device buffers."""
+    keep = [s for s in range(m) if s not in erased][:k]
+    d = np.zeros(nchunks, dtype=DEC_DTYPE)
+    d["out_off"] = np.arange(nchunks, dtype=np.uint64) * n
+    d["B"] = B
+    d["padlen"] = B * k - n
+    d["slot0"] = np.arange(nchunks, dtype=np.uint64) * k
+    d["k"] = k
+    d["m"] = m
+    sn = np.tile(np.array(keep, np.int32), nchunks)
+    offs = np.zeros(nchunks * k, np.uint64)
+    for j, s in enumerate(keep):
+        ci = np.arange(nchunks, dtype=np.uint64)
+        if s < k:
+            offs[j::k] = data_base + ci * n + s * B
+        else:
+            offs[j::k] = par_base + ci * (m - k) * B + (s - k) * B
+    return d, sn, offs
+
+
+def _roundtrip_full(engine, nchunks, n, k, m, erased, sample):
+    src = _dev(nchunks * n, seed=n + k)
+    d, B = _enc_descs(nchunks, n, k, m)
+    par = torch.empty(nchunks * (m - k) * B, dtype=torch.uint8, device="cuda")
+    engine.encode_batch(d, src, par)
+    # oracle on a sample of chunks
+    src_h = src.cpu().numpy()
+    par_h = par.cpu().numpy()
+    for ci in sample:
+        want = oracle_parity(src_h[ci * n:(ci + 1) * n].tobytes(), k, m)
+        got = par_h[ci * (m - k) * B:(ci + 1) * (m - k) * B].tobytes()
+        assert got == b"".join(want), ci
+    # size-independent property over EVERY chunk: erase, decode, compare to the source
+    out = torch.empty(nchunks * n, dtype=torch.uint8, device="cuda")
+    dd, sn, offs = _dec_inputs(nchunks, n, k, m, B, erased, src.data_ptr(), par.data_ptr())
+    engine.decode_batch(dd, sn, offs, 0, out)
+    assert torch.equal(out, src)
+    # linearity of the whole batch: parity(src ^ x) == parity(src) ^ parity(x)
+    x = _dev(nchunks * n, seed=1234)
+    px = torch.empty_like(par)
+    pxs = torch.empty_like(par)
+    engine.encode_batch(d, x, px)
+    engine.encode_batch(d, src ^ x, pxs)
+    assert torch.equal(pxs, par ^ px)
+
+
+def test_c2_c3_full_size_rs42(engine):
+    # BASELINE configs[1] / configs[2]: 1024 x 1 MiB, RS(4,2) = zfec(4,6), data shards {1,3} erased
+    _roundtrip_full(engine, 1024, 1 << 20, 4, 6, erased={1, 3}, sample=[0, 1, 511, 1023])
+
+
+def test_c4_shape_rs104_unaligned(engine):
+    # BASELINE configs[3] per-GPU share at reduced count: 64 KiB chunks, RS(10,4): B = 6554 (unaligned)
+    _roundtrip_full(engine, 1024, 65536, 10, 14, erased={0, 5, 9, 2}, sample=[0, 3, 777, 1023])
+
+
+def test_decode_parity_only_and_more_than_8_missing(engine):
+    # k=16 with 16 parity rows: decode from parity only (e = 16 > 8 -> two row groups)
+    _roundtrip_full(engine, 16, 16 * 4096 * 3 + 5 * 16, 16, 32, erased=set(range(16)), sample=[0, 15])
+
+
+def test_external_stream_async_and_timing(engine):
+    n, k, m, nch = 1 << 20, 4, 6, 64
+    src = _dev(nch * n, seed=3)
+    d, B = _enc_descs(nch, n, k, m)
+    par1 = torch.empty(nch * 2 * B, dtype=torch.uint8, device="cuda")
+    par2 = torch.empty_like(par1)
+    engine.encode_batch(d, src, par1)
+    s = torch.cuda.Stream()
+    engine.set_stream(s)
+    engine.set_timing(True)
+    try:
+        engine.encode_batch(d, src, par2, asynchronous=True)
+        s.synchronize()
+        ms, launches = engine.collect_timing("encode")
+        assert launches == 1 and ms > 0
+    finally:
+        engine.set_timing(False)
+        engine.set_stream(None)
+    assert torch.equal(par1, par2)
+
+
+def test_c5_mixed_sizes_host_e2e(engine):
+    # BASELINE configs[4] at reduced total: sizes log-uniform in [4 KiB, 4 MiB], RS(8,3) = zfec(8,11)
+    rng = np.random.default_rng(5)
+    sizes = np.exp(rng.uniform(np.log(4096), np.log(4 << 20), 48)).astype(int).tolist()
+    chunks = [rng.integers(0, 256, s, dtype=np.uint8).tobytes() for s in sizes]
+    par = engine.encode_host(chunks, [(8, 11)] * len(chunks))
+    for c, p in zip(chunks, par):
+        assert p == oracle_parity(c, 8, 11)
+    items = []
+    for i, (c, p) in enumerate(zip(chunks, par)):
+        B = len(p[0])
+        blocks = [c[j * B:(j + 1) * B].ljust(B, b"\0") for j in range(8)] + p
+        sn = sorted(random.Random(i).sample(range(11), 8))
+        items.append((8, 11, [blocks[s] for s in sn], sn, B * 8 - len(c)))
+    assert engine.decode_host(items) == b"".join(chunks)
