@@ -99,7 +99,9 @@ int sec_device_count(int *count);              /* SEC_ENODEV when the HIP runtim
 int sec_ctx_create(int device, sec_ctx **out);
 void sec_ctx_destroy(sec_ctx *ctx);
 /* Launch on an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+ * NULL restores the context's own stream, which is created blocking (ordered with
+ * the legacy NULL stream, torch's default stream).  Producers on any other stream
+ * must be ordered by the caller (or the context switched onto their stream). */
 int sec_ctx_set_stream(sec_ctx *ctx, void *hip_stream);
 int sec_sync(sec_ctx *ctx);
 /* HIP-event timing of the hot kernels: when enabled every batch call records an
@@ -129,7 +131,8 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
 /* Decode + reassemble: for every chunk, its k blocks are at
  * blocks + block_offs[slot0 + i] (B bytes each) with block numbers
  * sharenums[slot0 + i]; the chunk's k*B - padlen bytes are written at
- * out + out_off.  Present primaries are copied, missing ones recovered. */
+ * out + out_off.  Present primaries are copied, missing ones recovered.
+ * `blocks` may be NULL, in which case block_offs are absolute addresses. */
 int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
                      const int32_t *sharenums, const uint64_t *block_offs,
                      const uint8_t *blocks, uint8_t *out, unsigned flags);

@@ -353,7 +353,10 @@ int sec_ctx_create(int device, sec_ctx **out)
     ctx->device = device;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess)
-        e = hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking);
+        // blocking w.r.t. the legacy NULL stream, so device buffers produced by work
+        // there (e.g. torch's default stream) are ordered before our kernels and
+        // results are ordered before the NULL stream's later work
+        e = hipStreamCreateWithFlags(&ctx->own, hipStreamDefault);
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&ctx->pin_ev, hipEventDisableTiming);
     if (e == hipSuccess)
@@ -744,7 +747,7 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
     }
     if (total_out == 0)
         return SEC_OK;
-    if (!out || (!blocks && !host))
+    if (!out)  // blocks may be NULL: block_offs are then absolute addresses
         return SEC_EINVAL;
 
     Plan &plan = ctx->dec_plan;
