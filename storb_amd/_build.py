@@ -33,25 +33,29 @@ def _digest() -> str:
     return h.hexdigest()
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, defines: dict | None = None, tag: str | None = None) -> str:
+    """Compile libstorbec.so (or, with `tag`, an A/B variant libstorbec_<tag>.so built with
+    extra -D `defines`, used by tools/sweep.py)."""
     os.makedirs(LIBDIR, exist_ok=True)
-    stamp = LIB + ".stamp"
-    dig = _digest()
-    if not force and os.path.exists(LIB) and os.path.exists(stamp):
+    lib = LIB if not tag else os.path.join(LIBDIR, f"libstorbec_{tag}.so")
+    defs = [f"-D{k}={v}" for k, v in sorted((defines or {}).items())]
+    stamp = lib + ".stamp"
+    dig = _digest() + " ".join(defs)
+    if not force and os.path.exists(lib) and os.path.exists(stamp):
         with open(stamp) as f:
             if f.read().strip() == dig:
-                return LIB
-    tmp = LIB + ".tmp"
+                return lib
+    tmp = lib + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", "-o", tmp]
+           "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", *defs, "-o", tmp]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     with open(stamp, "w") as f:
         f.write(dig)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

@@ -80,15 +80,17 @@ _SIGS = {
 }
 SYMBOLS = tuple(_SIGS)
 
-_lib = None
+_libs: dict = {}
 
 
-def load() -> ctypes.CDLL:
-    """Load libstorbec.so from the package tree; raise if it is absent (no fallback)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    path = os.environ.get("STORB_EC_LIB", LIB)
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load libstorbec.so from the package tree; raise if it is absent (no fallback).
+
+    `path` selects an A/B build variant (tools/sweep.py); default: $STORB_EC_LIB or the
+    in-tree storb_amd/lib/libstorbec.so."""
+    path = path or os.environ.get("STORB_EC_LIB", LIB)
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise ImportError(
             f"libstorbec.so not found at {path}: build it with `python -m storb_amd._build` "
@@ -100,7 +102,7 @@ def load() -> ctypes.CDLL:
         fn.argtypes = args
     if lib.sec_abi_version() != 1:
         raise ImportError("libstorbec.so ABI version mismatch")
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 

@@ -131,10 +131,8 @@ struct Plan {
 // bytes in flight per lane but more registers; SEC_TILE_U overrides.
 int pick_u(uint64_t B, int rows)
 {
-    static int forced = [] {
-        const char *s = getenv("SEC_TILE_U");
-        return s ? atoi(s) : 0;
-    }();
+    const char *env = getenv("SEC_TILE_U");  // read per plan build (plans are cached)
+    const int forced = env ? atoi(env) : 0;
     if (forced == 1 || forced == 2 || forced == 4)
         return forced;
     if (B >= 4 * (uint64_t)sec::kStepBytes * 4 && rows <= 2)

@@ -77,8 +77,8 @@ def device_count() -> int:
 class Engine:
     """A libstorbec context on one device.  Not thread-safe; use ``get_engine()`` per thread."""
 
-    def __init__(self, device: int | None = None):
-        self.lib = _lib.load()
+    def __init__(self, device: int | None = None, lib_path: str | None = None):
+        self.lib = _lib.load(lib_path)
         self.device = default_device() if device is None else int(device)
         h = ctypes.c_void_p()
         rc = self.lib.sec_ctx_create(self.device, ctypes.byref(h))

@@ -1,0 +1,129 @@
+// stream_ceiling.hip — measured HBM ceilings for the access pattern of the RS kernels.
+//
+// Not product code: a calibration tool for DESIGN.md's roofline.  Prints one JSON line with
+// GB/s (algorithmic bytes / kernel time, HIP events, median of 20 after 3 warm-ups) for:
+//   copy      uint4 grid-stride copy, 1 GiB -> 1 GiB
+//   read      uint4 grid-stride XOR-reduce of 1.5 GiB (one store per workgroup)
+//   write     uint4 grid-stride fill of 1.5 GiB
+//   rs42_xor  the encode kernel's exact pattern for 1024 x 1 MiB RS(4,2) chunks (4 coalesced
+//             block streams read, 2 written, 16 KiB positions per 256-lane workgroup) with
+//             the GF arithmetic replaced by XOR: the practical roof for sec_encode_kernel
+//   rs42_xor_nt  the same with nontemporal loads and stores
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <vector>
+
+typedef unsigned int u32;
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e = (x);                                                                \
+        if (e != hipSuccess) {                                                             \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                         \
+            return 1;                                                                      \
+        }                                                                                  \
+    } while (0)
+
+__global__ __launch_bounds__(256) void k_copy(const u32x4 *__restrict__ in, u32x4 *__restrict__ out, size_t n)
+{
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        out[i] = in[i];
+}
+
+__global__ __launch_bounds__(256) void k_read(const u32x4 *__restrict__ in, u32x4 *__restrict__ out, size_t n)
+{
+    u32x4 a = {0, 0, 0, 0};
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        a ^= in[i];
+    if ((a.x ^ a.y ^ a.z ^ a.w) == 0x12345678u)
+        out[blockIdx.x] = a;
+}
+
+__global__ __launch_bounds__(256) void k_write(u32x4 *__restrict__ out, size_t n)
+{
+    const u32x4 v = {1, 2, 3, 4};
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        out[i] = v;
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void k_rs42(const unsigned char *__restrict__ in, unsigned char *__restrict__ par)
+{
+    // 16 tiles of 16 KiB positions per 1 MiB chunk (B = 256 KiB)
+    const u32 chunk = blockIdx.x >> 4, t0 = (blockIdx.x & 15) * 16384;
+    const size_t B = 262144;
+    const unsigned char *src = in + (size_t)chunk * 1048576 + t0 + threadIdx.x * 16;
+    unsigned char *dst = par + (size_t)chunk * 2 * B + t0 + threadIdx.x * 16;
+    u32x4 a0[4], a1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        a0[u] = a1[u] = u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const u32x4 *p = (const u32x4 *)(src + j * B + u * 4096);
+            u32x4 x = NT ? __builtin_nontemporal_load(p) : *p;
+            a0[u] ^= x;
+            a1[u] ^= (x << 1);
+        }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        u32x4 *q0 = (u32x4 *)(dst + u * 4096), *q1 = (u32x4 *)(dst + B + u * 4096);
+        if (NT) {
+            __builtin_nontemporal_store(a0[u], q0);
+            __builtin_nontemporal_store(a1[u], q1);
+        } else {
+            *q0 = a0[u];
+            *q1 = a1[u];
+        }
+    }
+}
+
+template <class F>
+double time_ms(F launch)
+{
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int i = 0; i < 3; ++i)
+        launch();
+    std::vector<float> t;
+    for (int i = 0; i < 20; ++i) {
+        (void)hipEventRecord(a);
+        launch();
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms;
+        (void)hipEventElapsedTime(&ms, a, b);
+        t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+int main()
+{
+    const size_t G = 1ull << 30;
+    unsigned char *a, *b;
+    CK(hipMalloc(&a, 2 * G));
+    CK(hipMalloc(&b, 2 * G));
+    CK(hipMemset(a, 7, 2 * G));
+    CK(hipMemset(b, 1, 2 * G));
+    const int grid = 256 * 8;
+    double ms_copy = time_ms([&] { hipLaunchKernelGGL(k_copy, dim3(grid), dim3(256), 0, 0, (u32x4 *)a, (u32x4 *)b, G / 16); });
+    double ms_read = time_ms([&] { hipLaunchKernelGGL(k_read, dim3(grid), dim3(256), 0, 0, (u32x4 *)a, (u32x4 *)b, (G + G / 2) / 16); });
+    double ms_write = time_ms([&] { hipLaunchKernelGGL(k_write, dim3(grid), dim3(256), 0, 0, (u32x4 *)b, (G + G / 2) / 16); });
+    double ms_rs = time_ms([&] { hipLaunchKernelGGL(k_rs42<false>, dim3(1024 * 16), dim3(256), 0, 0, a, b); });
+    double ms_rsnt = time_ms([&] { hipLaunchKernelGGL(k_rs42<true>, dim3(1024 * 16), dim3(256), 0, 0, a, b); });
+    CK(hipDeviceSynchronize());
+    const double gb = 1e9;
+    printf("{\"copy_GBs\": %.1f, \"read_GBs\": %.1f, \"write_GBs\": %.1f, \"rs42_xor_GBs\": %.1f, "
+           "\"rs42_xor_nt_GBs\": %.1f, \"rs42_xor_ms\": %.4f}\n",
+           2.0 * G / (ms_copy * 1e-3) / gb, 1.5 * G / (ms_read * 1e-3) / gb, 1.5 * G / (ms_write * 1e-3) / gb,
+           1.5 * G / (ms_rs * 1e-3) / gb, 1.5 * G / (ms_rsnt * 1e-3) / gb, ms_rs);
+    return 0;
+}

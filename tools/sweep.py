@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""Interleaved A/B sweep of kernel build variants x tile sizes, in ONE process on one GPU
+(cdna_hip_programming.md §5.4 rule 24).  Not product code.
+
+    python tools/sweep.py [--build] [--rounds 5] [--variants base,nt,...] [--us 1,2,4]
+                          [--workload c2|c4]
+
+Each variant is libstorbec_<tag>.so built with the -D knobs in VARIANTS; each (variant, U)
+gets its own Engine (fresh plan).  Prints one JSON line per config: median / min encode and
+decode kernel time (HIP events) and GB/s of algorithmic bytes.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+VARIANTS = {
+    "base": {},  # defaults: nontemporal loads + stores, prefetch
+    "nopf": {"SEC_PREFETCH": 0},
+    "tmp": {"SEC_NT_LOAD": 0, "SEC_NT_STORE": 0},  # temporal (cached) loads and stores
+}
+
+
+def build(tags):
+    from storb_amd import _build
+
+    return {t: _build.build(defines=VARIANTS[t], tag=t) for t in tags}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--variants", default="base,nopf,tmp")
+    ap.add_argument("--us", default="1,2,4")
+    ap.add_argument("--workload", default="c2")
+    a = ap.parse_args()
+    tags = a.variants.split(",")
+    libs = build(tags)
+    if a.build:
+        return
+    import torch
+
+    from bench import dec_descs, enc_descs
+    from storb_amd.engine import Engine
+
+    if a.workload == "c2":
+        nch, n, k, m, erased = 1024, 1 << 20, 4, 6, (1, 3)
+    else:  # c4 per-GPU share: 8192 x 64 KiB RS(10,4)
+        nch, n, k, m, erased = 8192, 65536, 10, 14, (0, 2, 5, 9)
+    src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
+    ed, B = enc_descs(nch, n, k, m)
+    par = torch.empty(nch * (m - k) * B, dtype=torch.uint8, device="cuda")
+    out = torch.empty_like(src)
+    dd, sn, offs = dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), erased)
+    enc_bytes = nch * (n + (m - k) * B)
+    dec_bytes = nch * (k * B + n)
+
+    configs = [(t, int(u)) for t in tags for u in a.us.split(",")]
+    engines = {}
+    for t, u in configs:
+        os.environ["SEC_TILE_U"] = str(u)
+        e = Engine(0, lib_path=libs[t])
+        e.encode_batch(ed, src, par)  # builds + caches this engine's plan with U
+        e.decode_batch(dd, sn, offs, 0, out)
+        assert torch.equal(out, src), (t, u)
+        engines[(t, u)] = e
+    os.environ.pop("SEC_TILE_U", None)
+    samples = {c: ([], []) for c in configs}
+    for _ in range(a.rounds):
+        for c in configs:
+            e = engines[c]
+            e.set_timing(True)
+            for _ in range(a.reps):
+                e.encode_batch(ed, src, par, asynchronous=True)
+            for _ in range(a.reps):
+                e.decode_batch(dd, sn, offs, 0, out, asynchronous=True)
+            e.sync()
+            e.set_timing(False)
+            ms, nl = e.collect_timing("encode")
+            samples[c][0].append(ms / nl)
+            ms, nl = e.collect_timing("decode")
+            samples[c][1].append(ms / nl)
+    for c in configs:
+        enc, dec = np.array(samples[c][0]), np.array(samples[c][1])
+        print(json.dumps({"variant": c[0], "U": c[1], "workload": a.workload,
+                          "enc_ms_med": round(float(np.median(enc)), 4), "enc_GBs": round(enc_bytes / np.median(enc) / 1e6, 1),
+                          "enc_GBs_best": round(enc_bytes / enc.min() / 1e6, 1),
+                          "dec_ms_med": round(float(np.median(dec)), 4), "dec_GBs": round(dec_bytes / np.median(dec) / 1e6, 1),
+                          "dec_GBs_best": round(dec_bytes / dec.min() / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
