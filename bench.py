@@ -73,8 +73,15 @@ def enc_descs(nchunks, n, k, m):
 
 
 def dec_descs(nchunks, n, k, m, B, data_base, par_base, erased):
+    """Decode descriptors whose surviving blocks are read in place from the encode buffers.
+
+    The C ABI needs B readable bytes per block; an in-place data block k-1 is short when
+    padlen > 0 (zfec's padded copy is not in the chunk buffer), so it must be erased then.
+    """
     from storb_amd._lib import DEC_DTYPE
 
+    if B * k != n and (k - 1) not in erased:
+        raise ValueError("padded last data block cannot be read in place: erase block k-1")
     keep = [s for s in range(m) if s not in erased][:k]
     d = np.zeros(nchunks, dtype=DEC_DTYPE)
     d["out_off"] = np.arange(nchunks, dtype=np.uint64) * n

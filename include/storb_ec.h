@@ -132,7 +132,9 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
  * blocks + block_offs[slot0 + i] (B bytes each) with block numbers
  * sharenums[slot0 + i]; the chunk's k*B - padlen bytes are written at
  * out + out_off.  Present primaries are copied, missing ones recovered.
- * `blocks` may be NULL, in which case block_offs are absolute addresses. */
+ * `blocks` may be NULL, in which case block_offs are absolute addresses.
+ * Every block must have B readable bytes: data block k-1 is zfec's zero-padded
+ * copy, so a chunk buffer read in place does not provide it when padlen > 0. */
 int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
                      const int32_t *sharenums, const uint64_t *block_offs,
                      const uint8_t *blocks, uint8_t *out, unsigned flags);

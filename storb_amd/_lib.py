@@ -106,8 +106,10 @@ def load(path: str | None = None) -> ctypes.CDLL:
     return lib
 
 
-def strerror(code: int) -> str:
-    lib = load()
+def strerror(code: int, lib: ctypes.CDLL | None = None) -> str:
+    """Message for a status code; pass the library that returned it (its HIP error text is
+    thread-local per loaded library)."""
+    lib = lib or load()
     msg = lib.sec_strerror(code).decode()
     if code == SEC_EHIP:
         msg += ": " + lib.sec_last_hip_error().decode()

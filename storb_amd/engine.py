@@ -32,10 +32,10 @@ class ECRuntimeError(RuntimeError):
     """Device / runtime failure (no GPU, HIP error, out of memory)."""
 
 
-def check(rc: int) -> None:
+def check(rc: int, lib=None) -> None:
     if rc == 0:
         return
-    msg = _lib.strerror(rc)
+    msg = _lib.strerror(rc, lib)
     if rc in _lib.PRECONDITION_CODES:
         raise Error(msg)
     raise ECRuntimeError(f"libstorbec: {msg} (status {rc})")
@@ -86,6 +86,9 @@ class Engine:
             raise ECRuntimeError(f"cannot create HIP context on device {self.device}: {_lib.strerror(rc)}")
         self._ctx = h
 
+    def _check(self, rc: int) -> None:
+        check(rc, self.lib)
+
     # -- lifecycle / stream / timing ----------------------------------------
     def close(self) -> None:
         if self._ctx:
@@ -101,19 +104,19 @@ class Engine:
     def set_stream(self, stream) -> None:
         """Launch on an external hipStream_t (int handle or torch.cuda.Stream); None = own."""
         h = getattr(stream, "cuda_stream", stream)
-        check(self.lib.sec_ctx_set_stream(self._ctx, h or None))
+        self._check(self.lib.sec_ctx_set_stream(self._ctx, h or None))
 
     def sync(self) -> None:
-        check(self.lib.sec_sync(self._ctx))
+        self._check(self.lib.sec_sync(self._ctx))
 
     def set_timing(self, enable: bool) -> None:
-        check(self.lib.sec_ctx_set_timing(self._ctx, int(bool(enable))))
+        self._check(self.lib.sec_ctx_set_timing(self._ctx, int(bool(enable))))
 
     def collect_timing(self, kind: str) -> tuple[float, int]:
         """(summed kernel ms, launch count) recorded since the last collect; kind 'encode'|'decode'."""
         ms = ctypes.c_double(0)
         n = ctypes.c_int64(0)
-        check(self.lib.sec_timing_collect(self._ctx, {"encode": 0, "decode": 1}[kind], ctypes.byref(ms),
+        self._check(self.lib.sec_timing_collect(self._ctx, {"encode": 0, "decode": 1}[kind], ctypes.byref(ms),
                                           ctypes.byref(n)))
         return ms.value, n.value
 
@@ -123,7 +126,7 @@ class Engine:
         s, _ks = addr(src)
         p, _kp = addr(parity)
         flags = (SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0)
-        check(self.lib.sec_encode_batch(self._ctx, _ptr(descs), len(descs), s or None, p or None, flags))
+        self._check(self.lib.sec_encode_batch(self._ctx, _ptr(descs), len(descs), s or None, p or None, flags))
 
     def decode_batch(self, descs: np.ndarray, sharenums: np.ndarray, block_offs: np.ndarray, blocks, out, *,
                      host: bool = False, asynchronous: bool = False) -> None:
@@ -133,7 +136,7 @@ class Engine:
         b, _kb = addr(blocks)
         o, _ko = addr(out)
         flags = (SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0)
-        check(self.lib.sec_decode_batch(self._ctx, _ptr(descs), len(descs), _ptr(sn), _ptr(bo), b or None,
+        self._check(self.lib.sec_decode_batch(self._ctx, _ptr(descs), len(descs), _ptr(sn), _ptr(bo), b or None,
                                         o or None, flags))
 
     # -- host batches ---------------------------------------------------------

@@ -140,7 +140,9 @@ def _enc_descs(nchunks, n, k, m):
 
 
 def _dec_inputs(nchunks, n, k, m, B, erased, data_base, par_base):
-    """Descriptors reading the surviving blocks straight from the encoded device buffers."""
+    """Descriptors reading the surviving blocks straight from the encoded device buffers
+    (an in-place last data block is short by padlen bytes, so it must be among the erased)."""
+    assert B * k == n or (k - 1) in erased
     keep = [s for s in range(m) if s not in erased][:k]
     d = np.zeros(nchunks, dtype=DEC_DTYPE)
     d["out_off"] = np.arange(nchunks, dtype=np.uint64) * n

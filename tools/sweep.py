@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="base,nopf,tmp")
     ap.add_argument("--us", default="1,2,4")
-    ap.add_argument("--workload", default="c2")
+    ap.add_argument("--workload", default="c2", help="c2 | c4 | nch,n,k,m (custom shape)")
     a = ap.parse_args()
     tags = a.variants.split(",")
     libs = build(tags)
@@ -55,8 +55,11 @@ def main():
 
     if a.workload == "c2":
         nch, n, k, m, erased = 1024, 1 << 20, 4, 6, (1, 3)
-    else:  # c4 per-GPU share: 8192 x 64 KiB RS(10,4)
+    elif a.workload == "c4":  # per-GPU share: 8192 x 64 KiB RS(10,4)
         nch, n, k, m, erased = 8192, 65536, 10, 14, (0, 2, 5, 9)
+    else:
+        nch, n, k, m = map(int, a.workload.split(","))
+        erased = ((k - 1,) + tuple(range(0, k - 1, 2)))[: m - k]  # k-1 first: see bench.dec_descs
     src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
     ed, B = enc_descs(nch, n, k, m)
     par = torch.empty(nch * (m - k) * B, dtype=torch.uint8, device="cuda")
