@@ -103,7 +103,6 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct Group {
     int rows, U;
-    bool edge;
     uint32_t first, count;
 };
 
@@ -120,8 +119,9 @@ struct Plan {
     std::vector<uint8_t> key;
     uint64_t gen_enc = 0, gen_dec = 0;
     std::vector<Group> groups;
-    DevBuf meta;  // device copy of descriptors, tiles, slot arrays
-    size_t off_desc = 0, off_tiles = 0, off_soff = 0, off_srow = 0, off_mrow = 0;
+    DevBuf meta;  // device copy of descriptors, tiles, tail items, slot arrays
+    size_t off_desc = 0, off_tiles = 0, off_tail = 0, off_soff = 0, off_srow = 0, off_mrow = 0;
+    uint32_t ntail = 0;
     // host-mode bookkeeping
     size_t dev_in_bytes = 0, dev_out_bytes = 0;
     bool valid = false;
@@ -142,28 +142,47 @@ int pick_u(uint64_t B, int rows)
     return 1;
 }
 
-// Tiles for one chunk: full tiles over [0, valid) in steps of 4 KiB * U,
-// U=1 edge tiles over the rest of [0, B).  `valid` = positions where every
-// block (incl. the zero-padded last data block) is readable in full.
-void add_tiles(std::map<std::tuple<int, int, bool>, std::vector<sec::Tile>> &bins, uint32_t chunk, uint64_t B,
-               int64_t valid, int rows_total)
+using Bins = std::map<std::pair<int, int>, std::vector<sec::Tile>>;
+
+// Work for one chunk.  `valid` = positions where every block is fully readable and
+// every output row writable (the last data block's length, clamped to [0, B]).
+// Tiles of 4 KiB * U cover [0, valid); a ragged remainder gets U = 1 tiles whose
+// lanes clamp to end at `valid`.  Positions [valid, B) — or all of [0, B) when
+// valid < 16 — become one-thread tail items (at most padlen per normal chunk).
+void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B, int64_t valid,
+              int rows_total)
 {
     if (B == 0)
         return;
     valid = std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)B));
+    const uint64_t v = valid >= sec::kLaneBytes ? (uint64_t)valid : 0;
     const int ngroups = rows_total == 0 ? 1 : (rows_total + sec::kMaxRows - 1) / sec::kMaxRows;
-    for (int g = 0; g < ngroups; ++g) {
-        const int r0 = g * sec::kMaxRows;
-        const int rows = std::min(sec::kMaxRows, rows_total - r0);
-        const int U = pick_u(B, rows);
-        const uint64_t step = (uint64_t)sec::kStepBytes * U;
-        const uint64_t nfull = (uint64_t)valid / step;
-        auto &full = bins[std::make_tuple(rows, U, false)];
-        for (uint64_t i = 0; i < nfull; ++i)
-            full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
-        auto &edge = bins[std::make_tuple(rows, 1, true)];
-        for (uint64_t t0 = nfull * step; t0 < B; t0 += sec::kStepBytes)
-            edge.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
+    if (v > 0)
+        for (int g = 0; g < ngroups; ++g) {
+            const int r0 = g * sec::kMaxRows;
+            const int rows = std::min(sec::kMaxRows, rows_total - r0);
+            const int U = pick_u(B, rows);
+            const uint64_t step = (uint64_t)sec::kStepBytes * U;
+            const uint64_t nfull = v / step;
+            auto &full = bins[{rows, U}];
+            for (uint64_t i = 0; i < nfull; ++i)
+                full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
+            auto &rest = bins[{rows, 1}];
+            for (uint64_t t0 = nfull * step; t0 < v; t0 += sec::kStepBytes)
+                rest.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
+        }
+    for (uint64_t t = v; t < B; ++t)
+        tail.push_back(sec::TailItem{chunk, (uint32_t)t});
+}
+
+void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile> &tiles)
+{
+    groups.clear();
+    for (auto &kv : bins) {
+        if (kv.second.empty())
+            continue;
+        groups.push_back(Group{kv.first.first, kv.first.second, (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
+        tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
     }
 }
 
@@ -585,9 +604,10 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
                 return rc;
         }
 
-        // descriptors + tiles
+        // descriptors + tiles + tail items
         std::vector<sec::EncDesc> descs((size_t)nchunks);
-        std::map<std::tuple<int, int, bool>, std::vector<sec::Tile>> bins;
+        Bins bins;
+        std::vector<sec::TailItem> tail;
         uint64_t dense = 0, idense = 0;
         for (int64_t i = 0; i < nchunks; ++i) {
             const sec_enc_chunk &c = chunks[i];
@@ -598,31 +618,28 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
             idense += c.n;
             d.par_off = host ? dense : c.parity_off;
             d.par_stride = host ? B : c.parity_stride;
-            d.n = c.n;
+            const int64_t valid = (int64_t)c.n - (int64_t)(c.k - 1) * (int64_t)B;
             d.B = (uint32_t)B;
             d.k = (uint32_t)c.k;
             d.p = (uint32_t)p;
             d.tab = tab_of[i];
+            d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)B));
+            d.pad = 0;
             dense += (uint64_t)p * B;
             if (p > 0)
-                add_tiles(bins, (uint32_t)i, B, (int64_t)c.n - (int64_t)(c.k - 1) * (int64_t)B, p);
+                add_work(bins, tail, (uint32_t)i, B, valid, p);
         }
-        plan.groups.clear();
         std::vector<sec::Tile> tiles;
-        for (auto &kv : bins) {
-            if (kv.second.empty())
-                continue;
-            plan.groups.push_back(Group{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first),
-                                        (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
-            tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
-        }
-        // metadata image: [descs][tiles][coefs]
+        flatten(bins, plan.groups, tiles);
+        plan.ntail = (uint32_t)tail.size();
+        // metadata image: [descs][tiles][tail][coefs]
         size_t coef_bytes = 0;
         for (auto &pe : pending)
             coef_bytes += pe.coef.size();
         plan.off_desc = 0;
         plan.off_tiles = align_up(descs.size() * sizeof(sec::EncDesc), 256);
-        const size_t off_coef = align_up(plan.off_tiles + tiles.size() * sizeof(sec::Tile), 256);
+        plan.off_tail = align_up(plan.off_tiles + tiles.size() * sizeof(sec::Tile), 256);
+        const size_t off_coef = align_up(plan.off_tail + tail.size() * sizeof(sec::TailItem), 256);
         const size_t bytes = off_coef + coef_bytes;
         rc = pin_wait(ctx);
         if (!rc)
@@ -632,6 +649,7 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
         char *img = (char *)ctx->pin.p;
         memcpy(img + plan.off_desc, descs.data(), descs.size() * sizeof(sec::EncDesc));
         memcpy(img + plan.off_tiles, tiles.data(), tiles.size() * sizeof(sec::Tile));
+        memcpy(img + plan.off_tail, tail.data(), tail.size() * sizeof(sec::TailItem));
         size_t o = off_coef;
         for (auto &pe : pending) {
             memcpy(img + o, pe.coef.data(), pe.coef.size());
@@ -683,10 +701,16 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
     const sec::EncDesc *dd = plan.meta.as<sec::EncDesc>(plan.off_desc);
     const sec::Tile *dt = plan.meta.as<sec::Tile>(plan.off_tiles);
     for (const Group &g : plan.groups) {
-        int e = sec_launch_encode(g.rows, g.U, g.edge, d_in, d_par, dd, dt + g.first, g.count,
+        int e = sec_launch_encode(g.rows, g.U, d_in, d_par, dd, dt + g.first, g.count,
                                   ctx->enc_tabs.buf.as<uint32_t>(), ctx->stream());
         if (e)
             return hip_fail((hipError_t)e, "sec_encode_kernel");
+    }
+    if (plan.ntail) {
+        int e = sec_launch_encode_tail(d_in, d_par, dd, plan.meta.as<sec::TailItem>(plan.off_tail), plan.ntail,
+                                       ctx->enc_tabs.buf.as<uint32_t>(), ctx->stream());
+        if (e)
+            return hip_fail((hipError_t)e, "sec_encode_tail");
     }
     rc = timing_end(ctx, t0, 0);
     if (rc)
@@ -839,7 +863,8 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         std::vector<sec::DecDesc> descs((size_t)nchunks);
         std::vector<uint64_t> soff(perm_all.size());
         std::vector<uint32_t> srow(perm_all.size()), mrow(perm_all.size(), 0);
-        std::map<std::tuple<int, int, bool>, std::vector<sec::Tile>> bins;
+        Bins bins;
+        std::vector<sec::TailItem> tail;
         uint64_t in_dense = 0, out_dense = 0;
         for (int64_t i = 0; i < nchunks; ++i) {
             const sec_dec_chunk &c = chunks[i];
@@ -862,27 +887,23 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
             d.e = e_of[i];
             d.tab = tab_of[i];
             d.slot0 = (uint32_t)base;
-            d.pad = 0;
+            const int64_t valid = (int64_t)nout - (int64_t)(c.k - 1) * (int64_t)c.B;
+            d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)c.B));
             in_dense += (uint64_t)c.k * c.B;
             out_dense += nout;
             if (nout > 0)
-                add_tiles(bins, (uint32_t)i, c.B, (int64_t)nout - (int64_t)(c.k - 1) * (int64_t)c.B, (int)e_of[i]);
+                add_work(bins, tail, (uint32_t)i, c.B, valid, (int)e_of[i]);
         }
-        plan.groups.clear();
         std::vector<sec::Tile> tiles;
-        for (auto &kv : bins) {
-            if (kv.second.empty())
-                continue;
-            plan.groups.push_back(Group{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first),
-                                        (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
-            tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
-        }
+        flatten(bins, plan.groups, tiles);
+        plan.ntail = (uint32_t)tail.size();
         size_t coef_bytes = 0;
         for (auto &pe : pending)
             coef_bytes += pe.coef.size();
         plan.off_desc = 0;
         plan.off_tiles = align_up(descs.size() * sizeof(sec::DecDesc), 256);
-        plan.off_soff = align_up(plan.off_tiles + tiles.size() * sizeof(sec::Tile), 256);
+        plan.off_tail = align_up(plan.off_tiles + tiles.size() * sizeof(sec::Tile), 256);
+        plan.off_soff = align_up(plan.off_tail + tail.size() * sizeof(sec::TailItem), 256);
         plan.off_srow = align_up(plan.off_soff + soff.size() * 8, 256);
         plan.off_mrow = align_up(plan.off_srow + srow.size() * 4, 256);
         const size_t off_coef = align_up(plan.off_mrow + mrow.size() * 4, 256);
@@ -895,6 +916,7 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         char *img = (char *)ctx->pin.p;
         memcpy(img + plan.off_desc, descs.data(), descs.size() * sizeof(sec::DecDesc));
         memcpy(img + plan.off_tiles, tiles.data(), tiles.size() * sizeof(sec::Tile));
+        memcpy(img + plan.off_tail, tail.data(), tail.size() * sizeof(sec::TailItem));
         memcpy(img + plan.off_soff, soff.data(), soff.size() * 8);
         memcpy(img + plan.off_srow, srow.data(), srow.size() * 4);
         memcpy(img + plan.off_mrow, mrow.data(), mrow.size() * 4);
@@ -951,12 +973,20 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
     const sec::DecDesc *dd = plan.meta.as<sec::DecDesc>(plan.off_desc);
     const sec::Tile *dt = plan.meta.as<sec::Tile>(plan.off_tiles);
     for (const Group &g : plan.groups) {
-        int e = sec_launch_decode(g.rows, g.U, g.edge, d_blocks, d_out, dd, dt + g.first, g.count,
+        int e = sec_launch_decode(g.rows, g.U, d_blocks, d_out, dd, dt + g.first, g.count,
                                   ctx->dec_tabs.buf.as<uint32_t>(), plan.meta.as<uint64_t>(plan.off_soff),
                                   plan.meta.as<uint32_t>(plan.off_srow), plan.meta.as<uint32_t>(plan.off_mrow),
                                   ctx->stream());
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_kernel");
+    }
+    if (plan.ntail) {
+        int e = sec_launch_decode_tail(d_blocks, d_out, dd, plan.meta.as<sec::TailItem>(plan.off_tail), plan.ntail,
+                                       ctx->dec_tabs.buf.as<uint32_t>(), plan.meta.as<uint64_t>(plan.off_soff),
+                                       plan.meta.as<uint32_t>(plan.off_srow), plan.meta.as<uint32_t>(plan.off_mrow),
+                                       ctx->stream());
+        if (e)
+            return hip_fail((hipError_t)e, "sec_decode_tail");
     }
     rc = timing_end(ctx, t0, 1);
     if (rc)

@@ -23,7 +23,8 @@
 //     wave reads one coalesced 1 KiB run from each of the k blocks; block
 //     starts that are not 16 B aligned (B % 16 != 0) use the hardware's
 //     unaligned dwordx4 access; the last data block's zero padding is
-//     synthesised for the few edge lanes, never read.
+//     synthesised by the byte-granular tail kernels (at most padlen positions per
+//     chunk), never read.
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
@@ -147,34 +148,21 @@ __device__ __forceinline__ void store16(u8 *p, u32x4 v)
 #endif
 }
 
-// bytes [pos, pos+16) of a row, zero at and beyond `lim`
-__device__ __forceinline__ u32x4 load_edge(const u8 *row, u32 pos, int64_t lim)
+// GF(2^8) product of one byte through the same 5-dword table (tail kernels)
+__device__ __forceinline__ u32 gf_mul_byte(const u32 *__restrict__ t, u32 x)
 {
-    u32x4 v = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int b = 0; b < 16; ++b)
-        if ((int64_t)pos + b < lim)
-            v[b >> 2] |= (u32)row[pos + b] << (8 * (b & 3));
-    return v;
-}
-
-__device__ __forceinline__ void store_edge(u8 *row, u32 pos, int64_t lim, u32x4 v)
-{
-#pragma unroll
-    for (int b = 0; b < 16; ++b)
-        if ((int64_t)pos + b < lim)
-            row[pos + b] = (u8)(v[b >> 2] >> (8 * (b & 3)));
-}
-
-__device__ __forceinline__ int64_t row_limit(uint64_t n, u32 B, u32 row)
-{
-    const int64_t l = (int64_t)n - (int64_t)row * B;
-    return l < 0 ? 0 : (l > (int64_t)B ? (int64_t)B : l);
+    return (__builtin_amdgcn_perm(t[1], t[0], x & 7u) ^ __builtin_amdgcn_perm(t[3], t[2], (x >> 3) & 7u) ^
+            __builtin_amdgcn_perm(t[4], t[4], x >> 6)) & 0xFFu;
 }
 
 // ---- encode ----------------------------------------------------------------
-// grid = tiles of one row-group size R; tile = (chunk, t0, r0).
-template <int R, int U, bool EDGE>
+// Tile = (chunk, t0, r0): lanes cover t0 + 16*lane + 4096*u.  Every position handled here
+// is < `valid` (all k blocks fully readable there, including the last, shorter data
+// block); a lane's 16 bytes are clamped to end at `valid`, so the last lane of a ragged
+// chunk overlaps its neighbour (identical bytes written twice) instead of taking a
+// byte-granular path.  Positions in [valid, B) — at most padlen of them — belong to
+// sec_encode_tail.
+template <int R, int U>
 __global__ __launch_bounds__(256) void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
                                                          const sec::EncDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
@@ -182,11 +170,15 @@ __global__ __launch_bounds__(256) void sec_encode_kernel(const u8 *__restrict__ 
 {
     const sec::Tile tl = tiles[blockIdx.x];
     const sec::EncDesc d = descs[tl.chunk];
-    const u32 B = d.B, k = d.k;
-    const u32 tbase = tl.t0 + threadIdx.x * sec::kLaneBytes;
-    if (tbase >= B)
+    const u32 B = d.B, k = d.k, valid = d.valid;
+    const u32 t = tl.t0 + threadIdx.x * sec::kLaneBytes;
+    if (t >= valid)
         return;
-    const u8 *src = in + d.in_off;
+    u32 pos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        pos[u] = min(t + u * sec::kStepBytes, valid - sec::kLaneBytes);
+    const u8 *row = in + d.in_off;
     u8 *dst = par + d.par_off + (u64)tl.r0 * d.par_stride;
     const u32 *tj = tabs + d.tab + tl.r0 * sec::kTabDwords;
     const u32 tstep = d.p * sec::kTabDwords;
@@ -198,58 +190,60 @@ __global__ __launch_bounds__(256) void sec_encode_kernel(const u8 *__restrict__ 
         for (int u = 0; u < U; ++u)
             acc[r][u] = u32x4{0u, 0u, 0u, 0u};
 
-    const u32 tlast = tbase + (U - 1) * sec::kStepBytes + sec::kLaneBytes;
-    const bool full = !EDGE || (tlast <= B && (u64)(k - 1) * B + tlast <= d.n);
-    if (full) {
 #if SEC_PREFETCH
-        const u8 *row = src + tbase;
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        x[u] = load16(row + pos[u]);
+    for (u32 j = 0; j < k; ++j, tj += tstep) {
+        u32x4 xn[U];
+        row += B;
+        if (j + 1 < k) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                xn[u] = load16(row + pos[u]);
+        }
+        gf_mac<R, U>(acc, x, tj);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            x[u] = xn[u];
+    }
+#else
+    for (u32 j = 0; j < k; ++j, tj += tstep, row += B) {
         u32x4 x[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            x[u] = load16(row + u * sec::kStepBytes);
-        for (u32 j = 0; j < k; ++j, tj += tstep) {
-            u32x4 xn[U];
-            row += B;
-            if (j + 1 < k) {
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    xn[u] = load16(row + u * sec::kStepBytes);
-            }
-            gf_mac<R, U>(acc, x, tj);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                x[u] = xn[u];
-        }
-#else
-        for (u32 j = 0; j < k; ++j, tj += tstep) {
-            const u8 *row = src + (u64)j * B + tbase;
-            u32x4 x[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                x[u] = load16(row + u * sec::kStepBytes);
-            gf_mac<R, U>(acc, x, tj);
-        }
+            x[u] = load16(row + pos[u]);
+        gf_mac<R, U>(acc, x, tj);
+    }
 #endif
 #pragma unroll
-        for (int r = 0; r < R; ++r)
+    for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                store16(dst + (u64)r * d.par_stride + tbase + u * sec::kStepBytes, acc[r][u]);
-    } else if constexpr (EDGE) {
-        for (u32 j = 0; j < k; ++j, tj += tstep) {
-            const u8 *row = src + (u64)j * B;
-            const int64_t lim = row_limit(d.n, B, j);
-            u32x4 x[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                x[u] = load_edge(row, tbase + u * sec::kStepBytes, lim);
-            gf_mac<R, U>(acc, x, tj);
+        for (int u = 0; u < U; ++u)
+            store16(dst + (u64)r * d.par_stride + pos[u], acc[r][u]);
+}
+
+// One thread per (chunk, position) in [valid, B) — or [0, B) for chunks with valid < 16:
+// all p parity bytes at that position, the last block's padding read as zero.
+__global__ __launch_bounds__(256) void sec_encode_tail(const u8 *__restrict__ in, u8 *__restrict__ par,
+                                                       const sec::EncDesc *__restrict__ descs,
+                                                       const sec::TailItem *__restrict__ items, u32 nitems,
+                                                       const u32 *__restrict__ tabs)
+{
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nitems)
+        return;
+    const sec::TailItem it = items[i];
+    const sec::EncDesc d = descs[it.chunk];
+    const u8 *src = in + d.in_off + it.t;
+    for (u32 r = 0; r < d.p; ++r) {
+        u32 acc = 0;
+        for (u32 j = 0; j < d.k; ++j) {
+            const u32 x = (j + 1 < d.k || it.t < d.valid) ? (u32)src[(u64)j * d.B] : 0u;
+            acc ^= gf_mul_byte(tabs + d.tab + (j * d.p + r) * sec::kTabDwords, x);
         }
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                store_edge(dst + (u64)r * d.par_stride, tbase + u * sec::kStepBytes, B, acc[r][u]);
+        par[d.par_off + (u64)r * d.par_stride + it.t] = (u8)acc;
     }
 }
 
@@ -257,7 +251,9 @@ __global__ __launch_bounds__(256) void sec_encode_kernel(const u8 *__restrict__ 
 // Slot c of a chunk holds block number idx[c]; primaries sit in their own slot
 // (zfec's normalisation).  Present primaries are copied to their output row;
 // the R missing rows of this tile's row group are XOR_c Minv[row][c] * slot_c.
-template <int R, int U, bool EDGE>
+// Positions are < valid = the last output row's length, so every row is writable
+// and every slot (always B bytes) readable; the rest goes to sec_decode_tail.
+template <int R, int U>
 __global__ __launch_bounds__(256) void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                          const sec::DecDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
@@ -268,10 +264,14 @@ __global__ __launch_bounds__(256) void sec_decode_kernel(const u8 *__restrict__ 
 {
     const sec::Tile tl = tiles[blockIdx.x];
     const sec::DecDesc d = descs[tl.chunk];
-    const u32 B = d.B, k = d.k;
-    const u32 tbase = tl.t0 + threadIdx.x * sec::kLaneBytes;
-    if (tbase >= B)
+    const u32 B = d.B, k = d.k, valid = d.valid;
+    const u32 t = tl.t0 + threadIdx.x * sec::kLaneBytes;
+    if (t >= valid)
         return;
+    u32 pos[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        pos[u] = min(t + u * sec::kStepBytes, valid - sec::kLaneBytes);
     u8 *dst = out + d.out_off;
     const bool copies = tl.r0 == 0;  // row group 0 also copies the present primaries
     const u32 *tj = tabs + d.tab + tl.r0 * sec::kTabDwords;
@@ -284,131 +284,127 @@ __global__ __launch_bounds__(256) void sec_decode_kernel(const u8 *__restrict__ 
         for (int u = 0; u < U; ++u)
             acc[r][u] = u32x4{0u, 0u, 0u, 0u};
 
-    const u32 tlast = tbase + (U - 1) * sec::kStepBytes + sec::kLaneBytes;
-    const bool full = !EDGE || (tlast <= B && (u64)(k - 1) * B + tlast <= d.n);
-#if SEC_PREFETCH
-    if constexpr (!EDGE) {
-        // every slot is read (R > 0) or copied (R == 0: all primaries present)
-        u32x4 x[U];
-        {
-            const u8 *s = blocks + slot_off[d.slot0] + tbase;
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                x[u] = load16(s + u * sec::kStepBytes);
-        }
-        for (u32 c = 0; c < k; ++c, tj += tstep) {
-            u32x4 xn[U];
-            if (c + 1 < k) {
-                const u8 *s = blocks + slot_off[d.slot0 + c + 1] + tbase;
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    xn[u] = load16(s + u * sec::kStepBytes);
-            }
-            const u32 orow = slot_row[d.slot0 + c];
-            if (copies && orow != 0xFFFFFFFFu) {
-                u8 *o = dst + (u64)orow * B + tbase;
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    store16(o + u * sec::kStepBytes, x[u]);
-            }
-            if constexpr (R > 0)
-                gf_mac<R, U>(acc, x, tj);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                x[u] = xn[u];
-        }
-    } else
-#endif
-    for (u32 c = 0; c < k; ++c, tj += tstep) {
-        const u32 orow = slot_row[d.slot0 + c];
-        const bool copy = copies && orow != 0xFFFFFFFFu;
-        if (R == 0 && !copy)
-            continue;
-        const u8 *s = blocks + slot_off[d.slot0 + c] + tbase;
-        u32x4 x[U];
+    // every slot is read (R > 0) or copied (R == 0: all primaries present)
+    u32x4 x[U];
+    {
+        const u8 *s = blocks + slot_off[d.slot0];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            x[u] = (!EDGE || full) ? load16(s + u * sec::kStepBytes) : load_edge(s, u * sec::kStepBytes, (int64_t)B - tbase);
-        if (copy) {
-            u8 *o = dst + (u64)orow * B;
-            const int64_t lim = row_limit(d.n, B, orow);
+            x[u] = load16(s + pos[u]);
+    }
+    for (u32 c = 0; c < k; ++c, tj += tstep) {
+        u32x4 xn[U];
+        if (c + 1 < k) {
+            const u8 *s = blocks + slot_off[d.slot0 + c + 1];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (!EDGE || full)
-                    store16(o + tbase + u * sec::kStepBytes, x[u]);
-                else
-                    store_edge(o, tbase + u * sec::kStepBytes, lim, x[u]);
-            }
+            for (int u = 0; u < U; ++u)
+                xn[u] = load16(s + pos[u]);
+        }
+        const u32 orow = slot_row[d.slot0 + c];
+        if (copies && orow != 0xFFFFFFFFu) {
+            u8 *o = dst + (u64)orow * B;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                store16(o + pos[u], x[u]);
         }
         if constexpr (R > 0)
             gf_mac<R, U>(acc, x, tj);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            x[u] = xn[u];
     }
     if constexpr (R > 0) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const u32 orow = miss_row[d.slot0 + tl.r0 + r];
-            u8 *o = dst + (u64)orow * B;
-            const int64_t lim = row_limit(d.n, B, orow);
+            u8 *o = dst + (u64)miss_row[d.slot0 + tl.r0 + r] * B;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (!EDGE || full)
-                    store16(o + tbase + u * sec::kStepBytes, acc[r][u]);
-                else
-                    store_edge(o, tbase + u * sec::kStepBytes, lim, acc[r][u]);
-            }
+            for (int u = 0; u < U; ++u)
+                store16(o + pos[u], acc[r][u]);
         }
     }
 }
 
-template <int R, int U, bool EDGE>
+// One thread per (chunk, position) outside the main kernel's range: copies and
+// recovered bytes for every output row that is still inside the chunk there.
+__global__ __launch_bounds__(256) void sec_decode_tail(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+                                                       const sec::DecDesc *__restrict__ descs,
+                                                       const sec::TailItem *__restrict__ items, u32 nitems,
+                                                       const u32 *__restrict__ tabs,
+                                                       const u64 *__restrict__ slot_off,
+                                                       const u32 *__restrict__ slot_row,
+                                                       const u32 *__restrict__ miss_row)
+{
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nitems)
+        return;
+    const sec::TailItem it = items[i];
+    const sec::DecDesc d = descs[it.chunk];
+    u8 *dst = out + d.out_off + it.t;
+    for (u32 c = 0; c < d.k; ++c) {
+        const u32 orow = slot_row[d.slot0 + c];
+        if (orow != 0xFFFFFFFFu && (u64)orow * d.B + it.t < d.n)
+            dst[(u64)orow * d.B] = blocks[slot_off[d.slot0 + c] + it.t];
+    }
+    for (u32 r = 0; r < d.e; ++r) {
+        const u32 orow = miss_row[d.slot0 + r];
+        if ((u64)orow * d.B + it.t >= d.n)
+            continue;
+        u32 acc = 0;
+        for (u32 c = 0; c < d.k; ++c)
+            acc ^= gf_mul_byte(tabs + d.tab + (c * d.e + r) * sec::kTabDwords,
+                               (u32)blocks[slot_off[d.slot0 + c] + it.t]);
+        dst[(u64)orow * d.B] = (u8)acc;
+    }
+}
+
+template <int R, int U>
 hipError_t launch_enc(const u8 *in, u8 *par, const sec::EncDesc *descs, const sec::Tile *tiles, u32 ntiles,
                       const u32 *tabs, hipStream_t s)
 {
-    hipLaunchKernelGGL((sec_encode_kernel<R, U, EDGE>), dim3(ntiles), dim3(sec::kLanes), 0, s, in, par, descs, tiles,
-                       tabs);
+    hipLaunchKernelGGL((sec_encode_kernel<R, U>), dim3(ntiles), dim3(sec::kLanes), 0, s, in, par, descs, tiles, tabs);
     return hipGetLastError();
 }
 
-template <int R, int U, bool EDGE>
+template <int R, int U>
 hipError_t launch_dec(const u8 *blocks, u8 *out, const sec::DecDesc *descs, const sec::Tile *tiles, u32 ntiles,
                       const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, hipStream_t s)
 {
-    hipLaunchKernelGGL((sec_decode_kernel<R, U, EDGE>), dim3(ntiles), dim3(sec::kLanes), 0, s, blocks, out, descs, tiles,
+    hipLaunchKernelGGL((sec_decode_kernel<R, U>), dim3(ntiles), dim3(sec::kLanes), 0, s, blocks, out, descs, tiles,
                        tabs, so, sr, mr);
     return hipGetLastError();
 }
 
-template <int U, bool EDGE>
+template <int U>
 hipError_t dispatch_enc(int rows, const u8 *in, u8 *par, const sec::EncDesc *d, const sec::Tile *t, u32 nt,
                         const u32 *tabs, hipStream_t s)
 {
     switch (rows) {
-    case 1: return launch_enc<1, U, EDGE>(in, par, d, t, nt, tabs, s);
-    case 2: return launch_enc<2, U, EDGE>(in, par, d, t, nt, tabs, s);
-    case 3: return launch_enc<3, U, EDGE>(in, par, d, t, nt, tabs, s);
-    case 4: return launch_enc<4, U, EDGE>(in, par, d, t, nt, tabs, s);
-    case 5: return launch_enc<5, U, EDGE>(in, par, d, t, nt, tabs, s);
-    case 6: return launch_enc<6, U, EDGE>(in, par, d, t, nt, tabs, s);
-    case 7: return launch_enc<7, U, EDGE>(in, par, d, t, nt, tabs, s);
-    case 8: return launch_enc<8, U, EDGE>(in, par, d, t, nt, tabs, s);
+    case 1: return launch_enc<1, U>(in, par, d, t, nt, tabs, s);
+    case 2: return launch_enc<2, U>(in, par, d, t, nt, tabs, s);
+    case 3: return launch_enc<3, U>(in, par, d, t, nt, tabs, s);
+    case 4: return launch_enc<4, U>(in, par, d, t, nt, tabs, s);
+    case 5: return launch_enc<5, U>(in, par, d, t, nt, tabs, s);
+    case 6: return launch_enc<6, U>(in, par, d, t, nt, tabs, s);
+    case 7: return launch_enc<7, U>(in, par, d, t, nt, tabs, s);
+    case 8: return launch_enc<8, U>(in, par, d, t, nt, tabs, s);
     default: return hipErrorInvalidValue;
     }
 }
 
-template <int U, bool EDGE>
+template <int U>
 hipError_t dispatch_dec(int rows, const u8 *b, u8 *o, const sec::DecDesc *d, const sec::Tile *t, u32 nt,
                         const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, hipStream_t s)
 {
     switch (rows) {
-    case 0: return launch_dec<0, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 1: return launch_dec<1, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 2: return launch_dec<2, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 3: return launch_dec<3, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 4: return launch_dec<4, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 5: return launch_dec<5, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 6: return launch_dec<6, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 7: return launch_dec<7, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 8: return launch_dec<8, U, EDGE>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 0: return launch_dec<0, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 1: return launch_dec<1, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 2: return launch_dec<2, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 3: return launch_dec<3, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 4: return launch_dec<4, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 5: return launch_dec<5, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 6: return launch_dec<6, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 7: return launch_dec<7, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 8: return launch_dec<8, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -424,21 +420,31 @@ int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void 
     return hipGetLastError();
 }
 
-int sec_launch_encode(int rows, int U, bool edge, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
+int sec_launch_encode(int rows, int U, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
                       const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, void *stream)
 {
     if (ntiles == 0)
         return hipSuccess;
     hipStream_t s = (hipStream_t)stream;
     switch (U) {
-    case 1: return edge ? dispatch_enc<1, true>(rows, in, par, descs, tiles, ntiles, tabs, s) : dispatch_enc<1, false>(rows, in, par, descs, tiles, ntiles, tabs, s);
-    case 2: return edge ? dispatch_enc<2, true>(rows, in, par, descs, tiles, ntiles, tabs, s) : dispatch_enc<2, false>(rows, in, par, descs, tiles, ntiles, tabs, s);
-    case 4: return edge ? dispatch_enc<4, true>(rows, in, par, descs, tiles, ntiles, tabs, s) : dispatch_enc<4, false>(rows, in, par, descs, tiles, ntiles, tabs, s);
+    case 1: return dispatch_enc<1>(rows, in, par, descs, tiles, ntiles, tabs, s);
+    case 2: return dispatch_enc<2>(rows, in, par, descs, tiles, ntiles, tabs, s);
+    case 4: return dispatch_enc<4>(rows, in, par, descs, tiles, ntiles, tabs, s);
     default: return hipErrorInvalidValue;
     }
 }
 
-int sec_launch_decode(int rows, int U, bool edge, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
+int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
+                           uint32_t nitems, const uint32_t *tabs, void *stream)
+{
+    if (nitems == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_encode_tail, dim3((nitems + 255) / 256), dim3(256), 0, (hipStream_t)stream, in, par, descs,
+                       items, nitems, tabs);
+    return hipGetLastError();
+}
+
+int sec_launch_decode(int rows, int U, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
                       const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, const uint64_t *slot_off,
                       const uint32_t *slot_row, const uint32_t *miss_row, void *stream)
 {
@@ -446,9 +452,21 @@ int sec_launch_decode(int rows, int U, bool edge, const uint8_t *blocks, uint8_t
         return hipSuccess;
     hipStream_t s = (hipStream_t)stream;
     switch (U) {
-    case 1: return edge ? dispatch_dec<1, true>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s) : dispatch_dec<1, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
-    case 2: return edge ? dispatch_dec<2, true>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s) : dispatch_dec<2, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
-    case 4: return edge ? dispatch_dec<4, true>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s) : dispatch_dec<4, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
+    case 1: return dispatch_dec<1>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
+    case 2: return dispatch_dec<2>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
+    case 4: return dispatch_dec<4>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+int sec_launch_decode_tail(const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
+                           const sec::TailItem *items, uint32_t nitems, const uint32_t *tabs,
+                           const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,
+                           void *stream)
+{
+    if (nitems == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_decode_tail, dim3((nitems + 255) / 256), dim3(256), 0, (hipStream_t)stream, blocks, out,
+                       descs, items, nitems, tabs, slot_off, slot_row, miss_row);
+    return hipGetLastError();
 }

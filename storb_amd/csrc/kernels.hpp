@@ -1,11 +1,13 @@
 // kernels.hpp — device-side descriptors shared by kernels.hip and api.cpp.
 //
 // Work decomposition.  A "tile" is one workgroup of 256 lanes over a run of
-// 256*16*U consecutive byte positions t of ONE chunk's blocks (U = 1 or 4), and
-// a group of up to 8 output rows (parity rows for encode, missing data rows
+// 256*16*U consecutive byte positions t of ONE chunk's blocks (U = 1, 2 or 4),
+// and a group of up to 8 output rows (parity rows for encode, missing data rows
 // for decode).  Each lane owns 16 consecutive positions per u-step, so every
 // wave reads one coalesced 1 KiB run from each of the k input blocks and
-// writes one 1 KiB run per output row.
+// writes one 1 KiB run per output row.  Tiles cover [0, valid) of a chunk
+// (valid = length of its last, possibly short, data block); the < padlen
+// positions in [valid, B) are "tail items", one thread each.
 #pragma once
 #include <stdint.h>
 
@@ -22,11 +24,12 @@ struct EncDesc {
     uint64_t in_off;      // chunk start in `in`
     uint64_t par_off;     // first parity block in `parity`
     uint64_t par_stride;  // bytes between parity blocks
-    uint64_t n;           // chunk bytes
     uint32_t B;           // block bytes = ceil(n/k)
     uint32_t k;           // data blocks
     uint32_t p;           // parity blocks (m - k)
     uint32_t tab;         // dword offset of this chunk's tables, layout [j][r][5]
+    uint32_t valid;       // n - (k-1)*B: bytes of the last (zero-padded) data block
+    uint32_t pad;
 };
 
 // One decode chunk, device copy (40 B).
@@ -38,7 +41,7 @@ struct DecDesc {
     uint32_t e;        // missing primaries (rows recovered)
     uint32_t tab;      // dword offset of tables, layout [slot][missing][5]
     uint32_t slot0;    // first entry in slot_off / slot_row / miss_row
-    uint32_t pad;
+    uint32_t valid;    // clamp(n - (k-1)*B, 0, B): positions where every row is writable
 };
 
 struct Tile {
@@ -48,15 +51,27 @@ struct Tile {
     uint32_t pad;
 };
 
+// One byte position handled by the tail kernels.
+struct TailItem {
+    uint32_t chunk;
+    uint32_t t;
+};
+
 }  // namespace sec
 
 // launchers (kernels.hip); all enqueue on `stream` and return hipError_t as int
 extern "C++" {
 int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void *stream);
-int sec_launch_encode(int rows, int U, bool edge, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
+int sec_launch_encode(int rows, int U, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
                       const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, void *stream);
-int sec_launch_decode(int rows, int U, bool edge, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
+int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
+                           uint32_t nitems, const uint32_t *tabs, void *stream);
+int sec_launch_decode(int rows, int U, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
                       const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
                       const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,
                       void *stream);
+int sec_launch_decode_tail(const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
+                           const sec::TailItem *items, uint32_t nitems, const uint32_t *tabs,
+                           const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,
+                           void *stream);
 }

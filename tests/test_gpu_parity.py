@@ -239,3 +239,35 @@ def test_c5_mixed_sizes_host_e2e(engine):
         sn = sorted(random.Random(i).sample(range(11), 8))
         items.append((8, 11, [blocks[s] for s in sn], sn, B * 8 - len(c)))
     assert engine.decode_host(items) == b"".join(chunks)
+
+
+def test_decode_odd_padlen_and_tiny_blocks(engine):
+    """padlen > B (several short output rows), B < 16 (tail-only chunks), valid < 16."""
+    rng = random.Random(21)
+    items, expect = [], []
+    for k, m, n in [(4, 6, 4096), (10, 14, 100), (16, 24, 16 * 20), (3, 5, 7), (8, 11, 8 * 15 + 1), (5, 8, 5 * 17)]:
+        data = rng.randbytes(n)
+        blocks = cfec.easy_encode(data, k, m)
+        B = len(blocks[0])
+        for pad in sorted({B * k - n, min(B * k, B + 3), B * k}):
+            sn = rng.sample(range(m), k)
+            items.append((k, m, [blocks[s] for s in sn], sn, pad))
+            expect.append(cfec.easy_decode([blocks[s] for s in sn], sn, pad, k, m))
+    assert engine.decode_host(items) == b"".join(expect)
+
+
+def test_encode_ragged_tails_many_shapes(engine):
+    """Every padlen 0..k-1 for several k, block sizes around the 16-byte lane and 4 KiB tile edges."""
+    rng = random.Random(22)
+    chunks, km = [], []
+    for k, m in [(3, 5), (10, 14), (16, 24), (64, 96)]:
+        for B in (1, 15, 16, 17, 4095, 4096, 4097, 16384 + 5):
+            for pad in range(0, k, max(1, k // 4)):
+                n = B * k - pad
+                if n <= 0 or -(-n // k) * (k - 1) > n:
+                    continue
+                chunks.append(rng.randbytes(n))
+                km.append((k, m))
+    par = engine.encode_host(chunks, km)
+    for c, (k, m), p in zip(chunks, km, par):
+        assert p == oracle_parity(c, k, m), (k, m, len(c))

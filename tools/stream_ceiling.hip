@@ -83,6 +83,50 @@ __global__ __launch_bounds__(256) void k_rs42(const unsigned char *__restrict__ 
     }
 }
 
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+
+// the encode pattern with every block start shifted by `off` bytes (unaligned 16 B lanes)
+// SHIFT: 0 = hardware unaligned dwordx4, 1 = dword-aligned dwordx4 + dword + v_alignbyte
+template <int SHIFT>
+__global__ __launch_bounds__(256) void k_rs42_mis(const unsigned char *__restrict__ in, unsigned char *__restrict__ par,
+                                                  int off, int soff)
+{
+    const u32 chunk = blockIdx.x >> 4, t0 = (blockIdx.x & 15) * 16384;
+    const size_t B = 262144;
+    const unsigned char *src = in + (size_t)chunk * 1048576 + t0 + threadIdx.x * 16 + off;
+    unsigned char *dst = par + (size_t)chunk * 2 * B + t0 + threadIdx.x * 16 + soff;
+    u32x4 a0[4], a1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        a0[u] = a1[u] = u32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const unsigned char *p = src + j * B + u * 4096;
+            u32x4 x;
+            if (SHIFT == 0) {
+                x = __builtin_nontemporal_load((const u32x4_u *)p);
+            } else {
+                const unsigned r = (unsigned)((size_t)p & 3);
+                const u32 *q = (const u32 *)(p - r);
+                u32x4 w = __builtin_nontemporal_load((const u32x4 __attribute__((aligned(4))) *)q);
+                u32 e = __builtin_nontemporal_load(q + 4);
+                x.x = __builtin_amdgcn_alignbyte(w.y, w.x, r);
+                x.y = __builtin_amdgcn_alignbyte(w.z, w.y, r);
+                x.z = __builtin_amdgcn_alignbyte(w.w, w.z, r);
+                x.w = __builtin_amdgcn_alignbyte(e, w.w, r);
+            }
+            a0[u] ^= x;
+            a1[u] ^= (x << 1);
+        }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        __builtin_nontemporal_store(a0[u], (u32x4_u *)(dst + u * 4096));
+        __builtin_nontemporal_store(a1[u], (u32x4_u *)(dst + B + u * 4096));
+    }
+}
+
 template <class F>
 double time_ms(F launch)
 {
@@ -119,8 +163,21 @@ int main()
     double ms_write = time_ms([&] { hipLaunchKernelGGL(k_write, dim3(grid), dim3(256), 0, 0, (u32x4 *)b, (G + G / 2) / 16); });
     double ms_rs = time_ms([&] { hipLaunchKernelGGL(k_rs42<false>, dim3(1024 * 16), dim3(256), 0, 0, a, b); });
     double ms_rsnt = time_ms([&] { hipLaunchKernelGGL(k_rs42<true>, dim3(1024 * 16), dim3(256), 0, 0, a, b); });
+    double mis[6];
+    const int offs[6][3] = {{2, 0, 0}, {4, 0, 0}, {8, 0, 0}, {2, 0, 1}, {0, 2, 0}, {0, 4, 0}};
+    for (int i = 0; i < 6; ++i) {
+        const int o = offs[i][0], so = offs[i][1];
+        if (offs[i][2])
+            mis[i] = time_ms([&] { hipLaunchKernelGGL(k_rs42_mis<1>, dim3(1024 * 16), dim3(256), 0, 0, a, b, o, so); });
+        else
+            mis[i] = time_ms([&] { hipLaunchKernelGGL(k_rs42_mis<0>, dim3(1024 * 16), dim3(256), 0, 0, a, b, o, so); });
+    }
     CK(hipDeviceSynchronize());
     const double gb = 1e9;
+    printf("{\"rs42_nt_read_off2_GBs\": %.1f, \"read_off4_GBs\": %.1f, \"read_off8_GBs\": %.1f, "
+           "\"read_off2_alignbyte_GBs\": %.1f, \"write_off2_GBs\": %.1f, \"write_off4_GBs\": %.1f}\n",
+           1.5 * G / (mis[0] * 1e-3) / gb, 1.5 * G / (mis[1] * 1e-3) / gb, 1.5 * G / (mis[2] * 1e-3) / gb,
+           1.5 * G / (mis[3] * 1e-3) / gb, 1.5 * G / (mis[4] * 1e-3) / gb, 1.5 * G / (mis[5] * 1e-3) / gb);
     printf("{\"copy_GBs\": %.1f, \"read_GBs\": %.1f, \"write_GBs\": %.1f, \"rs42_xor_GBs\": %.1f, "
            "\"rs42_xor_nt_GBs\": %.1f, \"rs42_xor_ms\": %.4f}\n",
            2.0 * G / (ms_copy * 1e-3) / gb, 1.5 * G / (ms_read * 1e-3) / gb, 1.5 * G / (ms_write * 1e-3) / gb,
