@@ -248,7 +248,7 @@ def main():
         dmod.destroy_process_group()
 
 
-def e2e_rate(eng, nchunks=256, steps=3) -> dict:
+def e2e_rate(eng, nchunks=1024, steps=3) -> dict:
     """Encode + decode of host-resident 1 MiB chunks through SEC_F_HOST (pinned staging, PCIe)."""
     rng = np.random.default_rng(7)
     host = rng.integers(0, 256, nchunks * CHUNK, dtype=np.uint8)

@@ -4,23 +4,28 @@
 // (/root/reference/storb/util/piece.py:8,129-130,196-197).  Responsibilities:
 //   * validate exactly the preconditions zfec / easyfec enforce, returning
 //     SEC_E* codes the Python layer maps to the same exceptions;
-//   * build the per-batch launch plan (descriptors + tiles) on the host and
-//     cache it, so a caller that repeats a batch shape (the validator's
-//     steady state, bench.py) pays no host work or metadata upload;
+//   * build the per-batch launch plan (descriptors, tiles, tail items) on the
+//     host and cache it, so a caller that repeats a batch shape (the
+//     validator's steady state, bench.py) pays no host work or metadata upload;
 //   * keep the coefficient tables device-resident, expanded on the GPU from
 //     coefficient bytes (encode tables per (k, m), decode tables per erasure
 //     pattern);
-//   * stage host buffers for SEC_F_HOST calls.
+//   * SEC_F_HOST calls: stream the batch through pinned slabs on two pipeline
+//     slots (gather -> H2D -> kernels -> D2H -> scatter), so host staging copies,
+//     PCIe transfers in both directions and the kernels of different slabs overlap.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
+#include "copy_pool.hpp"
 #include "gf_host.hpp"
 #include "kernels.hpp"
 #include "storb_ec.h"
@@ -40,6 +45,13 @@ int hip_fail(hipError_t e, const char *what)
         hipError_t e_ = (x);                    \
         if (e_ != hipSuccess)                   \
             return hip_fail(e_, #x);            \
+    } while (0)
+
+#define RC(x)                 \
+    do {                      \
+        int rc_ = (x);        \
+        if (rc_)              \
+            return rc_;       \
     } while (0)
 
 struct DevBuf {
@@ -97,13 +109,41 @@ struct PinBuf {
         p = nullptr;
         cap = 0;
     }
+    char *c(size_t off = 0) const { return (char *)p + off; }
 };
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+size_t env_size(const char *name, size_t dflt)
+{
+    const char *s = getenv(name);
+    if (!s || !*s)
+        return dflt;
+    const long long v = atoll(s);
+    return v > 0 ? (size_t)v : dflt;
+}
+
+// ---- plan ---------------------------------------------------------------
 struct Group {
     int rows, U;
     uint32_t first, count;
+};
+
+// One launch unit: all chunks (device mode) or one slab of chunks (host mode).
+struct SubPlan {
+    int64_t c0 = 0, c1 = 0;  // chunk range
+    std::vector<Group> groups;
+    size_t off_desc = 0, off_tiles = 0, off_tail = 0, off_soff = 0, off_srow = 0, off_mrow = 0;
+    uint32_t ntail = 0;
+    uint64_t in_bytes = 0, out_bytes = 0;  // dense slab sizes (host mode)
+};
+
+struct Plan {
+    std::vector<uint8_t> key;
+    uint64_t gen = 0;  // table-cache generation the plan was built against
+    std::vector<SubPlan> subs;
+    DevBuf meta;  // device copy of the metadata image of every sub-plan
+    bool valid = false;
 };
 
 // Device-resident GF coefficient tables (5 dwords per coefficient), keyed by
@@ -115,23 +155,29 @@ struct TableCache {
     std::map<std::string, uint32_t> index;
 };
 
-struct Plan {
-    std::vector<uint8_t> key;
-    uint64_t gen_enc = 0, gen_dec = 0;
-    std::vector<Group> groups;
-    DevBuf meta;  // device copy of descriptors, tiles, tail items, slot arrays
-    size_t off_desc = 0, off_tiles = 0, off_tail = 0, off_soff = 0, off_srow = 0, off_mrow = 0;
-    uint32_t ntail = 0;
-    // host-mode bookkeeping
-    size_t dev_in_bytes = 0, dev_out_bytes = 0;
-    bool valid = false;
+struct PendingExpand {
+    std::vector<uint8_t> coef;  // layout [input slot][output row]
+    uint32_t dst;               // dword offset in the cache buffer
 };
 
-// Picks the u-steps (4 KiB each) a lane covers per tile.  Larger U = more
-// bytes in flight per lane but more registers; SEC_TILE_U overrides.
+// Host-side image of the metadata, uploaded with one copy.
+struct Image {
+    std::vector<char> bytes;
+    size_t put(const void *src, size_t n)
+    {
+        const size_t off = align_up(bytes.size(), 256);
+        bytes.resize(off + n);
+        if (n)
+            memcpy(bytes.data() + off, src, n);
+        return off;
+    }
+};
+
+// u-steps (4 KiB each) a lane covers per tile.  Larger U = more bytes in flight
+// per lane but more registers; SEC_TILE_U overrides (read per plan build).
 int pick_u(uint64_t B, int rows)
 {
-    const char *env = getenv("SEC_TILE_U");  // read per plan build (plans are cached)
+    const char *env = getenv("SEC_TILE_U");
     const int forced = env ? atoi(env) : 0;
     if (forced == 1 || forced == 2 || forced == 4)
         return forced;
@@ -186,6 +232,37 @@ void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile
     }
 }
 
+// Contiguous chunk ranges of at most `slab` input bytes (at least one chunk each).
+std::vector<std::pair<int64_t, int64_t>> slabs_of(const std::vector<uint64_t> &in_bytes, size_t slab)
+{
+    std::vector<std::pair<int64_t, int64_t>> r;
+    int64_t c0 = 0;
+    uint64_t acc = 0;
+    for (int64_t i = 0; i < (int64_t)in_bytes.size(); ++i) {
+        if (i > c0 && acc + in_bytes[i] > slab) {
+            r.emplace_back(c0, i);
+            c0 = i;
+            acc = 0;
+        }
+        acc += in_bytes[i];
+    }
+    if (c0 < (int64_t)in_bytes.size())
+        r.emplace_back(c0, (int64_t)in_bytes.size());
+    return r;
+}
+
+// ---- host pipeline slots ----------------------------------------------------
+struct Slot {
+    PinBuf in, out;
+    DevBuf din, dout;
+    hipStream_t s = nullptr;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+    std::vector<sec::CopyJob> scatter;  // pinned out -> caller memory, once `done`
+};
+
+constexpr int kSlots = 2;
+
 }  // namespace
 
 struct sec_ctx {
@@ -195,11 +272,12 @@ struct sec_ctx {
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[2];
     std::vector<hipEvent_t> ev_pool;
-    PinBuf pin;  // metadata / host-data staging
-    hipEvent_t pin_ev = nullptr;
+    PinBuf pin;  // metadata image staging
+    hipEvent_t pin_ev = nullptr, meta_ev = nullptr;
     TableCache enc_tabs, dec_tabs;
     Plan enc_plan, dec_plan;
-    DevBuf d_in, d_out;  // host-mode device copies
+    Slot slots[kSlots];
+    std::unique_ptr<sec::CopyPool> pool;
 
     hipStream_t stream() const { return ext ? ext : own; }
     hipEvent_t ev()
@@ -223,22 +301,57 @@ int set_dev(const sec_ctx *ctx)
     return SEC_OK;
 }
 
-// Make sure the pinned staging is no longer read by an in-flight copy.
+sec::CopyPool &pool(sec_ctx *ctx)
+{
+    if (!ctx->pool) {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const int n = (int)env_size("SEC_COPY_THREADS", std::min(7u, std::max(1u, hw / 2)));
+        ctx->pool.reset(new sec::CopyPool(n));
+    }
+    return *ctx->pool;
+}
+
+int slots_init(sec_ctx *ctx)
+{
+    for (Slot &s : ctx->slots)
+        if (!s.s) {
+            CK(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
+            CK(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        }
+    return SEC_OK;
+}
+
+// Finish a slot's in-flight slab: wait for its D2H, then scatter to caller memory.
+int slot_retire(sec_ctx *ctx, Slot &s)
+{
+    if (!s.busy)
+        return SEC_OK;
+    s.busy = false;
+    CK(hipEventSynchronize(s.done));
+    pool(ctx).run(s.scatter);
+    s.scatter.clear();
+    return SEC_OK;
+}
+
+int drain_all(sec_ctx *ctx)
+{
+    for (Slot &s : ctx->slots) {
+        RC(slot_retire(ctx, s));
+        if (s.s)
+            CK(hipStreamSynchronize(s.s));
+    }
+    CK(hipStreamSynchronize(ctx->stream()));
+    return SEC_OK;
+}
+
+// Make sure the pinned metadata staging is no longer read by an in-flight copy.
 int pin_wait(sec_ctx *ctx)
 {
     CK(hipEventSynchronize(ctx->pin_ev));
     return SEC_OK;
 }
 
-// Adds the tables for one coefficient matrix (ncoef bytes, layout [slot][row])
-// unless present; returns the dword offset in *off.  New coefficients are
-// appended to `upload` with their destination.
-struct PendingExpand {
-    std::vector<uint8_t> coef;
-    uint32_t dst;  // dword offset in the cache buffer
-};
-
-int table_ensure(TableCache &tc, const std::string &key, const std::vector<uint8_t> &coef,
+int table_ensure(TableCache &tc, const std::string &key, std::vector<uint8_t> &&coef,
                  std::vector<PendingExpand> &pending, uint32_t *off)
 {
     auto it = tc.index.find(key);
@@ -251,69 +364,392 @@ int table_ensure(TableCache &tc, const std::string &key, const std::vector<uint8
         return 1;  // caller resets the cache and retries
     *off = (uint32_t)tc.used;
     tc.index.emplace(key, *off);
-    pending.push_back(PendingExpand{coef, *off});
+    pending.push_back(PendingExpand{std::move(coef), *off});
     tc.used += need;
     return SEC_OK;
 }
 
 int table_reset(sec_ctx *ctx, TableCache &tc, size_t need_dwords)
 {
-    CK(hipStreamSynchronize(ctx->stream()));
+    RC(drain_all(ctx));  // nothing may still read the old buffer
     size_t want = std::max<size_t>(tc.buf.cap * 2, std::max<size_t>(need_dwords * 4 * 2, (size_t)1 << 20));
     tc.buf.release();
-    int rc = tc.buf.ensure(want);
-    if (rc)
-        return rc;
+    RC(tc.buf.ensure(want));
     tc.used = 0;
     tc.index.clear();
     ++tc.gen;
     return SEC_OK;
 }
 
-// Upload one contiguous metadata image (built in the pinned buffer) into
-// plan.meta and launch the pending table expansions whose coefficient bytes
-// sit at `coef_base` within the image.
-int upload_meta(sec_ctx *ctx, Plan &plan, size_t bytes)
+// Uploads the image with one H2D from pinned memory and expands new tables from
+// the coefficient bytes placed at the end of the image.
+int upload_plan(sec_ctx *ctx, Plan &plan, Image &img, TableCache &tc, const std::vector<PendingExpand> &pending)
 {
-    int rc = plan.meta.ensure(bytes);
-    if (rc)
-        return rc;
+    std::vector<size_t> coef_off;
+    for (const auto &pe : pending)
+        coef_off.push_back(img.put(pe.coef.data(), pe.coef.size()));
+    const size_t bytes = img.bytes.size();
+    RC(pin_wait(ctx));
+    RC(ctx->pin.ensure(bytes));
+    memcpy(ctx->pin.p, img.bytes.data(), bytes);
+    RC(plan.meta.ensure(bytes));
     CK(hipMemcpyAsync(plan.meta.p, ctx->pin.p, bytes, hipMemcpyHostToDevice, ctx->stream()));
     CK(hipEventRecord(ctx->pin_ev, ctx->stream()));
-    return SEC_OK;
-}
-
-int launch_expansions(sec_ctx *ctx, TableCache &tc, const Plan &plan, size_t coef_off,
-                      const std::vector<PendingExpand> &pending)
-{
-    size_t o = coef_off;
-    for (const auto &pe : pending) {
-        int e = sec_launch_expand(plan.meta.as<uint8_t>(o), (uint32_t)pe.coef.size(), tc.buf.as<uint32_t>() + pe.dst,
-                                  ctx->stream());
+    for (size_t i = 0; i < pending.size(); ++i) {
+        int e = sec_launch_expand(plan.meta.as<uint8_t>(coef_off[i]), (uint32_t)pending[i].coef.size(),
+                                  tc.buf.as<uint32_t>() + pending[i].dst, ctx->stream());
         if (e)
             return hip_fail((hipError_t)e, "sec_expand_tables");
-        o += pe.coef.size();
     }
     return SEC_OK;
 }
 
-int timing_begin(sec_ctx *ctx, hipEvent_t *a)
+int timing_begin(sec_ctx *ctx, hipEvent_t *a, hipStream_t s)
 {
     *a = nullptr;
     if (!ctx->timing)
         return SEC_OK;
     *a = ctx->ev();
-    CK(hipEventRecord(*a, ctx->stream()));
+    CK(hipEventRecord(*a, s));
     return SEC_OK;
 }
 
-int timing_end(sec_ctx *ctx, hipEvent_t a, int kind)
+int timing_end(sec_ctx *ctx, hipEvent_t a, int kind, hipStream_t s)
 {
     if (!a)
         return SEC_OK;
     hipEvent_t b = ctx->ev();
-    CK(hipEventRecord(b, ctx->stream()));
+    CK(hipEventRecord(b, s));
     ctx->pending[kind].emplace_back(a, b);
+    return SEC_OK;
+}
+
+int check_sharenums(int k, int m, const int32_t *s)
+{
+    bool seen[256] = {false};
+    for (int i = 0; i < k; ++i) {
+        if (s[i] < 0 || s[i] >= m)
+            return SEC_ESHARENUM;
+        if (seen[s[i]])
+            return SEC_EDUPSHARE;
+        seen[s[i]] = true;
+    }
+    return SEC_OK;
+}
+
+uint64_t enc_B(const sec_enc_chunk &c) { return (c.n + (uint64_t)c.k - 1) / (uint64_t)c.k; }
+
+// ---- encode plan ------------------------------------------------------------
+int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, bool host)
+{
+    Plan &plan = ctx->enc_plan;
+    TableCache &tc = ctx->enc_tabs;
+    std::vector<PendingExpand> pending;
+    std::vector<uint32_t> tab_of((size_t)nchunks, 0);
+    for (int attempt = 0;; ++attempt) {
+        pending.clear();
+        size_t need = 0;
+        bool overflow = false;
+        std::map<std::pair<int, int>, uint32_t> local;
+        for (int64_t i = 0; i < nchunks && !overflow; ++i) {
+            const int k = chunks[i].k, m = chunks[i].m;
+            if (m == k)
+                continue;
+            auto lk = local.find({k, m});
+            if (lk != local.end()) {
+                tab_of[i] = lk->second;
+                continue;
+            }
+            const std::vector<uint8_t> enc = sec::encode_matrix(k, m);
+            const int p = m - k;
+            std::vector<uint8_t> coef((size_t)k * p);
+            for (int j = 0; j < k; ++j)
+                for (int r = 0; r < p; ++r)
+                    coef[(size_t)j * p + r] = enc[(size_t)(k + r) * k + j];
+            need += coef.size() * sec::kTabDwords;
+            uint32_t off = 0;
+            if (table_ensure(tc, std::to_string(k) + "/" + std::to_string(m), std::move(coef), pending, &off)) {
+                overflow = true;
+                break;
+            }
+            local[{k, m}] = off;
+            tab_of[i] = off;
+        }
+        if (!overflow)
+            break;
+        if (attempt == 1)
+            return SEC_ENOMEM;
+        RC(table_reset(ctx, tc, need));
+    }
+
+    std::vector<std::pair<int64_t, int64_t>> ranges;
+    if (host) {
+        std::vector<uint64_t> ib((size_t)nchunks);
+        for (int64_t i = 0; i < nchunks; ++i)
+            ib[i] = chunks[i].n;
+        ranges = slabs_of(ib, env_size("SEC_SLAB_BYTES", (size_t)64 << 20));
+    } else {
+        ranges.emplace_back(0, nchunks);
+    }
+    Image img;
+    plan.subs.clear();
+    for (auto [c0, c1] : ranges) {
+        SubPlan sp;
+        sp.c0 = c0;
+        sp.c1 = c1;
+        std::vector<sec::EncDesc> descs((size_t)(c1 - c0));
+        Bins bins;
+        std::vector<sec::TailItem> tail;
+        for (int64_t i = c0; i < c1; ++i) {
+            const sec_enc_chunk &c = chunks[i];
+            const uint64_t B = enc_B(c);
+            const int p = c.m - c.k;
+            const int64_t valid = (int64_t)c.n - (int64_t)(c.k - 1) * (int64_t)B;
+            sec::EncDesc &d = descs[i - c0];
+            d.in_off = host ? sp.in_bytes : c.in_off;
+            d.par_off = host ? sp.out_bytes : c.parity_off;
+            d.par_stride = host ? B : c.parity_stride;
+            d.B = (uint32_t)B;
+            d.k = (uint32_t)c.k;
+            d.p = (uint32_t)p;
+            d.tab = tab_of[i];
+            d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)B));
+            d.pad = 0;
+            sp.in_bytes += c.n;
+            sp.out_bytes += (uint64_t)p * B;
+            if (p > 0)
+                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p);
+        }
+        std::vector<sec::Tile> tiles;
+        flatten(bins, sp.groups, tiles);
+        sp.ntail = (uint32_t)tail.size();
+        sp.off_desc = img.put(descs.data(), descs.size() * sizeof(sec::EncDesc));
+        sp.off_tiles = img.put(tiles.data(), tiles.size() * sizeof(sec::Tile));
+        sp.off_tail = img.put(tail.data(), tail.size() * sizeof(sec::TailItem));
+        plan.subs.push_back(std::move(sp));
+    }
+    RC(upload_plan(ctx, plan, img, tc, pending));
+    plan.gen = tc.gen;
+    return SEC_OK;
+}
+
+int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const uint8_t *in, uint8_t *par,
+                      hipStream_t s)
+{
+    const sec::EncDesc *dd = plan.meta.as<sec::EncDesc>(sp.off_desc);
+    const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
+    const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
+    for (const Group &g : sp.groups) {
+        int e = sec_launch_encode(g.rows, g.U, in, par, dd, dt + g.first, g.count, tabs, s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_encode_kernel");
+    }
+    if (sp.ntail) {
+        int e = sec_launch_encode_tail(in, par, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs, s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_encode_tail");
+    }
+    return SEC_OK;
+}
+
+// ---- decode plan ------------------------------------------------------------
+// Normalised slot order of every chunk (zfec's _fecmodule.c: primaries moved to
+// their own slot); perm[i] = caller position of the block in normalised slot i.
+struct DecLayout {
+    std::vector<int> perm, idx;
+    std::vector<uint64_t> first;  // per chunk: start in perm/idx
+};
+
+DecLayout dec_layout(const sec_dec_chunk *chunks, int64_t nchunks, const int32_t *sharenums)
+{
+    DecLayout L;
+    L.first.resize((size_t)nchunks);
+    std::vector<int> idx, perm;
+    for (int64_t i = 0; i < nchunks; ++i) {
+        const sec_dec_chunk &c = chunks[i];
+        idx.assign(sharenums + c.slot0, sharenums + c.slot0 + c.k);
+        sec::normalise_slots(c.k, idx, perm);
+        L.first[i] = L.perm.size();
+        L.perm.insert(L.perm.end(), perm.begin(), perm.end());
+        L.idx.insert(L.idx.end(), idx.begin(), idx.end());
+    }
+    return L;
+}
+
+int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const uint64_t *block_offs,
+                      const DecLayout &L, bool host)
+{
+    Plan &plan = ctx->dec_plan;
+    TableCache &tc = ctx->dec_tabs;
+    std::vector<PendingExpand> pending;
+    std::vector<uint32_t> tab_of((size_t)nchunks, 0), e_of((size_t)nchunks, 0);
+    for (int attempt = 0;; ++attempt) {
+        pending.clear();
+        size_t need = 0;
+        bool overflow = false;
+        for (int64_t i = 0; i < nchunks && !overflow; ++i) {
+            const sec_dec_chunk &c = chunks[i];
+            const int k = c.k;
+            const int *idx = &L.idx[L.first[i]];
+            std::vector<int> miss;
+            for (int s = 0; s < k; ++s)
+                if (idx[s] >= k)
+                    miss.push_back(s);
+            e_of[i] = (uint32_t)miss.size();
+            if (miss.empty())
+                continue;
+            std::string key = std::to_string(k) + "/" + std::to_string(c.m) + ":";
+            for (int s = 0; s < k; ++s)
+                key += std::to_string(idx[s]) + ",";
+            auto it = tc.index.find(key);
+            if (it != tc.index.end()) {
+                tab_of[i] = it->second;
+                continue;
+            }
+            std::vector<int> iv(idx, idx + k);
+            std::vector<uint8_t> minv;
+            if (!sec::decode_matrix(k, c.m, iv, minv))
+                return SEC_ESINGULAR;
+            const int e = (int)miss.size();
+            std::vector<uint8_t> coef((size_t)k * e);
+            for (int s = 0; s < k; ++s)
+                for (int r = 0; r < e; ++r)
+                    coef[(size_t)s * e + r] = minv[(size_t)miss[r] * k + s];
+            need += coef.size() * sec::kTabDwords;
+            uint32_t off = 0;
+            if (table_ensure(tc, key, std::move(coef), pending, &off)) {
+                overflow = true;
+                break;
+            }
+            tab_of[i] = off;
+        }
+        if (!overflow)
+            break;
+        if (attempt == 1)
+            return SEC_ENOMEM;
+        RC(table_reset(ctx, tc, need * 2 + ((size_t)1 << 18)));
+    }
+
+    std::vector<std::pair<int64_t, int64_t>> ranges;
+    if (host) {
+        std::vector<uint64_t> ib((size_t)nchunks);
+        for (int64_t i = 0; i < nchunks; ++i)
+            ib[i] = (uint64_t)chunks[i].k * chunks[i].B;
+        ranges = slabs_of(ib, env_size("SEC_SLAB_BYTES", (size_t)64 << 20));
+    } else {
+        ranges.emplace_back(0, nchunks);
+    }
+    Image img;
+    plan.subs.clear();
+    for (auto [c0, c1] : ranges) {
+        SubPlan sp;
+        sp.c0 = c0;
+        sp.c1 = c1;
+        std::vector<sec::DecDesc> descs((size_t)(c1 - c0));
+        std::vector<uint64_t> soff;
+        std::vector<uint32_t> srow, mrow;
+        Bins bins;
+        std::vector<sec::TailItem> tail;
+        for (int64_t i = c0; i < c1; ++i) {
+            const sec_dec_chunk &c = chunks[i];
+            const uint64_t base = L.first[i];
+            const int *idx = &L.idx[base];
+            const uint32_t slot0 = (uint32_t)soff.size();
+            std::vector<uint32_t> mr;
+            for (int s = 0; s < c.k; ++s) {
+                const int from = L.perm[base + s];
+                soff.push_back(host ? sp.in_bytes + (uint64_t)s * c.B : block_offs[c.slot0 + from]);
+                srow.push_back(idx[s] < c.k ? (uint32_t)idx[s] : 0xFFFFFFFFu);
+                if (idx[s] >= c.k)
+                    mr.push_back((uint32_t)s);
+            }
+            mr.resize((size_t)c.k, 0);
+            mrow.insert(mrow.end(), mr.begin(), mr.end());
+            const uint64_t nout = (uint64_t)c.k * c.B - c.padlen;
+            const int64_t valid = (int64_t)nout - (int64_t)(c.k - 1) * (int64_t)c.B;
+            sec::DecDesc &d = descs[i - c0];
+            d.out_off = host ? sp.out_bytes : c.out_off;
+            d.n = nout;
+            d.B = (uint32_t)c.B;
+            d.k = (uint32_t)c.k;
+            d.e = e_of[i];
+            d.tab = tab_of[i];
+            d.slot0 = slot0;
+            d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)c.B));
+            sp.in_bytes += (uint64_t)c.k * c.B;
+            sp.out_bytes += nout;
+            if (nout > 0)
+                add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i]);
+        }
+        std::vector<sec::Tile> tiles;
+        flatten(bins, sp.groups, tiles);
+        sp.ntail = (uint32_t)tail.size();
+        sp.off_desc = img.put(descs.data(), descs.size() * sizeof(sec::DecDesc));
+        sp.off_tiles = img.put(tiles.data(), tiles.size() * sizeof(sec::Tile));
+        sp.off_tail = img.put(tail.data(), tail.size() * sizeof(sec::TailItem));
+        sp.off_soff = img.put(soff.data(), soff.size() * 8);
+        sp.off_srow = img.put(srow.data(), srow.size() * 4);
+        sp.off_mrow = img.put(mrow.data(), mrow.size() * 4);
+        plan.subs.push_back(std::move(sp));
+    }
+    RC(upload_plan(ctx, plan, img, tc, pending));
+    plan.gen = tc.gen;
+    return SEC_OK;
+}
+
+int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const uint8_t *blocks, uint8_t *out,
+                      hipStream_t s)
+{
+    const sec::DecDesc *dd = plan.meta.as<sec::DecDesc>(sp.off_desc);
+    const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
+    const uint32_t *tabs = ctx->dec_tabs.buf.as<uint32_t>();
+    const uint64_t *so = plan.meta.as<uint64_t>(sp.off_soff);
+    const uint32_t *sr = plan.meta.as<uint32_t>(sp.off_srow), *mr = plan.meta.as<uint32_t>(sp.off_mrow);
+    for (const Group &g : sp.groups) {
+        int e = sec_launch_decode(g.rows, g.U, blocks, out, dd, dt + g.first, g.count, tabs, so, sr, mr, s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_decode_kernel");
+    }
+    if (sp.ntail) {
+        int e = sec_launch_decode_tail(blocks, out, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs,
+                                       so, sr, mr, s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_decode_tail");
+    }
+    return SEC_OK;
+}
+
+// ---- host pipeline ----------------------------------------------------------
+// For each slab: (CPU) gather caller bytes into the slot's pinned `in`;
+// (slot stream) H2D, kernels, D2H into pinned `out`; the scatter of `out` into
+// caller memory runs when the slot is next needed or at the end.  Two slots, so
+// the CPU gathers slab i+1 and scatters slab i-1 while the GPU works on slab i.
+template <class Gather, class Scatter, class Launch>
+int run_pipeline(sec_ctx *ctx, Plan &plan, Gather gather, Scatter scatter, Launch launch)
+{
+    RC(slots_init(ctx));
+    CK(hipEventRecord(ctx->meta_ev, ctx->stream()));  // behind the plan upload / table expansion
+    size_t i = 0;
+    for (const SubPlan &sp : plan.subs) {
+        Slot &sl = ctx->slots[i++ % kSlots];
+        RC(slot_retire(ctx, sl));
+        RC(sl.in.ensure(sp.in_bytes));
+        RC(sl.out.ensure(sp.out_bytes));
+        RC(sl.din.ensure(sp.in_bytes));
+        RC(sl.dout.ensure(sp.out_bytes));
+        std::vector<sec::CopyJob> jobs;
+        gather(sp, sl.in.c(), jobs);
+        pool(ctx).run(jobs);
+        CK(hipStreamWaitEvent(sl.s, ctx->meta_ev, 0));
+        CK(hipMemcpyAsync(sl.din.p, sl.in.p, sp.in_bytes, hipMemcpyHostToDevice, sl.s));
+        RC(launch(sp, sl.din.as<uint8_t>(), sl.dout.as<uint8_t>(), sl.s));
+        CK(hipMemcpyAsync(sl.out.p, sl.dout.p, sp.out_bytes, hipMemcpyDeviceToHost, sl.s));
+        CK(hipEventRecord(sl.done, sl.s));
+        scatter(sp, sl.out.c(), sl.scatter);
+        sl.busy = true;
+    }
+    for (size_t j = 0; j < (size_t)kSlots; ++j)
+        RC(slot_retire(ctx, ctx->slots[(i + j) % kSlots]));
     return SEC_OK;
 }
 
@@ -377,6 +813,8 @@ int sec_ctx_create(int device, sec_ctx **out)
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&ctx->pin_ev, hipEventDisableTiming);
     if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&ctx->meta_ev, hipEventDisableTiming);
+    if (e == hipSuccess)
         e = hipEventRecord(ctx->pin_ev, ctx->own);
     if (e != hipSuccess) {
         sec_ctx_destroy(ctx);
@@ -391,10 +829,9 @@ void sec_ctx_destroy(sec_ctx *ctx)
     if (!ctx)
         return;
     (void)hipSetDevice(ctx->device);
+    (void)drain_all(ctx);
     if (ctx->own)
         (void)hipStreamSynchronize(ctx->own);
-    if (ctx->ext)
-        (void)hipStreamSynchronize(ctx->ext);
     for (auto &v : ctx->pending)
         for (auto &pr : v) {
             (void)hipEventDestroy(pr.first);
@@ -404,13 +841,24 @@ void sec_ctx_destroy(sec_ctx *ctx)
         (void)hipEventDestroy(e);
     if (ctx->pin_ev)
         (void)hipEventDestroy(ctx->pin_ev);
+    if (ctx->meta_ev)
+        (void)hipEventDestroy(ctx->meta_ev);
+    for (Slot &s : ctx->slots) {
+        s.in.release();
+        s.out.release();
+        s.din.release();
+        s.dout.release();
+        if (s.done)
+            (void)hipEventDestroy(s.done);
+        if (s.s)
+            (void)hipStreamDestroy(s.s);
+    }
+    ctx->pool.reset();
     ctx->pin.release();
     ctx->enc_tabs.buf.release();
     ctx->dec_tabs.buf.release();
     ctx->enc_plan.meta.release();
     ctx->dec_plan.meta.release();
-    ctx->d_in.release();
-    ctx->d_out.release();
     if (ctx->own)
         (void)hipStreamDestroy(ctx->own);
     delete ctx;
@@ -420,9 +868,7 @@ int sec_ctx_set_stream(sec_ctx *ctx, void *stream)
 {
     if (!ctx)
         return SEC_EINVAL;
-    int rc = set_dev(ctx);
-    if (rc)
-        return rc;
+    RC(set_dev(ctx));
     // order the switch: work queued so far completes before the new stream runs
     CK(hipStreamSynchronize(ctx->stream()));
     ctx->ext = (hipStream_t)stream;
@@ -434,9 +880,7 @@ int sec_sync(sec_ctx *ctx)
 {
     if (!ctx)
         return SEC_EINVAL;
-    int rc = set_dev(ctx);
-    if (rc)
-        return rc;
+    RC(set_dev(ctx));
     CK(hipStreamSynchronize(ctx->stream()));
     return SEC_OK;
 }
@@ -453,9 +897,7 @@ int sec_timing_collect(sec_ctx *ctx, int kind, double *total_ms, int64_t *launch
 {
     if (!ctx || kind < 0 || kind > 1 || !total_ms || !launches)
         return SEC_EINVAL;
-    int rc = set_dev(ctx);
-    if (rc)
-        return rc;
+    RC(set_dev(ctx));
     double tot = 0;
     for (auto &pr : ctx->pending[kind]) {
         CK(hipEventSynchronize(pr.second));
@@ -477,21 +919,8 @@ int sec_encode_matrix(int k, int m, uint8_t *out)
         return SEC_EINVAL;
     if (k < 1 || m < k || m > 256)
         return SEC_EKM;
-    std::vector<uint8_t> enc = sec::encode_matrix(k, m);
+    const std::vector<uint8_t> enc = sec::encode_matrix(k, m);
     memcpy(out, enc.data() + (size_t)k * k, (size_t)(m - k) * k);
-    return SEC_OK;
-}
-
-static int check_sharenums(int k, int m, const int32_t *s)
-{
-    bool seen[256] = {false};
-    for (int i = 0; i < k; ++i) {
-        if (s[i] < 0 || s[i] >= m)
-            return SEC_ESHARENUM;
-        if (seen[s[i]])
-            return SEC_EDUPSHARE;
-        seen[s[i]] = true;
-    }
     return SEC_OK;
 }
 
@@ -501,9 +930,7 @@ int sec_decode_matrix(int k, int m, const int32_t *sharenums, uint8_t *out, int3
         return SEC_EINVAL;
     if (k < 1 || m < k || m > 256)
         return SEC_EKM;
-    int rc = check_sharenums(k, m, sharenums);
-    if (rc)
-        return rc;
+    RC(check_sharenums(k, m, sharenums));
     std::vector<int> idx(sharenums, sharenums + k), perm;
     sec::normalise_slots(k, idx, perm);
     std::vector<uint8_t> minv;
@@ -527,17 +954,15 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
     if (nchunks >= (int64_t)UINT32_MAX)
         return SEC_EINVAL;
     const bool host = flags & SEC_F_HOST;
-    int rc = set_dev(ctx);
-    if (rc)
-        return rc;
+    RC(set_dev(ctx));
 
-    // ---- validate (easyfec.Encoder.encode / _fec.Encoder preconditions) ----
-    uint64_t in_dense = 0, total_par = 0;
+    // easyfec.Encoder.encode / _fec.Encoder preconditions
+    uint64_t total_par = 0;
     for (int64_t i = 0; i < nchunks; ++i) {
         const sec_enc_chunk &c = chunks[i];
         if (c.k < 1 || c.m < c.k || c.m > 256)
             return SEC_EKM;
-        const uint64_t B = (c.n + c.k - 1) / c.k;
+        const uint64_t B = enc_B(c);
         if (c.k > 1 && (uint64_t)(c.k - 1) * B > c.n)
             return SEC_EBLOCKLEN;
         if (B >= (1ull << 31))
@@ -545,7 +970,6 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
         const uint64_t p = (uint64_t)(c.m - c.k);
         if (p > 0 && B > 0 && c.parity_stride < B)
             return SEC_EINVAL;
-        in_dense += c.n;
         total_par += p * B;
     }
     if (total_par == 0)
@@ -557,182 +981,47 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
     std::vector<uint8_t> key(sizeof(sec_enc_chunk) * (size_t)nchunks + sizeof(unsigned));
     memcpy(key.data(), chunks, sizeof(sec_enc_chunk) * (size_t)nchunks);
     memcpy(key.data() + sizeof(sec_enc_chunk) * (size_t)nchunks, &flags, sizeof(unsigned));
-    const bool reuse = plan.valid && plan.gen_enc == ctx->enc_tabs.gen && plan.key == key;
-
-    if (!reuse) {
+    if (!(plan.valid && plan.gen == ctx->enc_tabs.gen && plan.key == key)) {
         plan.valid = false;
-        // tables for every distinct (k, m)
-        std::vector<PendingExpand> pending;
-        std::vector<uint32_t> tab_of((size_t)nchunks, 0);
-        for (int attempt = 0; attempt < 2; ++attempt) {
-            pending.clear();
-            size_t need = 0;
-            bool overflow = false;
-            std::map<std::pair<int, int>, uint32_t> local;
-            for (int64_t i = 0; i < nchunks && !overflow; ++i) {
-                const int k = chunks[i].k, m = chunks[i].m;
-                if (m == k)
-                    continue;
-                auto lk = local.find({k, m});
-                if (lk != local.end()) {
-                    tab_of[i] = lk->second;
-                    continue;
-                }
-                std::vector<uint8_t> enc = sec::encode_matrix(k, m);
-                const int p = m - k;
-                std::vector<uint8_t> coef((size_t)k * p);
-                for (int j = 0; j < k; ++j)
-                    for (int r = 0; r < p; ++r)
-                        coef[(size_t)j * p + r] = enc[(size_t)(k + r) * k + j];
-                need += coef.size() * sec::kTabDwords;
-                uint32_t off = 0;
-                const std::string tk = std::to_string(k) + "/" + std::to_string(m);
-                int st = table_ensure(ctx->enc_tabs, tk, coef, pending, &off);
-                if (st == 1) {
-                    overflow = true;
-                    break;
-                }
-                local[{k, m}] = off;
-                tab_of[i] = off;
-            }
-            if (!overflow)
-                break;
-            if (attempt == 1)
-                return SEC_ENOMEM;
-            rc = table_reset(ctx, ctx->enc_tabs, need);
-            if (rc)
-                return rc;
-        }
-
-        // descriptors + tiles + tail items
-        std::vector<sec::EncDesc> descs((size_t)nchunks);
-        Bins bins;
-        std::vector<sec::TailItem> tail;
-        uint64_t dense = 0, idense = 0;
-        for (int64_t i = 0; i < nchunks; ++i) {
-            const sec_enc_chunk &c = chunks[i];
-            const uint64_t B = (c.n + c.k - 1) / c.k;
-            const int p = c.m - c.k;
-            sec::EncDesc &d = descs[i];
-            d.in_off = host ? idense : c.in_off;
-            idense += c.n;
-            d.par_off = host ? dense : c.parity_off;
-            d.par_stride = host ? B : c.parity_stride;
-            const int64_t valid = (int64_t)c.n - (int64_t)(c.k - 1) * (int64_t)B;
-            d.B = (uint32_t)B;
-            d.k = (uint32_t)c.k;
-            d.p = (uint32_t)p;
-            d.tab = tab_of[i];
-            d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)B));
-            d.pad = 0;
-            dense += (uint64_t)p * B;
-            if (p > 0)
-                add_work(bins, tail, (uint32_t)i, B, valid, p);
-        }
-        std::vector<sec::Tile> tiles;
-        flatten(bins, plan.groups, tiles);
-        plan.ntail = (uint32_t)tail.size();
-        // metadata image: [descs][tiles][tail][coefs]
-        size_t coef_bytes = 0;
-        for (auto &pe : pending)
-            coef_bytes += pe.coef.size();
-        plan.off_desc = 0;
-        plan.off_tiles = align_up(descs.size() * sizeof(sec::EncDesc), 256);
-        plan.off_tail = align_up(plan.off_tiles + tiles.size() * sizeof(sec::Tile), 256);
-        const size_t off_coef = align_up(plan.off_tail + tail.size() * sizeof(sec::TailItem), 256);
-        const size_t bytes = off_coef + coef_bytes;
-        rc = pin_wait(ctx);
-        if (!rc)
-            rc = ctx->pin.ensure(bytes);
-        if (rc)
-            return rc;
-        char *img = (char *)ctx->pin.p;
-        memcpy(img + plan.off_desc, descs.data(), descs.size() * sizeof(sec::EncDesc));
-        memcpy(img + plan.off_tiles, tiles.data(), tiles.size() * sizeof(sec::Tile));
-        memcpy(img + plan.off_tail, tail.data(), tail.size() * sizeof(sec::TailItem));
-        size_t o = off_coef;
-        for (auto &pe : pending) {
-            memcpy(img + o, pe.coef.data(), pe.coef.size());
-            o += pe.coef.size();
-        }
-        rc = upload_meta(ctx, plan, bytes);
-        if (!rc)
-            rc = launch_expansions(ctx, ctx->enc_tabs, plan, off_coef, pending);
-        if (rc)
-            return rc;
+        RC(build_encode_plan(ctx, chunks, nchunks, host));
         plan.key.swap(key);
-        plan.gen_enc = ctx->enc_tabs.gen;
-        plan.dev_in_bytes = in_dense;
-        plan.dev_out_bytes = dense;
         plan.valid = true;
     }
 
-    // ---- data movement (host mode) ----
-    const uint8_t *d_in = in;
-    uint8_t *d_par = parity;
-    if (host) {
-        // gather every chunk (arbitrary host addresses) into pinned staging, one H2D
-        rc = ctx->d_in.ensure(plan.dev_in_bytes);
-        if (!rc)
-            rc = ctx->d_out.ensure(plan.dev_out_bytes);
-        if (!rc)
-            rc = pin_wait(ctx);
-        if (!rc)
-            rc = ctx->pin.ensure(plan.dev_in_bytes);
-        if (rc)
-            return rc;
-        char *stage = (char *)ctx->pin.p;
+    if (!host) {
+        hipEvent_t t0 = nullptr;
+        RC(timing_begin(ctx, &t0, ctx->stream()));
+        RC(launch_encode_sub(ctx, plan, plan.subs[0], in, parity, ctx->stream()));
+        RC(timing_end(ctx, t0, 0, ctx->stream()));
+        if (!(flags & SEC_F_ASYNC))
+            CK(hipStreamSynchronize(ctx->stream()));
+        return SEC_OK;
+    }
+    auto gather = [&](const SubPlan &sp, char *stage, std::vector<sec::CopyJob> &jobs) {
         uint64_t o = 0;
-        for (int64_t i = 0; i < nchunks; ++i) {
-            memcpy(stage + o, in + chunks[i].in_off, chunks[i].n);
+        for (int64_t i = sp.c0; i < sp.c1; ++i) {
+            jobs.push_back(sec::CopyJob{stage + o, in + chunks[i].in_off, chunks[i].n});
             o += chunks[i].n;
         }
-        CK(hipMemcpyAsync(ctx->d_in.p, stage, plan.dev_in_bytes, hipMemcpyHostToDevice, ctx->stream()));
-        CK(hipEventRecord(ctx->pin_ev, ctx->stream()));
-        d_in = ctx->d_in.as<uint8_t>();
-        d_par = ctx->d_out.as<uint8_t>();
-    }
-
-    // ---- launches ----
-    hipEvent_t t0 = nullptr;
-    rc = timing_begin(ctx, &t0);
-    if (rc)
-        return rc;
-    const sec::EncDesc *dd = plan.meta.as<sec::EncDesc>(plan.off_desc);
-    const sec::Tile *dt = plan.meta.as<sec::Tile>(plan.off_tiles);
-    for (const Group &g : plan.groups) {
-        int e = sec_launch_encode(g.rows, g.U, d_in, d_par, dd, dt + g.first, g.count,
-                                  ctx->enc_tabs.buf.as<uint32_t>(), ctx->stream());
-        if (e)
-            return hip_fail((hipError_t)e, "sec_encode_kernel");
-    }
-    if (plan.ntail) {
-        int e = sec_launch_encode_tail(d_in, d_par, dd, plan.meta.as<sec::TailItem>(plan.off_tail), plan.ntail,
-                                       ctx->enc_tabs.buf.as<uint32_t>(), ctx->stream());
-        if (e)
-            return hip_fail((hipError_t)e, "sec_encode_tail");
-    }
-    rc = timing_end(ctx, t0, 0);
-    if (rc)
-        return rc;
-
-    if (host) {
-        uint64_t dense = 0;
-        for (int64_t i = 0; i < nchunks; ++i) {
+    };
+    auto scatter = [&](const SubPlan &sp, char *stage, std::vector<sec::CopyJob> &jobs) {
+        uint64_t o = 0;
+        for (int64_t i = sp.c0; i < sp.c1; ++i) {
             const sec_enc_chunk &c = chunks[i];
-            const uint64_t B = (c.n + c.k - 1) / c.k;
-            const uint64_t p = (uint64_t)(c.m - c.k);
-            if (p == 0 || B == 0)
-                continue;
-            CK(hipMemcpy2DAsync(parity + c.parity_off, c.parity_stride, d_par + dense, B, B, p,
-                                hipMemcpyDeviceToHost, ctx->stream()));
-            dense += p * B;
+            const uint64_t B = enc_B(c), p = (uint64_t)(c.m - c.k);
+            if (c.parity_stride == B) {
+                jobs.push_back(sec::CopyJob{parity + c.parity_off, stage + o, p * B});
+            } else {
+                for (uint64_t r = 0; r < p; ++r)
+                    jobs.push_back(sec::CopyJob{parity + c.parity_off + r * c.parity_stride, stage + o + r * B, B});
+            }
+            o += p * B;
         }
-        CK(hipStreamSynchronize(ctx->stream()));
-    } else if (!(flags & SEC_F_ASYNC)) {
-        CK(hipStreamSynchronize(ctx->stream()));
-    }
-    return SEC_OK;
+    };
+    auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
+        return launch_encode_sub(ctx, plan, sp, din, dout, s);
+    };
+    return run_pipeline(ctx, plan, gather, scatter, launch);
 }
 
 // ---------------------------------------------------------------------------
@@ -747,11 +1036,9 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
     if (nchunks >= (int64_t)UINT32_MAX)
         return SEC_EINVAL;
     const bool host = flags & SEC_F_HOST;
-    int rc = set_dev(ctx);
-    if (rc)
-        return rc;
+    RC(set_dev(ctx));
 
-    // ---- validate (_fec.Decoder.decode / easyfec.Decoder.decode) ----
+    // _fec.Decoder.decode / easyfec.Decoder.decode preconditions
     uint64_t total_slots = 0, total_out = 0;
     for (int64_t i = 0; i < nchunks; ++i) {
         const sec_dec_chunk &c = chunks[i];
@@ -761,9 +1048,7 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
             return SEC_ESIZE;
         if (c.padlen > (uint64_t)c.k * c.B)
             return SEC_EPADLEN;
-        rc = check_sharenums(c.k, c.m, sharenums + c.slot0);
-        if (rc)
-            return rc;
+        RC(check_sharenums(c.k, c.m, sharenums + c.slot0));
         total_slots = std::max<uint64_t>(total_slots, c.slot0 + (uint64_t)c.k);
         total_out += (uint64_t)c.k * c.B - c.padlen;
     }
@@ -788,224 +1073,50 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         const void *b = host ? (const void *)blocks : nullptr;
         memcpy(key.data() + o, &b, sizeof(void *));
     }
-    const bool reuse = plan.valid && plan.gen_dec == ctx->dec_tabs.gen && plan.key == key;
-
-    // normalised slot order per chunk (needed for host gather even on reuse)
-    std::vector<int> perm_all;  // caller position for each normalised slot
-    std::vector<int> idx_all;
-    perm_all.reserve((size_t)nchunks * 4);
-    std::vector<uint64_t> chunk_slot((size_t)nchunks);
-    {
-        std::vector<int> idx, perm;
-        for (int64_t i = 0; i < nchunks; ++i) {
-            const sec_dec_chunk &c = chunks[i];
-            idx.assign(sharenums + c.slot0, sharenums + c.slot0 + c.k);
-            sec::normalise_slots(c.k, idx, perm);
-            chunk_slot[i] = perm_all.size();
-            perm_all.insert(perm_all.end(), perm.begin(), perm.end());
-            idx_all.insert(idx_all.end(), idx.begin(), idx.end());
-        }
-    }
-
+    const bool reuse = plan.valid && plan.gen == ctx->dec_tabs.gen && plan.key == key;
+    DecLayout L;
+    if (!reuse || host)
+        L = dec_layout(chunks, nchunks, sharenums);
     if (!reuse) {
         plan.valid = false;
-        std::vector<PendingExpand> pending;
-        std::vector<uint32_t> tab_of((size_t)nchunks, 0), e_of((size_t)nchunks, 0);
-        for (int attempt = 0; attempt < 2; ++attempt) {
-            pending.clear();
-            size_t need = 0;
-            bool overflow = false;
-            for (int64_t i = 0; i < nchunks && !overflow; ++i) {
-                const sec_dec_chunk &c = chunks[i];
-                const int k = c.k;
-                const int *idx = &idx_all[chunk_slot[i]];
-                std::vector<int> miss;
-                for (int s = 0; s < k; ++s)
-                    if (idx[s] >= k)
-                        miss.push_back(s);
-                e_of[i] = (uint32_t)miss.size();
-                if (miss.empty())
-                    continue;
-                std::string tk = std::to_string(k) + "/" + std::to_string(c.m) + ":";
-                for (int s = 0; s < k; ++s)
-                    tk += std::to_string(idx[s]) + ",";
-                auto it = ctx->dec_tabs.index.find(tk);
-                if (it != ctx->dec_tabs.index.end()) {
-                    tab_of[i] = it->second;
-                    continue;
-                }
-                std::vector<int> iv(idx, idx + k);
-                std::vector<uint8_t> minv;
-                if (!sec::decode_matrix(k, c.m, iv, minv))
-                    return SEC_ESINGULAR;
-                const int e = (int)miss.size();
-                std::vector<uint8_t> coef((size_t)k * e);
-                for (int s = 0; s < k; ++s)
-                    for (int r = 0; r < e; ++r)
-                        coef[(size_t)s * e + r] = minv[(size_t)miss[r] * k + s];
-                need += coef.size() * sec::kTabDwords;
-                uint32_t off = 0;
-                if (table_ensure(ctx->dec_tabs, tk, coef, pending, &off) == 1) {
-                    overflow = true;
-                    break;
-                }
-                tab_of[i] = off;
-            }
-            if (!overflow)
-                break;
-            if (attempt == 1)
-                return SEC_ENOMEM;
-            rc = table_reset(ctx, ctx->dec_tabs, need * 2 + ((size_t)1 << 18));
-            if (rc)
-                return rc;
-        }
-
-        std::vector<sec::DecDesc> descs((size_t)nchunks);
-        std::vector<uint64_t> soff(perm_all.size());
-        std::vector<uint32_t> srow(perm_all.size()), mrow(perm_all.size(), 0);
-        Bins bins;
-        std::vector<sec::TailItem> tail;
-        uint64_t in_dense = 0, out_dense = 0;
-        for (int64_t i = 0; i < nchunks; ++i) {
-            const sec_dec_chunk &c = chunks[i];
-            const uint64_t base = chunk_slot[i];
-            const int *idx = &idx_all[base];
-            uint32_t nm = 0;
-            for (int s = 0; s < c.k; ++s) {
-                const int from = perm_all[base + s];
-                soff[base + s] = host ? in_dense + (uint64_t)s * c.B : block_offs[c.slot0 + from];
-                srow[base + s] = idx[s] < c.k ? (uint32_t)idx[s] : 0xFFFFFFFFu;
-                if (idx[s] >= c.k)
-                    mrow[base + nm++] = (uint32_t)s;
-            }
-            const uint64_t nout = (uint64_t)c.k * c.B - c.padlen;
-            sec::DecDesc &d = descs[i];
-            d.out_off = host ? out_dense : c.out_off;
-            d.n = nout;
-            d.B = (uint32_t)c.B;
-            d.k = (uint32_t)c.k;
-            d.e = e_of[i];
-            d.tab = tab_of[i];
-            d.slot0 = (uint32_t)base;
-            const int64_t valid = (int64_t)nout - (int64_t)(c.k - 1) * (int64_t)c.B;
-            d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)c.B));
-            in_dense += (uint64_t)c.k * c.B;
-            out_dense += nout;
-            if (nout > 0)
-                add_work(bins, tail, (uint32_t)i, c.B, valid, (int)e_of[i]);
-        }
-        std::vector<sec::Tile> tiles;
-        flatten(bins, plan.groups, tiles);
-        plan.ntail = (uint32_t)tail.size();
-        size_t coef_bytes = 0;
-        for (auto &pe : pending)
-            coef_bytes += pe.coef.size();
-        plan.off_desc = 0;
-        plan.off_tiles = align_up(descs.size() * sizeof(sec::DecDesc), 256);
-        plan.off_tail = align_up(plan.off_tiles + tiles.size() * sizeof(sec::Tile), 256);
-        plan.off_soff = align_up(plan.off_tail + tail.size() * sizeof(sec::TailItem), 256);
-        plan.off_srow = align_up(plan.off_soff + soff.size() * 8, 256);
-        plan.off_mrow = align_up(plan.off_srow + srow.size() * 4, 256);
-        const size_t off_coef = align_up(plan.off_mrow + mrow.size() * 4, 256);
-        const size_t bytes = off_coef + coef_bytes;
-        rc = pin_wait(ctx);
-        if (!rc)
-            rc = ctx->pin.ensure(bytes);
-        if (rc)
-            return rc;
-        char *img = (char *)ctx->pin.p;
-        memcpy(img + plan.off_desc, descs.data(), descs.size() * sizeof(sec::DecDesc));
-        memcpy(img + plan.off_tiles, tiles.data(), tiles.size() * sizeof(sec::Tile));
-        memcpy(img + plan.off_tail, tail.data(), tail.size() * sizeof(sec::TailItem));
-        memcpy(img + plan.off_soff, soff.data(), soff.size() * 8);
-        memcpy(img + plan.off_srow, srow.data(), srow.size() * 4);
-        memcpy(img + plan.off_mrow, mrow.data(), mrow.size() * 4);
-        size_t o = off_coef;
-        for (auto &pe : pending) {
-            memcpy(img + o, pe.coef.data(), pe.coef.size());
-            o += pe.coef.size();
-        }
-        rc = upload_meta(ctx, plan, bytes);
-        if (!rc)
-            rc = launch_expansions(ctx, ctx->dec_tabs, plan, off_coef, pending);
-        if (rc)
-            return rc;
+        RC(build_decode_plan(ctx, chunks, nchunks, block_offs, L, host));
         plan.key.swap(key);
-        plan.gen_dec = ctx->dec_tabs.gen;
-        plan.dev_in_bytes = in_dense;
-        plan.dev_out_bytes = out_dense;
         plan.valid = true;
     }
 
-    // ---- data movement (host mode): gather blocks in normalised slot order ----
-    const uint8_t *d_blocks = blocks;
-    uint8_t *d_out = out;
-    if (host) {
-        rc = ctx->d_in.ensure(plan.dev_in_bytes);
-        if (!rc)
-            rc = ctx->d_out.ensure(plan.dev_out_bytes);
-        if (!rc)
-            rc = pin_wait(ctx);
-        if (!rc)
-            rc = ctx->pin.ensure(plan.dev_in_bytes);
-        if (rc)
-            return rc;
-        char *stage = (char *)ctx->pin.p;
+    if (!host) {
+        hipEvent_t t0 = nullptr;
+        RC(timing_begin(ctx, &t0, ctx->stream()));
+        RC(launch_decode_sub(ctx, plan, plan.subs[0], blocks, out, ctx->stream()));
+        RC(timing_end(ctx, t0, 1, ctx->stream()));
+        if (!(flags & SEC_F_ASYNC))
+            CK(hipStreamSynchronize(ctx->stream()));
+        return SEC_OK;
+    }
+    auto gather = [&](const SubPlan &sp, char *stage, std::vector<sec::CopyJob> &jobs) {
         uint64_t o = 0;
-        for (int64_t i = 0; i < nchunks; ++i) {
+        for (int64_t i = sp.c0; i < sp.c1; ++i) {
             const sec_dec_chunk &c = chunks[i];
             for (int s = 0; s < c.k; ++s) {
-                const int from = perm_all[chunk_slot[i] + s];
-                memcpy(stage + o, blocks + block_offs[c.slot0 + from], c.B);
+                const int from = L.perm[L.first[i] + s];
+                jobs.push_back(sec::CopyJob{stage + o, blocks + block_offs[c.slot0 + from], c.B});
                 o += c.B;
             }
         }
-        CK(hipMemcpyAsync(ctx->d_in.p, stage, plan.dev_in_bytes, hipMemcpyHostToDevice, ctx->stream()));
-        CK(hipEventRecord(ctx->pin_ev, ctx->stream()));
-        d_blocks = ctx->d_in.as<uint8_t>();
-        d_out = ctx->d_out.as<uint8_t>();
-    }
-
-    hipEvent_t t0 = nullptr;
-    rc = timing_begin(ctx, &t0);
-    if (rc)
-        return rc;
-    const sec::DecDesc *dd = plan.meta.as<sec::DecDesc>(plan.off_desc);
-    const sec::Tile *dt = plan.meta.as<sec::Tile>(plan.off_tiles);
-    for (const Group &g : plan.groups) {
-        int e = sec_launch_decode(g.rows, g.U, d_blocks, d_out, dd, dt + g.first, g.count,
-                                  ctx->dec_tabs.buf.as<uint32_t>(), plan.meta.as<uint64_t>(plan.off_soff),
-                                  plan.meta.as<uint32_t>(plan.off_srow), plan.meta.as<uint32_t>(plan.off_mrow),
-                                  ctx->stream());
-        if (e)
-            return hip_fail((hipError_t)e, "sec_decode_kernel");
-    }
-    if (plan.ntail) {
-        int e = sec_launch_decode_tail(d_blocks, d_out, dd, plan.meta.as<sec::TailItem>(plan.off_tail), plan.ntail,
-                                       ctx->dec_tabs.buf.as<uint32_t>(), plan.meta.as<uint64_t>(plan.off_soff),
-                                       plan.meta.as<uint32_t>(plan.off_srow), plan.meta.as<uint32_t>(plan.off_mrow),
-                                       ctx->stream());
-        if (e)
-            return hip_fail((hipError_t)e, "sec_decode_tail");
-    }
-    rc = timing_end(ctx, t0, 1);
-    if (rc)
-        return rc;
-
-    if (host) {
-        uint64_t dense = 0;
-        for (int64_t i = 0; i < nchunks; ++i) {
+    };
+    auto scatter = [&](const SubPlan &sp, char *stage, std::vector<sec::CopyJob> &jobs) {
+        uint64_t o = 0;
+        for (int64_t i = sp.c0; i < sp.c1; ++i) {
             const sec_dec_chunk &c = chunks[i];
             const uint64_t nout = (uint64_t)c.k * c.B - c.padlen;
-            if (nout)
-                CK(hipMemcpyAsync(out + c.out_off, d_out + dense, nout, hipMemcpyDeviceToHost, ctx->stream()));
-            dense += nout;
+            jobs.push_back(sec::CopyJob{out + c.out_off, stage + o, nout});
+            o += nout;
         }
-        CK(hipStreamSynchronize(ctx->stream()));
-    } else if (!(flags & SEC_F_ASYNC)) {
-        CK(hipStreamSynchronize(ctx->stream()));
-    }
-    return SEC_OK;
+    };
+    auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
+        return launch_decode_sub(ctx, plan, sp, din, dout, s);
+    };
+    return run_pipeline(ctx, plan, gather, scatter, launch);
 }
 
 // ---------------------------------------------------------------------------
@@ -1013,9 +1124,7 @@ int sec_malloc(sec_ctx *ctx, size_t bytes, void **dptr)
 {
     if (!ctx || !dptr)
         return SEC_EINVAL;
-    int rc = set_dev(ctx);
-    if (rc)
-        return rc;
+    RC(set_dev(ctx));
     if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess)
         return SEC_ENOMEM;
     return SEC_OK;
@@ -1025,9 +1134,7 @@ int sec_free(sec_ctx *ctx, void *dptr)
 {
     if (!ctx)
         return SEC_EINVAL;
-    int rc = set_dev(ctx);
-    if (rc)
-        return rc;
+    RC(set_dev(ctx));
     CK(hipFree(dptr));
     return SEC_OK;
 }
@@ -1036,9 +1143,7 @@ int sec_host_alloc(sec_ctx *ctx, size_t bytes, void **hptr)
 {
     if (!ctx || !hptr)
         return SEC_EINVAL;
-    int rc = set_dev(ctx);
-    if (rc)
-        return rc;
+    RC(set_dev(ctx));
     if (hipHostMalloc(hptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess)
         return SEC_ENOMEM;
     return SEC_OK;
@@ -1056,9 +1161,7 @@ int sec_memcpy(sec_ctx *ctx, void *dst, const void *src, size_t bytes, int kind)
 {
     if (!ctx || (bytes && (!dst || !src)) || kind < 0 || kind > 2)
         return SEC_EINVAL;
-    int rc = set_dev(ctx);
-    if (rc)
-        return rc;
+    RC(set_dev(ctx));
     static const hipMemcpyKind kinds[3] = {hipMemcpyHostToDevice, hipMemcpyDeviceToHost, hipMemcpyDeviceToDevice};
     if (bytes) {
         CK(hipMemcpyAsync(dst, src, bytes, kinds[kind], ctx->stream()));
@@ -1071,9 +1174,7 @@ int sec_memset(sec_ctx *ctx, void *dptr, int value, size_t bytes)
 {
     if (!ctx || (bytes && !dptr))
         return SEC_EINVAL;
-    int rc = set_dev(ctx);
-    if (rc)
-        return rc;
+    RC(set_dev(ctx));
     if (bytes) {
         CK(hipMemsetAsync(dptr, value, bytes, ctx->stream()));
         CK(hipStreamSynchronize(ctx->stream()));
