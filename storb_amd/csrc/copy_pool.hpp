@@ -50,7 +50,8 @@ public:
             total += j.len;
         if (threads_.empty() || total < kInline) {
             for (const auto &j : jobs)
-                memcpy(j.dst, j.src, j.len);
+                if (j.len)  // memcpy's pointers must be valid even for 0 bytes
+                    memcpy(j.dst, j.src, j.len);
             return;
         }
         {

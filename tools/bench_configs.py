@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Measures every BASELINE.json config on one MI355X (C4 at its per-GPU share) and prints one
+JSON object.  Complements bench.py (which is the C2+C3 headline line).
+
+    python tools/bench_configs.py > gpurun_out/configs.json
+
+C1  4 MiB object (reference policy: 8 x 512 KiB chunks, zfec(4,6)) and the 1 MiB object
+    (4 x 256 KiB, zfec(2,3) = BASELINE's "RS(k=2,m=1)"): loopback upload -> SHA-1 -> in-memory
+    miner dict -> retrieve -> reconstruct.  Timed twice: the reference's CPU path restated
+    (oracle/fec_oracle.c through the same piece logic, 1 thread) and storb_amd.piece on the GPU.
+C2/C3  1024 x 1 MiB RS(4,2) encode / decode ({1,3} erased), device-resident.
+C4  8192 x 64 KiB RS(10,4) (one GPU's share of 65536), device-resident encode / decode with
+    data blocks {9,0,5,2} erased.
+C5  mixed chunk sizes log-uniform in [4 KiB, 4 MiB] (seed 5) up to ~1 GiB, RS(8,3):
+    device-resident encode / decode (blocks {7,2,5} erased) and end-to-end from host memory.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+MIB = float(1 << 20)
+
+
+def timed(fn, reps):
+    fn()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return (time.perf_counter() - t0) / reps
+
+
+# ---------------------------------------------------------------- C1 loopback
+def c1_reference_cpu(data: bytes) -> float:
+    """Reference CPU path (restated): piece.py policy + zfec arithmetic via the C oracle."""
+    from oracle import cfec, zfec_ref
+
+    def run():
+        chunk_size = zfec_ref.piece_length(len(data))
+        store, meta = {}, []
+        for ci in range(math.ceil(len(data) / chunk_size)):
+            chunk = data[ci * chunk_size:(ci + 1) * chunk_size]
+            k, m, B, pad = zfec_ref.chunk_shape(len(chunk))
+            blocks = cfec.easy_encode(chunk, k, m)
+            ids = []
+            for b in blocks:
+                h = hashlib.sha1(b).hexdigest()
+                store[h] = b
+                ids.append(h)
+            meta.append((k, m, pad, ids))
+        out = []
+        for k, m, pad, ids in meta:
+            blocks = [store[h] for h in ids[:k]]
+            out.append(cfec.easy_decode(blocks, list(range(k)), pad, k, m))
+        assert b"".join(out) == data
+
+    return len(data) / timed(run, 5) / MIB
+
+
+def c1_gpu_dropin(data: bytes) -> float:
+    from storb_amd import piece
+
+    def run():
+        chunk_size = piece.piece_length(len(data))
+        store, chunks = {}, []
+        for ci in range(math.ceil(len(data) / chunk_size)):
+            info = piece.encode_chunk(data[ci * chunk_size:(ci + 1) * chunk_size], ci)
+            for p in info.pieces:
+                store[piece.piece_hash(p.data)] = p
+            chunks.append(info.model_copy(update={"pieces": None}))
+        pieces = list(store.values())
+        assert piece.reconstruct_data(pieces, chunks) == data
+
+    return len(data) / timed(run, 5) / MIB
+
+
+# ---------------------------------------------------------------- device-resident
+def enc_descs_var(sizes, k, m):
+    from storb_amd._lib import ENC_DTYPE
+
+    sizes = np.asarray(sizes, dtype=np.uint64)
+    B = (sizes + k - 1) // k
+    d = np.zeros(len(sizes), dtype=ENC_DTYPE)
+    d["in_off"] = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    d["n"] = sizes
+    d["parity_off"] = np.concatenate([[0], np.cumsum(B * (m - k))[:-1]])
+    d["parity_stride"] = B
+    d["k"], d["m"] = k, m
+    return d, B
+
+
+def dec_descs_var(sizes, k, m, B, data_base, par_base, erased):
+    from storb_amd._lib import DEC_DTYPE
+
+    keep = [s for s in range(m) if s not in erased][:k]
+    n = len(sizes)
+    sizes = np.asarray(sizes, dtype=np.uint64)
+    in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    par_off = np.concatenate([[0], np.cumsum(B * (m - k))[:-1]]).astype(np.uint64)
+    d = np.zeros(n, dtype=DEC_DTYPE)
+    d["out_off"] = in_off
+    d["B"] = B
+    d["padlen"] = B * k - sizes
+    d["slot0"] = np.arange(n, dtype=np.uint64) * k
+    d["k"], d["m"] = k, m
+    sn = np.tile(np.array(keep, np.int32), n)
+    offs = np.zeros(n * k, np.uint64)
+    for j, s in enumerate(keep):
+        offs[j::k] = (data_base + in_off + s * B) if s < k else (par_base + par_off + (s - k) * B)
+    return d, sn, offs
+
+
+def device_case(eng, sizes, k, m, erased, reps=20):
+    import torch
+
+    assert (k - 1) in erased or all(int(s) % k == 0 for s in sizes)
+    total = int(np.sum(sizes))
+    ed, B = enc_descs_var(sizes, k, m)
+    src = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda")
+    par = torch.empty(int(np.sum(B)) * (m - k), dtype=torch.uint8, device="cuda")
+    out = torch.empty_like(src)
+    dd, sn, offs = dec_descs_var(sizes, k, m, B, src.data_ptr(), par.data_ptr(), erased)
+    eng.encode_batch(ed, src, par)
+    eng.decode_batch(dd, sn, offs, 0, out)
+    assert torch.equal(out, src)
+    eng.set_timing(True)
+    for _ in range(reps):
+        eng.encode_batch(ed, src, par, asynchronous=True)
+    for _ in range(reps):
+        eng.decode_batch(dd, sn, offs, 0, out, asynchronous=True)
+    eng.sync()
+    eng.set_timing(False)
+    ems, en = eng.collect_timing("encode")
+    dms, dn = eng.collect_timing("decode")
+    te, td = ems / en / 1e3, dms / dn / 1e3
+    enc_bytes = total + int(np.sum(B)) * (m - k)
+    dec_bytes = int(np.sum(B)) * k + total
+    return {"chunks": len(sizes), "input_bytes": total, "encode_ms": round(te * 1e3, 4),
+            "encode_gibs": round(total / te / GIB, 2), "encode_hbm_GBs": round(enc_bytes / te / 1e9, 1),
+            "decode_ms": round(td * 1e3, 4), "decode_gibs": round(total / td / GIB, 2),
+            "decode_hbm_GBs": round(dec_bytes / td / 1e9, 1)}
+
+
+def host_case(eng, sizes, k, m, erased, reps=3):
+    total = int(np.sum(sizes))
+    rng = np.random.default_rng(55)
+    host = rng.integers(0, 256, total, dtype=np.uint8)
+    ed, B = enc_descs_var(sizes, k, m)
+    par = np.empty(int(np.sum(B)) * (m - k), dtype=np.uint8)
+    out = np.empty_like(host)
+    dd, sn, offs = dec_descs_var(sizes, k, m, B, host.ctypes.data, par.ctypes.data, erased)
+    te = timed(lambda: eng.encode_batch(ed, host, par, host=True), reps)
+    td = timed(lambda: eng.decode_batch(dd, sn, offs, 0, out, host=True), reps)
+    assert np.array_equal(out, host)
+    return {"encode_gibs": round(total / te / GIB, 2), "decode_gibs": round(total / td / GIB, 2)}
+
+
+def main():
+    from storb_amd.engine import Engine
+
+    eng = Engine(0)
+    res = {}
+    rng = np.random.default_rng(1)
+    for label, size in (("c1_4MiB_object_zfec(4,6)", 4 << 20), ("c1_1MiB_object_zfec(2,3)", 1 << 20)):
+        data = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+        res[label] = {"reference_cpu_restated_MiBs": round(c1_reference_cpu(data), 1),
+                      "storb_amd_gpu_dropin_MiBs": round(c1_gpu_dropin(data), 1),
+                      "note": "loopback: encode_chunk -> sha1 -> dict store -> reconstruct_data; "
+                              "reference path = piece.py policy + oracle/fec_oracle.c (zfec restated), 1 thread"}
+    res["c2_c3_1024x1MiB_rs(4,2)"] = device_case(eng, [1 << 20] * 1024, 4, 6, (1, 3))
+    res["c4_8192x64KiB_rs(10,4)_per_gpu"] = device_case(eng, [65536] * 8192, 10, 14, (9, 0, 5, 2))
+    r5 = np.random.default_rng(5)
+    sizes, tot = [], 0
+    while tot < (1 << 30):
+        s = int(np.exp(r5.uniform(np.log(4096), np.log(4 << 20))))
+        sizes.append(s)
+        tot += s
+    res["c5_mixed_4KiB-4MiB_rs(8,3)_device"] = device_case(eng, sizes, 8, 11, (7, 2, 5))
+    res["c5_mixed_4KiB-4MiB_rs(8,3)_e2e_host"] = host_case(eng, sizes, 8, 11, (7, 2, 5))
+    res["c2_1024x1MiB_rs(4,2)_e2e_host"] = host_case(eng, [1 << 20] * 1024, 4, 6, (1, 3))
+    print(json.dumps(res, indent=1))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
