@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -91,6 +92,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     path = path or os.environ.get("STORB_EC_LIB", LIB)
     if path in _libs:
         return _libs[path]
+    _share_torch_runtime()
     if not os.path.exists(path):
         raise ImportError(
             f"libstorbec.so not found at {path}: build it with `python -m storb_amd._build` "
@@ -104,6 +106,23 @@ def load(path: str | None = None) -> ctypes.CDLL:
         raise ImportError("libstorbec.so ABI version mismatch")
     _libs[path] = lib
     return lib
+
+
+def _share_torch_runtime() -> None:
+    """Load torch's bundled HIP runtime before libstorbec.so when torch is installed.
+
+    ROCm torch wheels ship their own libamdhip64.so / libhsa-runtime64.so.  If libstorbec
+    pulled /opt/rocm's runtime in first, a later `import torch` would start a second HIP
+    runtime in the process that sees no GPU ("No HIP GPUs are available").  Loaded after
+    torch, libstorbec's NEEDED libamdhip64.so.7 resolves to torch's copy: one runtime, and
+    torch tensors / streams interoperate.  STORB_EC_PRELOAD_TORCH=0 skips this.
+    """
+    if "torch" in sys.modules or os.environ.get("STORB_EC_PRELOAD_TORCH", "1") == "0":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 
 
 def strerror(code: int, lib: ctypes.CDLL | None = None) -> str:

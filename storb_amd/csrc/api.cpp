@@ -977,10 +977,23 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
     if ((!in && !host) || !parity)
         return SEC_EINVAL;
 
+    // Plan key: the whole descriptor array for device mode; only the shapes for
+    // host mode (its device layout is dense, caller addresses are used by the
+    // gather / scatter alone), so repeated per-chunk calls reuse one plan.
     Plan &plan = ctx->enc_plan;
-    std::vector<uint8_t> key(sizeof(sec_enc_chunk) * (size_t)nchunks + sizeof(unsigned));
-    memcpy(key.data(), chunks, sizeof(sec_enc_chunk) * (size_t)nchunks);
-    memcpy(key.data() + sizeof(sec_enc_chunk) * (size_t)nchunks, &flags, sizeof(unsigned));
+    std::vector<uint8_t> key;
+    if (host) {
+        key.resize((size_t)nchunks * 16 + sizeof(unsigned));
+        for (int64_t i = 0; i < nchunks; ++i) {
+            memcpy(key.data() + i * 16, &chunks[i].n, 8);
+            memcpy(key.data() + i * 16 + 8, &chunks[i].k, 4);
+            memcpy(key.data() + i * 16 + 12, &chunks[i].m, 4);
+        }
+    } else {
+        key.resize(sizeof(sec_enc_chunk) * (size_t)nchunks + sizeof(unsigned));
+        memcpy(key.data(), chunks, sizeof(sec_enc_chunk) * (size_t)nchunks);
+    }
+    memcpy(key.data() + key.size() - sizeof(unsigned), &flags, sizeof(unsigned));
     if (!(plan.valid && plan.gen == ctx->enc_tabs.gen && plan.key == key)) {
         plan.valid = false;
         RC(build_encode_plan(ctx, chunks, nchunks, host));
@@ -1057,22 +1070,28 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
     if (!out)  // blocks may be NULL: block_offs are then absolute addresses
         return SEC_EINVAL;
 
+    // Plan key (see sec_encode_batch): host mode keys on shapes + sharenums only.
     Plan &plan = ctx->dec_plan;
-    const size_t kc = sizeof(sec_dec_chunk) * (size_t)nchunks;
-    std::vector<uint8_t> key(kc + total_slots * (4 + 8) + sizeof(unsigned) + sizeof(void *));
-    {
-        size_t o = 0;
-        memcpy(key.data() + o, chunks, kc);
-        o += kc;
-        memcpy(key.data() + o, sharenums, total_slots * 4);
-        o += total_slots * 4;
-        memcpy(key.data() + o, block_offs, total_slots * 8);
-        o += total_slots * 8;
-        memcpy(key.data() + o, &flags, sizeof(unsigned));
-        o += sizeof(unsigned);
-        const void *b = host ? (const void *)blocks : nullptr;
-        memcpy(key.data() + o, &b, sizeof(void *));
+    std::vector<uint8_t> key;
+    if (host) {
+        for (int64_t i = 0; i < nchunks; ++i) {
+            const sec_dec_chunk &c = chunks[i];
+            const size_t o = key.size();
+            key.resize(o + 24 + (size_t)c.k * 4);
+            memcpy(key.data() + o, &c.B, 8);
+            memcpy(key.data() + o + 8, &c.padlen, 8);
+            memcpy(key.data() + o + 16, &c.k, 4);
+            memcpy(key.data() + o + 20, &c.m, 4);
+            memcpy(key.data() + o + 24, sharenums + c.slot0, (size_t)c.k * 4);
+        }
+    } else {
+        const size_t kc = sizeof(sec_dec_chunk) * (size_t)nchunks;
+        key.resize(kc + total_slots * (4 + 8));
+        memcpy(key.data(), chunks, kc);
+        memcpy(key.data() + kc, sharenums, total_slots * 4);
+        memcpy(key.data() + kc + total_slots * 4, block_offs, total_slots * 8);
     }
+    key.insert(key.end(), (const uint8_t *)&flags, (const uint8_t *)&flags + sizeof(unsigned));
     const bool reuse = plan.valid && plan.gen == ctx->dec_tabs.gen && plan.key == key;
     DecLayout L;
     if (!reuse || host)
