@@ -139,6 +139,28 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
                      const int32_t *sharenums, const uint64_t *block_offs,
                      const uint8_t *blocks, uint8_t *out, unsigned flags);
 
+/* ---- piece ids: SHA-1 (piece_hash, /root/reference/storb/util/piece.py:54-68) ----
+ * A message is `len` bytes at `addr`, of which the first `avail` exist in
+ * memory and the rest read as zero (so zfec's zero-padded last data block can
+ * be hashed in place).  digests: 20 bytes per message, in order.
+ * Device mode: addr / digests are device memory.  SEC_F_HOST: both are host
+ * memory (messages are staged through pinned slabs).                        */
+typedef struct sec_msg {
+    uint64_t addr;
+    uint64_t len;
+    uint64_t avail;
+} sec_msg;
+
+int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *digests, unsigned flags);
+
+/* Encode + the SHA-1 of every one of the chunk's m blocks (the piece ids the
+ * validator computes right after encode, validator.py:1081), while data and
+ * parity are still on the device.  Block j of chunk c gets digest slot
+ * M_c + j with M_c = sum of m over chunks before c; digests (20 B per slot)
+ * live where the parity does (device, or host with SEC_F_HOST). */
+int sec_encode_digest_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
+                            const uint8_t *in, uint8_t *parity, uint8_t *digests, unsigned flags);
+
 /* ---- memory helpers for hosts without a device allocator ----------------- */
 int sec_malloc(sec_ctx *ctx, size_t bytes, void **dptr);
 int sec_free(sec_ctx *ctx, void *dptr);

@@ -51,7 +51,15 @@ ENC_DTYPE = np.dtype([("in_off", "<u8"), ("n", "<u8"), ("parity_off", "<u8"), ("
                       ("k", "<i4"), ("m", "<i4")], align=True)
 DEC_DTYPE = np.dtype([("out_off", "<u8"), ("B", "<u8"), ("padlen", "<u8"), ("slot0", "<u8"),
                       ("k", "<i4"), ("m", "<i4")], align=True)
+MSG_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u8"), ("avail", "<u8")], align=True)
+
+
+class sec_msg(ctypes.Structure):
+    _fields_ = [("addr", ctypes.c_uint64), ("len", ctypes.c_uint64), ("avail", ctypes.c_uint64)]
+
+
 assert ENC_DTYPE.itemsize == ctypes.sizeof(sec_enc_chunk) == 40
+assert MSG_DTYPE.itemsize == ctypes.sizeof(sec_msg) == 24
 assert DEC_DTYPE.itemsize == ctypes.sizeof(sec_dec_chunk) == 40
 
 # every symbol include/storb_ec.h declares: name -> (restype, argtypes)
@@ -72,6 +80,8 @@ _SIGS = {
     "sec_decode_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
     "sec_encode_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint]),
     "sec_decode_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_uint]),
+    "sec_sha1_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, ctypes.c_uint]),
+    "sec_encode_digest_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_uint]),
     "sec_malloc": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
     "sec_free": (ctypes.c_int, [_vp, _vp]),
     "sec_host_alloc": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),

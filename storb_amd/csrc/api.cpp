@@ -136,6 +136,10 @@ struct SubPlan {
     size_t off_desc = 0, off_tiles = 0, off_tail = 0, off_soff = 0, off_srow = 0, off_mrow = 0;
     uint32_t ntail = 0;
     uint64_t in_bytes = 0, out_bytes = 0;  // dense slab sizes (host mode)
+    size_t off_msgs = 0;                   // SHA-1 messages of this unit
+    uint32_t nmsgs = 0;
+    uint64_t dig_first = 0;                // first digest slot of this unit
+    uint64_t dig_off = 0;                  // host mode: digests' offset in the slab output
 };
 
 struct Plan {
@@ -275,7 +279,7 @@ struct sec_ctx {
     PinBuf pin;  // metadata image staging
     hipEvent_t pin_ev = nullptr, meta_ev = nullptr;
     TableCache enc_tabs, dec_tabs;
-    Plan enc_plan, dec_plan;
+    Plan enc_plan, dec_plan, sha_plan;
     Slot slots[kSlots];
     std::unique_ptr<sec::CopyPool> pool;
 
@@ -440,7 +444,7 @@ int check_sharenums(int k, int m, const int32_t *s)
 uint64_t enc_B(const sec_enc_chunk &c) { return (c.n + (uint64_t)c.k - 1) / (uint64_t)c.k; }
 
 // ---- encode plan ------------------------------------------------------------
-int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, bool host)
+int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, bool host, bool digest)
 {
     Plan &plan = ctx->enc_plan;
     TableCache &tc = ctx->enc_tabs;
@@ -493,13 +497,16 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
     }
     Image img;
     plan.subs.clear();
+    uint64_t dig = 0;
     for (auto [c0, c1] : ranges) {
         SubPlan sp;
         sp.c0 = c0;
         sp.c1 = c1;
+        sp.dig_first = dig;
         std::vector<sec::EncDesc> descs((size_t)(c1 - c0));
         Bins bins;
         std::vector<sec::TailItem> tail;
+        std::vector<sec::MsgDesc> msgs;
         for (int64_t i = c0; i < c1; ++i) {
             const sec_enc_chunk &c = chunks[i];
             const uint64_t B = enc_B(c);
@@ -515,6 +522,17 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             d.tab = tab_of[i];
             d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)B));
             d.pad = 0;
+            if (digest) {  // data blocks from the input (padding synthesised), then parity
+                for (int j = 0; j < c.k; ++j) {
+                    const int64_t av = (int64_t)c.n - (int64_t)j * (int64_t)B;
+                    msgs.push_back(sec::MsgDesc{d.in_off + (uint64_t)j * B, B,
+                                                (uint64_t)std::max<int64_t>(0, std::min<int64_t>(av, (int64_t)B)), 0,
+                                                0});
+                }
+                for (int r = 0; r < p; ++r)
+                    msgs.push_back(sec::MsgDesc{d.par_off + (uint64_t)r * d.par_stride, B, B, 1, 0});
+                dig += (uint64_t)c.m;
+            }
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
             if (p > 0)
@@ -523,9 +541,14 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles);
         sp.ntail = (uint32_t)tail.size();
+        sp.nmsgs = (uint32_t)msgs.size();
+        sp.dig_off = sp.out_bytes;  // host mode: digests follow the slab's parity
+        if (host)
+            sp.out_bytes += (uint64_t)msgs.size() * 20;
         sp.off_desc = img.put(descs.data(), descs.size() * sizeof(sec::EncDesc));
         sp.off_tiles = img.put(tiles.data(), tiles.size() * sizeof(sec::Tile));
         sp.off_tail = img.put(tail.data(), tail.size() * sizeof(sec::TailItem));
+        sp.off_msgs = img.put(msgs.data(), msgs.size() * sizeof(sec::MsgDesc));
         plan.subs.push_back(std::move(sp));
     }
     RC(upload_plan(ctx, plan, img, tc, pending));
@@ -534,7 +557,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
 }
 
 int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const uint8_t *in, uint8_t *par,
-                      hipStream_t s)
+                      uint8_t *digests, hipStream_t s)
 {
     const sec::EncDesc *dd = plan.meta.as<sec::EncDesc>(sp.off_desc);
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
@@ -548,6 +571,11 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
         int e = sec_launch_encode_tail(in, par, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs, s);
         if (e)
             return hip_fail((hipError_t)e, "sec_encode_tail");
+    }
+    if (sp.nmsgs) {
+        int e = sec_launch_sha1(in, par, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, digests, s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_sha1_kernel");
     }
     return SEC_OK;
 }
@@ -859,6 +887,7 @@ void sec_ctx_destroy(sec_ctx *ctx)
     ctx->dec_tabs.buf.release();
     ctx->enc_plan.meta.release();
     ctx->dec_plan.meta.release();
+    ctx->sha_plan.meta.release();
     if (ctx->own)
         (void)hipStreamDestroy(ctx->own);
     delete ctx;
@@ -944,8 +973,13 @@ int sec_decode_matrix(int k, int m, const int32_t *sharenums, uint8_t *out, int3
 }
 
 // ---------------------------------------------------------------------------
-int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
-                     uint8_t *parity, unsigned flags)
+}  // extern "C"
+
+namespace {
+
+// sec_encode_batch (digests == nullptr, digest == false) and sec_encode_digest_batch.
+int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in, uint8_t *parity,
+                uint8_t *digests, unsigned flags, bool digest)
 {
     if (!ctx || nchunks < 0 || (nchunks > 0 && !chunks) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC)))
         return SEC_EINVAL;
@@ -957,7 +991,7 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
     RC(set_dev(ctx));
 
     // easyfec.Encoder.encode / _fec.Encoder preconditions
-    uint64_t total_par = 0;
+    uint64_t total_par = 0, total_in = 0;
     for (int64_t i = 0; i < nchunks; ++i) {
         const sec_enc_chunk &c = chunks[i];
         if (c.k < 1 || c.m < c.k || c.m > 256)
@@ -971,10 +1005,11 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
         if (p > 0 && B > 0 && c.parity_stride < B)
             return SEC_EINVAL;
         total_par += p * B;
+        total_in += c.n;
     }
-    if (total_par == 0)
+    if (total_par == 0 && !digest)
         return SEC_OK;  // nothing to compute (m == k, or empty chunks)
-    if ((!in && !host) || !parity)
+    if ((!in && !host && total_in) || (!parity && total_par) || (digest && !digests))
         return SEC_EINVAL;
 
     // Plan key: the whole descriptor array for device mode; only the shapes for
@@ -983,20 +1018,21 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
     Plan &plan = ctx->enc_plan;
     std::vector<uint8_t> key;
     if (host) {
-        key.resize((size_t)nchunks * 16 + sizeof(unsigned));
+        key.resize((size_t)nchunks * 16);
         for (int64_t i = 0; i < nchunks; ++i) {
             memcpy(key.data() + i * 16, &chunks[i].n, 8);
             memcpy(key.data() + i * 16 + 8, &chunks[i].k, 4);
             memcpy(key.data() + i * 16 + 12, &chunks[i].m, 4);
         }
     } else {
-        key.resize(sizeof(sec_enc_chunk) * (size_t)nchunks + sizeof(unsigned));
+        key.resize(sizeof(sec_enc_chunk) * (size_t)nchunks);
         memcpy(key.data(), chunks, sizeof(sec_enc_chunk) * (size_t)nchunks);
     }
-    memcpy(key.data() + key.size() - sizeof(unsigned), &flags, sizeof(unsigned));
+    const unsigned kflags = flags | (digest ? 0x10000u : 0u);
+    key.insert(key.end(), (const uint8_t *)&kflags, (const uint8_t *)&kflags + sizeof(unsigned));
     if (!(plan.valid && plan.gen == ctx->enc_tabs.gen && plan.key == key)) {
         plan.valid = false;
-        RC(build_encode_plan(ctx, chunks, nchunks, host));
+        RC(build_encode_plan(ctx, chunks, nchunks, host, digest));
         plan.key.swap(key);
         plan.valid = true;
     }
@@ -1004,7 +1040,7 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
     if (!host) {
         hipEvent_t t0 = nullptr;
         RC(timing_begin(ctx, &t0, ctx->stream()));
-        RC(launch_encode_sub(ctx, plan, plan.subs[0], in, parity, ctx->stream()));
+        RC(launch_encode_sub(ctx, plan, plan.subs[0], in, parity, digests, ctx->stream()));
         RC(timing_end(ctx, t0, 0, ctx->stream()));
         if (!(flags & SEC_F_ASYNC))
             CK(hipStreamSynchronize(ctx->stream()));
@@ -1030,9 +1066,111 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
             }
             o += p * B;
         }
+        if (sp.nmsgs)
+            jobs.push_back(sec::CopyJob{digests + sp.dig_first * 20, stage + sp.dig_off, (size_t)sp.nmsgs * 20});
     };
     auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
-        return launch_encode_sub(ctx, plan, sp, din, dout, s);
+        return launch_encode_sub(ctx, plan, sp, din, dout, dout + sp.dig_off, s);
+    };
+    return run_pipeline(ctx, plan, gather, scatter, launch);
+}
+
+}  // namespace
+
+extern "C" {
+
+int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
+                     uint8_t *parity, unsigned flags)
+{
+    return encode_impl(ctx, chunks, nchunks, in, parity, nullptr, flags, false);
+}
+
+int sec_encode_digest_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
+                            uint8_t *parity, uint8_t *digests, unsigned flags)
+{
+    return encode_impl(ctx, chunks, nchunks, in, parity, digests, flags, true);
+}
+
+int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *digests, unsigned flags)
+{
+    if (!ctx || nmsgs < 0 || (nmsgs > 0 && (!msgs || !digests)) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC)) ||
+        nmsgs >= (int64_t)UINT32_MAX)
+        return SEC_EINVAL;
+    if (nmsgs == 0)
+        return SEC_OK;
+    const bool host = flags & SEC_F_HOST;
+    RC(set_dev(ctx));
+    Plan &plan = ctx->sha_plan;
+    std::vector<uint8_t> key;
+    if (host) {  // dense staging: only lengths matter
+        key.resize((size_t)nmsgs * 16);
+        for (int64_t i = 0; i < nmsgs; ++i) {
+            const uint64_t av = std::min(msgs[i].avail, msgs[i].len);
+            memcpy(key.data() + i * 16, &msgs[i].len, 8);
+            memcpy(key.data() + i * 16 + 8, &av, 8);
+        }
+    } else {
+        key.assign((const uint8_t *)msgs, (const uint8_t *)(msgs + nmsgs));
+    }
+    key.insert(key.end(), (const uint8_t *)&flags, (const uint8_t *)&flags + sizeof(unsigned));
+    if (!(plan.valid && plan.key == key)) {
+        plan.valid = false;
+        std::vector<std::pair<int64_t, int64_t>> ranges;
+        if (host) {
+            std::vector<uint64_t> ib((size_t)nmsgs);
+            for (int64_t i = 0; i < nmsgs; ++i)
+                ib[i] = std::min(msgs[i].avail, msgs[i].len);
+            ranges = slabs_of(ib, env_size("SEC_SLAB_BYTES", (size_t)64 << 20));
+        } else {
+            ranges.emplace_back(0, nmsgs);
+        }
+        Image img;
+        plan.subs.clear();
+        for (auto [c0, c1] : ranges) {
+            SubPlan sp;
+            sp.c0 = c0;
+            sp.c1 = c1;
+            sp.dig_first = (uint64_t)c0;
+            std::vector<sec::MsgDesc> md;
+            for (int64_t i = c0; i < c1; ++i) {
+                const uint64_t av = std::min(msgs[i].avail, msgs[i].len);
+                md.push_back(sec::MsgDesc{host ? sp.in_bytes : msgs[i].addr, msgs[i].len, av, 0, 0});
+                sp.in_bytes += av;
+            }
+            sp.nmsgs = (uint32_t)md.size();
+            sp.out_bytes = (uint64_t)md.size() * 20;
+            sp.off_msgs = img.put(md.data(), md.size() * sizeof(sec::MsgDesc));
+            plan.subs.push_back(std::move(sp));
+        }
+        std::vector<PendingExpand> none;
+        RC(upload_plan(ctx, plan, img, ctx->enc_tabs, none));
+        plan.key.swap(key);
+        plan.valid = true;
+    }
+    if (!host) {
+        const SubPlan &sp = plan.subs[0];
+        int e = sec_launch_sha1(nullptr, nullptr, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, digests,
+                                ctx->stream());
+        if (e)
+            return hip_fail((hipError_t)e, "sec_sha1_kernel");
+        if (!(flags & SEC_F_ASYNC))
+            CK(hipStreamSynchronize(ctx->stream()));
+        return SEC_OK;
+    }
+    auto gather = [&](const SubPlan &sp, char *stage, std::vector<sec::CopyJob> &jobs) {
+        uint64_t o = 0;
+        for (int64_t i = sp.c0; i < sp.c1; ++i) {
+            const uint64_t av = std::min(msgs[i].avail, msgs[i].len);
+            jobs.push_back(sec::CopyJob{stage + o, (const void *)(uintptr_t)msgs[i].addr, av});
+            o += av;
+        }
+    };
+    auto scatter = [&](const SubPlan &sp, char *stage, std::vector<sec::CopyJob> &jobs) {
+        jobs.push_back(sec::CopyJob{digests + sp.dig_first * 20, stage, (size_t)sp.nmsgs * 20});
+    };
+    auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
+        int e = sec_launch_sha1(din, nullptr, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, dout, s);
+        return e ? hip_fail((hipError_t)e, "sec_sha1_kernel") : SEC_OK;
     };
     return run_pipeline(ctx, plan, gather, scatter, launch);
 }

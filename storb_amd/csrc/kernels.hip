@@ -357,6 +357,121 @@ __global__ __launch_bounds__(256) void sec_decode_tail(const u8 *__restrict__ bl
     }
 }
 
+// ---- SHA-1 of pieces (storb piece ids, /root/reference/storb/util/piece.py:54-68) ----
+// One lane per message: SHA-1 is a sequential chain of 64-byte compressions, so a
+// message cannot be split; the kernel is latency-bound on each lane's round chain
+// and wants many messages in flight.  Words are loaded 16 B at a time (unaligned
+// allowed) and byte-swapped to SHA-1's big-endian order.
+__device__ __forceinline__ u32 rotl(u32 x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+
+__device__ __forceinline__ void sha1_compress(u32 (&h)[5], u32 (&w)[16])
+{
+    u32 a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) {
+        u32 wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+            w[t & 15] = wt;
+        }
+        u32 f, k;
+        if (t < 20) {
+            f = (b & c) | (~b & d);
+            k = 0x5A827999u;
+        } else if (t < 40) {
+            f = b ^ c ^ d;
+            k = 0x6ED9EBA1u;
+        } else if (t < 60) {
+            f = (b & c) | (b & d) | (c & d);
+            k = 0x8F1BBCDCu;
+        } else {
+            f = b ^ c ^ d;
+            k = 0xCA62C1D6u;
+        }
+        const u32 tmp = rotl(a, 5) + f + e + k + wt;
+        e = d;
+        d = c;
+        c = rotl(b, 30);
+        b = a;
+        a = tmp;
+    }
+    h[0] += a;
+    h[1] += b;
+    h[2] += c;
+    h[3] += d;
+    h[4] += e;
+}
+
+// byte i of the message: real below `avail`, zero from there to `len`
+__device__ __forceinline__ u32 msg_byte(const u8 *p, uint64_t i, uint64_t avail) { return i < avail ? p[i] : 0u; }
+
+__global__ __launch_bounds__(64) void sec_sha1_kernel(const u8 *__restrict__ base0, const u8 *__restrict__ base1,
+                                                      const sec::MsgDesc *__restrict__ msgs, u32 nmsgs,
+                                                      u8 *__restrict__ digests)
+{
+    const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nmsgs)
+        return;
+    const sec::MsgDesc m = msgs[i];
+    const u8 *p = (m.base ? base1 : base0) + m.off;
+    u32 h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+    u32 w[16];
+    const uint64_t nfull = m.len / 64;
+    for (uint64_t blk = 0; blk < nfull; ++blk) {
+        const uint64_t o = blk * 64;
+        if (o + 64 <= m.avail) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const u32x4 v = *reinterpret_cast<const u32x4_u *>(p + o + 16 * q);
+                w[4 * q + 0] = __builtin_bswap32(v.x);
+                w[4 * q + 1] = __builtin_bswap32(v.y);
+                w[4 * q + 2] = __builtin_bswap32(v.z);
+                w[4 * q + 3] = __builtin_bswap32(v.w);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                u32 x = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    x = (x << 8) | msg_byte(p, o + 4 * q + b, m.avail);
+                w[q] = x;
+            }
+        }
+        sha1_compress(h, w);
+    }
+    // final block(s): remaining bytes, 0x80, zeros, 64-bit big-endian bit length
+    const uint64_t o = nfull * 64;
+    const u32 rem = (u32)(m.len - o);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        u32 x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const u32 pos = 4 * q + b;
+            const u32 byte = pos < rem ? msg_byte(p, o + pos, m.avail) : (pos == rem ? 0x80u : 0u);
+            x = (x << 8) | byte;
+        }
+        w[q] = x;
+    }
+    const uint64_t bits = m.len * 8;
+    if (rem >= 56) {
+        sha1_compress(h, w);
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            w[q] = 0;
+    }
+    w[14] = (u32)(bits >> 32);
+    w[15] = (u32)bits;
+    sha1_compress(h, w);
+    u32 *out = reinterpret_cast<u32 *>(digests + (uint64_t)i * 20);
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+        out[q] = __builtin_bswap32(h[q]);
+}
+
 template <int R, int U>
 hipError_t launch_enc(const u8 *in, u8 *par, const sec::EncDesc *descs, const sec::Tile *tiles, u32 ntiles,
                       const u32 *tabs, hipStream_t s)
@@ -457,6 +572,16 @@ int sec_launch_decode(int rows, int U, const uint8_t *blocks, uint8_t *out, cons
     case 4: return dispatch_dec<4>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDesc *msgs, uint32_t nmsgs,
+                    uint8_t *digests, void *stream)
+{
+    if (nmsgs == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_sha1_kernel, dim3((nmsgs + 63) / 64), dim3(64), 0, (hipStream_t)stream, base0, base1,
+                       msgs, nmsgs, digests);
+    return hipGetLastError();
 }
 
 int sec_launch_decode_tail(const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,

@@ -57,6 +57,17 @@ struct TailItem {
     uint32_t t;
 };
 
+// One SHA-1 message (a piece): `len` bytes at bases[base] + off, of which the
+// first `avail` exist in memory; the rest read as zero (zfec's padding of the
+// last data block, which is part of that piece's bytes).
+struct MsgDesc {
+    uint64_t off;
+    uint64_t len;
+    uint64_t avail;
+    uint32_t base;  // 0 or 1: which of the launch's two base pointers
+    uint32_t pad;
+};
+
 }  // namespace sec
 
 // launchers (kernels.hip); all enqueue on `stream` and return hipError_t as int
@@ -70,6 +81,8 @@ int sec_launch_decode(int rows, int U, const uint8_t *blocks, uint8_t *out, cons
                       const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
                       const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,
                       void *stream);
+int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDesc *msgs, uint32_t nmsgs,
+                    uint8_t *digests, void *stream);
 int sec_launch_decode_tail(const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
                            const sec::TailItem *items, uint32_t nitems, const uint32_t *tabs,
                            const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,

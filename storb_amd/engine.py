@@ -21,7 +21,7 @@ import threading
 import numpy as np
 
 from . import _lib
-from ._lib import DEC_DTYPE, ENC_DTYPE, SEC_F_ASYNC, SEC_F_HOST
+from ._lib import DEC_DTYPE, ENC_DTYPE, MSG_DTYPE, SEC_F_ASYNC, SEC_F_HOST
 
 
 class Error(Exception):
@@ -139,11 +139,44 @@ class Engine:
         self._check(self.lib.sec_decode_batch(self._ctx, _ptr(descs), len(descs), _ptr(sn), _ptr(bo), b or None,
                                         o or None, flags))
 
+    def encode_digest_batch(self, descs: np.ndarray, src, parity, digests, *, host: bool = False,
+                            asynchronous: bool = False) -> None:
+        """Encode + SHA-1 of every block (20 B per block, chunk-major) — sec_encode_digest_batch."""
+        descs = np.ascontiguousarray(descs, dtype=ENC_DTYPE)
+        s, _ks = addr(src)
+        p, _kp = addr(parity)
+        g, _kg = addr(digests)
+        flags = (SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0)
+        self._check(self.lib.sec_encode_digest_batch(self._ctx, _ptr(descs), len(descs), s or None, p or None,
+                                                     g or None, flags))
+
+    def sha1_batch(self, msgs: np.ndarray, digests, *, host: bool = False, asynchronous: bool = False) -> None:
+        """SHA-1 of each (addr, len, avail) message into 20-byte digests — sec_sha1_batch."""
+        msgs = np.ascontiguousarray(msgs, dtype=MSG_DTYPE)
+        g, _kg = addr(digests)
+        flags = (SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0)
+        self._check(self.lib.sec_sha1_batch(self._ctx, _ptr(msgs), len(msgs), g or None, flags))
+
     # -- host batches ---------------------------------------------------------
-    def encode_host(self, chunks, shapes) -> list[list[bytes]]:
+    def sha1_host(self, datas) -> list[bytes]:
+        """SHA-1 digests (20 bytes each) of host byte strings, hashed on the GPU."""
+        msgs = np.zeros(len(datas), dtype=MSG_DTYPE)
+        keep = []
+        for i, d in enumerate(datas):
+            a, kp = addr(d)
+            keep.append(kp)
+            ln = len(kp) if isinstance(kp, np.ndarray) else len(d)
+            msgs[i] = (a, ln, ln)
+        out = np.empty(max(20 * len(datas), 1), dtype=np.uint8)
+        self.sha1_batch(msgs, out, host=True)
+        mv = memoryview(out)
+        return [bytes(mv[20 * i:20 * (i + 1)]) for i in range(len(datas))]
+
+    def encode_host(self, chunks, shapes, digests: bool = False):
         """Parity blocks for each chunk.  chunks: bytes-like list; shapes: [(k, m)] per chunk.
 
-        Returns, per chunk, the m-k secondary blocks (block numbers k..m-1) as bytes.
+        Returns, per chunk, the m-k secondary blocks (block numbers k..m-1) as bytes; with
+        ``digests=True`` also, per chunk, the SHA-1 digests of all m blocks (GPU-computed).
         """
         n = len(chunks)
         descs = np.zeros(n, dtype=ENC_DTYPE)
@@ -159,9 +192,18 @@ class Engine:
             blocks.append((total, B, m - k))
             total += (m - k) * B
         out = np.empty(max(total, 1), dtype=np.uint8)
-        self.encode_batch(descs, 0, out, host=True)
-        mv = memoryview(out)
-        return [[bytes(mv[o + r * B:o + (r + 1) * B]) for r in range(p)] for (o, B, p) in blocks]
+        if not digests:
+            self.encode_batch(descs, 0, out, host=True)
+            mv = memoryview(out)
+            return [[bytes(mv[o + r * B:o + (r + 1) * B]) for r in range(p)] for (o, B, p) in blocks]
+        ms = [m for (_, m) in shapes]
+        dig = np.empty(max(20 * sum(ms), 1), dtype=np.uint8)
+        self.encode_digest_batch(descs, 0, out, dig, host=True)
+        mv, dv = memoryview(out), memoryview(dig)
+        par = [[bytes(mv[o + r * B:o + (r + 1) * B]) for r in range(p)] for (o, B, p) in blocks]
+        first = np.concatenate([[0], np.cumsum(ms)[:-1]]).astype(int) if ms else []
+        digs = [[bytes(dv[20 * (f + j):20 * (f + j + 1)]) for j in range(m)] for f, m in zip(first, ms)]
+        return par, digs
 
     def decode_host(self, items, out=None) -> bytes:
         """Reassemble chunks from host blocks, concatenated in order.

@@ -38,7 +38,7 @@ logger = logging.getLogger(__name__)
 __all__ = [
     "PieceType", "Piece", "EncodedChunk", "ProcessedPieceInfo", "EncodedPieces", "piece_hash", "piece_length",
     "encode_chunk", "decode_chunk", "reconstruct_data", "reconstruct_data_stream", "encode_chunks",
-    "decode_chunks", "chunk_shape", "Encoder", "Decoder", "Error",
+    "decode_chunks", "chunk_shape", "piece_hashes", "encode_chunks_with_ids", "Encoder", "Decoder", "Error",
 ]
 
 
@@ -77,6 +77,13 @@ class EncodedPieces(BaseModel):  # piece.py:50-51
 def piece_hash(data: bytes) -> str:
     """SHA-1 hex digest of a piece (piece.py:54-68)."""
     return hashlib.sha1(data).hexdigest()
+
+
+def piece_hashes(datas: typing.Sequence[bytes]) -> list[str]:
+    """``[piece_hash(d) for d in datas]`` computed by the GPU SHA-1 kernel in one call."""
+    if not datas:
+        return []
+    return [d.hex() for d in get_engine().sha1_host(list(datas))]
 
 
 def piece_length(content_length: int, min_size: int = MIN_PIECE_SIZE, max_size: int = MAX_PIECE_SIZE) -> int:
@@ -144,6 +151,24 @@ def encode_chunks(chunks: typing.Sequence[bytes], first_chunk_idx: int = 0) -> l
     for i, (c, (k, m, B, padlen), par) in enumerate(zip(chunks, shapes, parity)):
         out.append(_build(first_chunk_idx + i, k, m, B, padlen, len(c), _split(c, k, B) + par))
     return out
+
+
+def encode_chunks_with_ids(chunks: typing.Sequence[bytes],
+                           first_chunk_idx: int = 0) -> tuple[list[EncodedChunk], list[list[str]]]:
+    """``encode_chunks`` plus every piece's id (``piece_hash``, the SHA-1 the validator computes
+    right after encoding, validator.py:1081), hashed on the GPU while the pieces are still there."""
+    shapes = []
+    for c in chunks:
+        n = len(c)
+        piece_length(n)
+        shapes.append(chunk_shape(n))
+    if not chunks:
+        return [], []
+    parity, digs = get_engine().encode_host(list(chunks), [(k, m) for (k, m, _, _) in shapes], digests=True)
+    out = []
+    for i, (c, (k, m, B, padlen), par) in enumerate(zip(chunks, shapes, parity)):
+        out.append(_build(first_chunk_idx + i, k, m, B, padlen, len(c), _split(c, k, B) + par))
+    return out, [[d.hex() for d in ds] for ds in digs]
 
 
 def _sharenums(encoded_chunk: EncodedChunk, positional: bool):
