@@ -491,7 +491,10 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
         std::vector<uint64_t> ib((size_t)nchunks);
         for (int64_t i = 0; i < nchunks; ++i)
             ib[i] = chunks[i].n;
-        ranges = slabs_of(ib, env_size("SEC_SLAB_BYTES", (size_t)64 << 20));
+        // SHA-1 is one sequential chain per piece: a slab's hashing takes as long as
+        // one piece, whatever the slab size, so digest mode uses few large slabs
+        ranges = slabs_of(ib, digest ? env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20)
+                                     : env_size("SEC_SLAB_BYTES", (size_t)64 << 20));
     } else {
         ranges.emplace_back(0, nchunks);
     }
@@ -1120,7 +1123,7 @@ int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *di
             std::vector<uint64_t> ib((size_t)nmsgs);
             for (int64_t i = 0; i < nmsgs; ++i)
                 ib[i] = std::min(msgs[i].avail, msgs[i].len);
-            ranges = slabs_of(ib, env_size("SEC_SLAB_BYTES", (size_t)64 << 20));
+            ranges = slabs_of(ib, env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20));
         } else {
             ranges.emplace_back(0, nmsgs);
         }

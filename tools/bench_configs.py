@@ -152,6 +152,39 @@ def device_case(eng, sizes, k, m, erased, reps=20):
             "decode_hbm_GBs": round(dec_bytes / td / 1e9, 1)}
 
 
+def sha1_case(eng, nch=1024, n=1 << 20, k=4, m=6, reps=5):
+    """F1: SHA-1 of all m pieces of every C2 chunk on the device, alone and fused after encode."""
+    import torch
+
+    from storb_amd._lib import MSG_DTYPE
+
+    ed, B = enc_descs_var([n] * nch, k, m)
+    B = int(B[0])
+    src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
+    par = torch.empty(nch * (m - k) * B, dtype=torch.uint8, device="cuda")
+    dig = torch.empty(nch * m * 20, dtype=torch.uint8, device="cuda")
+    msgs = np.zeros(nch * m, dtype=MSG_DTYPE)
+    ci = np.arange(nch, dtype=np.uint64)
+    for j in range(m):
+        msgs["addr"][j::m] = (src.data_ptr() + ci * n + j * B) if j < k else (par.data_ptr() + ci * (m - k) * B + (j - k) * B)
+    msgs["len"] = B
+    msgs["avail"] = B
+    eng.encode_batch(ed, src, par)
+    t_sha = timed(lambda: eng.sha1_batch(msgs, dig), reps)
+    t_enc = timed(lambda: eng.encode_batch(ed, src, par), reps)
+    t_both = timed(lambda: eng.encode_digest_batch(ed, src, par, dig), reps)
+    hsrc = src.cpu().numpy()
+    hpar = np.empty(nch * (m - k) * B, dtype=np.uint8)
+    hdig = np.empty(nch * m * 20, dtype=np.uint8)
+    t_host = timed(lambda: eng.encode_digest_batch(ed, hsrc, hpar, hdig, host=True), 2)
+    hashed = nch * m * B
+    return {"pieces": nch * m, "piece_bytes": B, "sha1_ms": round(t_sha * 1e3, 3),
+            "sha1_GBs": round(hashed / t_sha / 1e9, 1), "encode_ms": round(t_enc * 1e3, 3),
+            "encode_plus_sha1_fused_ms": round(t_both * 1e3, 3),
+            "e2e_host_encode_plus_sha1_gibs": round(nch * n / t_host / GIB, 2),
+            "note": "wall time per call incl. launch + sync; one lane per piece (SHA-1 is sequential per message)"}
+
+
 def host_case(eng, sizes, k, m, erased, reps=3):
     total = int(np.sum(sizes))
     rng = np.random.default_rng(55)
@@ -189,6 +222,12 @@ def main():
     res["c5_mixed_4KiB-4MiB_rs(8,3)_device"] = device_case(eng, sizes, 8, 11, (7, 2, 5))
     res["c5_mixed_4KiB-4MiB_rs(8,3)_e2e_host"] = host_case(eng, sizes, 8, 11, (7, 2, 5))
     res["c2_1024x1MiB_rs(4,2)_e2e_host"] = host_case(eng, [1 << 20] * 1024, 4, 6, (1, 3))
+    res["f1_sha1_pieces_c2_device"] = sha1_case(eng)
+    import hashlib
+    blob = np.random.default_rng(3).integers(0, 256, 1 << 28, dtype=np.uint8).tobytes()
+    t0 = time.perf_counter()
+    hashlib.sha1(blob).digest()
+    res["f1_cpu_hashlib_sha1_1thread_GBs"] = round(len(blob) / (time.perf_counter() - t0) / 1e9, 2)
     print(json.dumps(res, indent=1))
     eng.close()
 
