@@ -127,6 +127,37 @@ __global__ __launch_bounds__(256) void k_rs42_mis(const unsigned char *__restric
     }
 }
 
+__global__ __launch_bounds__(256) void k_copy_nt(const u32x4 *__restrict__ in, u32x4 *__restrict__ out, size_t n)
+{
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(in + i), out + i);
+}
+
+// the decode kernel's pattern for 1024 x 1 MiB RS(4,2) with data {1,3} erased: read data
+// blocks {0,2} (chunk buffer) and parity {4,5} (parity buffer), write the 4 rows of the
+// reassembled chunk (copies + XOR in place of GF), nontemporal
+__global__ __launch_bounds__(256) void k_dec42(const unsigned char *__restrict__ in, const unsigned char *__restrict__ par,
+                                               unsigned char *__restrict__ out)
+{
+    const u32 chunk = blockIdx.x >> 4, t0 = (blockIdx.x & 15) * 16384;
+    const size_t B = 262144;
+    const size_t o = t0 + threadIdx.x * 16;
+    const unsigned char *d = in + (size_t)chunk * 1048576 + o;
+    const unsigned char *p = par + (size_t)chunk * 2 * B + o;
+    unsigned char *w = out + (size_t)chunk * 1048576 + o;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const u32x4 x0 = __builtin_nontemporal_load((const u32x4 *)(d + u * 4096));
+        const u32x4 x2 = __builtin_nontemporal_load((const u32x4 *)(d + 2 * B + u * 4096));
+        const u32x4 x4 = __builtin_nontemporal_load((const u32x4 *)(p + u * 4096));
+        const u32x4 x5 = __builtin_nontemporal_load((const u32x4 *)(p + B + u * 4096));
+        __builtin_nontemporal_store(x0, (u32x4 *)(w + u * 4096));
+        __builtin_nontemporal_store(x2, (u32x4 *)(w + 2 * B + u * 4096));
+        __builtin_nontemporal_store(x0 ^ x4 ^ x5, (u32x4 *)(w + B + u * 4096));
+        __builtin_nontemporal_store(x2 ^ x4 ^ (x5 << 1), (u32x4 *)(w + 3 * B + u * 4096));
+    }
+}
+
 template <class F>
 double time_ms(F launch)
 {
@@ -172,8 +203,12 @@ int main()
         else
             mis[i] = time_ms([&] { hipLaunchKernelGGL(k_rs42_mis<0>, dim3(1024 * 16), dim3(256), 0, 0, a, b, o, so); });
     }
+    const double ms_copy_nt = time_ms([&] { hipLaunchKernelGGL(k_copy_nt, dim3(grid), dim3(256), 0, 0, (u32x4 *)a, (u32x4 *)b, G / 16); });
+    const double ms_dec = time_ms([&] { hipLaunchKernelGGL(k_dec42, dim3(1024 * 16), dim3(256), 0, 0, a, a + G, b); });
     CK(hipDeviceSynchronize());
     const double gb = 1e9;
+    printf("{\"copy_nt_GBs\": %.1f, \"dec42_xor_nt_GBs\": %.1f}\n", 2.0 * G / (ms_copy_nt * 1e-3) / gb,
+           2.0 * G / (ms_dec * 1e-3) / gb);
     printf("{\"rs42_nt_read_off2_GBs\": %.1f, \"read_off4_GBs\": %.1f, \"read_off8_GBs\": %.1f, "
            "\"read_off2_alignbyte_GBs\": %.1f, \"write_off2_GBs\": %.1f, \"write_off4_GBs\": %.1f}\n",
            1.5 * G / (mis[0] * 1e-3) / gb, 1.5 * G / (mis[1] * 1e-3) / gb, 1.5 * G / (mis[2] * 1e-3) / gb,
