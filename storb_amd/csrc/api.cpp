@@ -125,7 +125,7 @@ size_t env_size(const char *name, size_t dflt)
 
 // ---- plan ---------------------------------------------------------------
 struct Group {
-    int rows, U;
+    int rows, U, lanes;
     uint32_t first, count;
 };
 
@@ -192,13 +192,17 @@ int pick_u(uint64_t B, int rows)
     return 1;
 }
 
-using Bins = std::map<std::pair<int, int>, std::vector<sec::Tile>>;
+using Bins = std::map<std::tuple<int, int, int>, std::vector<sec::Tile>>;  // (rows, U, lanes)
+
+uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 
 // Work for one chunk.  `valid` = positions where every block is fully readable and
 // every output row writable (the last data block's length, clamped to [0, B]).
-// Tiles of 4 KiB * U cover [0, valid); a ragged remainder gets U = 1 tiles whose
-// lanes clamp to end at `valid`.  Positions [valid, B) — or all of [0, B) when
-// valid < 16 — become one-thread tail items (at most padlen per normal chunk).
+// Tiles of 256 lanes x 4 KiB * U cover [0, valid); the ragged rest (and small chunks
+// entirely) get U = 1 tiles of up to 1024 lanes sized to what is left, so a 64 KiB
+// RS(10,4) chunk (6550 valid positions) is one 448-lane tile.  Lanes clamp to end at
+// `valid`.  Positions [valid, B) — or all of [0, B) when valid < 16 — become
+// one-thread tail items (at most padlen per normal chunk).
 void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B, int64_t valid,
               int rows_total)
 {
@@ -213,13 +217,15 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
             const int rows = std::min(sec::kMaxRows, rows_total - r0);
             const int U = pick_u(B, rows);
             const uint64_t step = (uint64_t)sec::kStepBytes * U;
-            const uint64_t nfull = v / step;
-            auto &full = bins[{rows, U}];
+            const uint64_t nfull = v > (uint64_t)sec::kLaneBytes * 1024 ? v / step : 0;
+            auto &full = bins[{rows, U, sec::kLanes}];
             for (uint64_t i = 0; i < nfull; ++i)
                 full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
-            auto &rest = bins[{rows, 1}];
-            for (uint64_t t0 = nfull * step; t0 < v; t0 += sec::kStepBytes)
-                rest.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
+            for (uint64_t t0 = nfull * step; t0 < v;) {
+                const uint64_t lanes = std::min<uint64_t>(1024, round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
+                bins[{rows, 1, (int)lanes}].push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
+                t0 += lanes * sec::kLaneBytes;
+            }
         }
     for (uint64_t t = v; t < B; ++t)
         tail.push_back(sec::TailItem{chunk, (uint32_t)t});
@@ -231,7 +237,8 @@ void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile
     for (auto &kv : bins) {
         if (kv.second.empty())
             continue;
-        groups.push_back(Group{kv.first.first, kv.first.second, (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
+        groups.push_back(Group{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first),
+                               (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
         tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
     }
 }
@@ -566,7 +573,7 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
     for (const Group &g : sp.groups) {
-        int e = sec_launch_encode(g.rows, g.U, in, par, dd, dt + g.first, g.count, tabs, s);
+        int e = sec_launch_encode(g.rows, g.U, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
         if (e)
             return hip_fail((hipError_t)e, "sec_encode_kernel");
     }
@@ -737,7 +744,7 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const uint64_t *so = plan.meta.as<uint64_t>(sp.off_soff);
     const uint32_t *sr = plan.meta.as<uint32_t>(sp.off_srow), *mr = plan.meta.as<uint32_t>(sp.off_mrow);
     for (const Group &g : sp.groups) {
-        int e = sec_launch_decode(g.rows, g.U, blocks, out, dd, dt + g.first, g.count, tabs, so, sr, mr, s);
+        int e = sec_launch_decode(g.rows, g.U, g.lanes, blocks, out, dd, dt + g.first, g.count, tabs, so, sr, mr, s);
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_kernel");
     }

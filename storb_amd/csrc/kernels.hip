@@ -163,7 +163,7 @@ __device__ __forceinline__ u32 gf_mul_byte(const u32 *__restrict__ t, u32 x)
 // byte-granular path.  Positions in [valid, B) — at most padlen of them — belong to
 // sec_encode_tail.
 template <int R, int U>
-__global__ __launch_bounds__(256) void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+__global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
                                                          const sec::EncDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
                                                          const u32 *__restrict__ tabs)
@@ -174,10 +174,11 @@ __global__ __launch_bounds__(256) void sec_encode_kernel(const u8 *__restrict__ 
     const u32 t = tl.t0 + threadIdx.x * sec::kLaneBytes;
     if (t >= valid)
         return;
+    const u32 step = blockDim.x * sec::kLaneBytes;  // bytes one u-step of the workgroup covers
     u32 pos[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        pos[u] = min(t + u * sec::kStepBytes, valid - sec::kLaneBytes);
+        pos[u] = min(t + u * step, valid - sec::kLaneBytes);
     const u8 *row = in + d.in_off;
     u8 *dst = par + d.par_off + (u64)tl.r0 * d.par_stride;
     const u32 *tj = tabs + d.tab + tl.r0 * sec::kTabDwords;
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(256) void sec_encode_tail(const u8 *__restrict__ in
 // Positions are < valid = the last output row's length, so every row is writable
 // and every slot (always B bytes) readable; the rest goes to sec_decode_tail.
 template <int R, int U>
-__global__ __launch_bounds__(256) void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+__global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                          const sec::DecDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
                                                          const u32 *__restrict__ tabs,
@@ -268,10 +269,11 @@ __global__ __launch_bounds__(256) void sec_decode_kernel(const u8 *__restrict__ 
     const u32 t = tl.t0 + threadIdx.x * sec::kLaneBytes;
     if (t >= valid)
         return;
+    const u32 step = blockDim.x * sec::kLaneBytes;  // bytes one u-step of the workgroup covers
     u32 pos[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        pos[u] = min(t + u * sec::kStepBytes, valid - sec::kLaneBytes);
+        pos[u] = min(t + u * step, valid - sec::kLaneBytes);
     u8 *dst = out + d.out_off;
     const bool copies = tl.r0 == 0;  // row group 0 also copies the present primaries
     const u32 *tj = tabs + d.tab + tl.r0 * sec::kTabDwords;
@@ -474,52 +476,52 @@ __global__ __launch_bounds__(64) void sec_sha1_kernel(const u8 *__restrict__ bas
 
 template <int R, int U>
 hipError_t launch_enc(const u8 *in, u8 *par, const sec::EncDesc *descs, const sec::Tile *tiles, u32 ntiles,
-                      const u32 *tabs, hipStream_t s)
+                      const u32 *tabs, u32 lanes, hipStream_t s)
 {
-    hipLaunchKernelGGL((sec_encode_kernel<R, U>), dim3(ntiles), dim3(sec::kLanes), 0, s, in, par, descs, tiles, tabs);
+    hipLaunchKernelGGL((sec_encode_kernel<R, U>), dim3(ntiles), dim3(lanes), 0, s, in, par, descs, tiles, tabs);
     return hipGetLastError();
 }
 
 template <int R, int U>
 hipError_t launch_dec(const u8 *blocks, u8 *out, const sec::DecDesc *descs, const sec::Tile *tiles, u32 ntiles,
-                      const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, hipStream_t s)
+                      const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, u32 lanes, hipStream_t s)
 {
-    hipLaunchKernelGGL((sec_decode_kernel<R, U>), dim3(ntiles), dim3(sec::kLanes), 0, s, blocks, out, descs, tiles,
-                       tabs, so, sr, mr);
+    hipLaunchKernelGGL((sec_decode_kernel<R, U>), dim3(ntiles), dim3(lanes), 0, s, blocks, out, descs, tiles, tabs,
+                       so, sr, mr);
     return hipGetLastError();
 }
 
 template <int U>
 hipError_t dispatch_enc(int rows, const u8 *in, u8 *par, const sec::EncDesc *d, const sec::Tile *t, u32 nt,
-                        const u32 *tabs, hipStream_t s)
+                        const u32 *tabs, u32 lanes, hipStream_t s)
 {
     switch (rows) {
-    case 1: return launch_enc<1, U>(in, par, d, t, nt, tabs, s);
-    case 2: return launch_enc<2, U>(in, par, d, t, nt, tabs, s);
-    case 3: return launch_enc<3, U>(in, par, d, t, nt, tabs, s);
-    case 4: return launch_enc<4, U>(in, par, d, t, nt, tabs, s);
-    case 5: return launch_enc<5, U>(in, par, d, t, nt, tabs, s);
-    case 6: return launch_enc<6, U>(in, par, d, t, nt, tabs, s);
-    case 7: return launch_enc<7, U>(in, par, d, t, nt, tabs, s);
-    case 8: return launch_enc<8, U>(in, par, d, t, nt, tabs, s);
+    case 1: return launch_enc<1, U>(in, par, d, t, nt, tabs, lanes, s);
+    case 2: return launch_enc<2, U>(in, par, d, t, nt, tabs, lanes, s);
+    case 3: return launch_enc<3, U>(in, par, d, t, nt, tabs, lanes, s);
+    case 4: return launch_enc<4, U>(in, par, d, t, nt, tabs, lanes, s);
+    case 5: return launch_enc<5, U>(in, par, d, t, nt, tabs, lanes, s);
+    case 6: return launch_enc<6, U>(in, par, d, t, nt, tabs, lanes, s);
+    case 7: return launch_enc<7, U>(in, par, d, t, nt, tabs, lanes, s);
+    case 8: return launch_enc<8, U>(in, par, d, t, nt, tabs, lanes, s);
     default: return hipErrorInvalidValue;
     }
 }
 
 template <int U>
 hipError_t dispatch_dec(int rows, const u8 *b, u8 *o, const sec::DecDesc *d, const sec::Tile *t, u32 nt,
-                        const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, hipStream_t s)
+                        const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, u32 lanes, hipStream_t s)
 {
     switch (rows) {
-    case 0: return launch_dec<0, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 1: return launch_dec<1, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 2: return launch_dec<2, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 3: return launch_dec<3, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 4: return launch_dec<4, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 5: return launch_dec<5, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 6: return launch_dec<6, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 7: return launch_dec<7, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
-    case 8: return launch_dec<8, U>(b, o, d, t, nt, tabs, so, sr, mr, s);
+    case 0: return launch_dec<0, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 1: return launch_dec<1, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 2: return launch_dec<2, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 3: return launch_dec<3, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 4: return launch_dec<4, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 5: return launch_dec<5, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 6: return launch_dec<6, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 7: return launch_dec<7, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 8: return launch_dec<8, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -535,16 +537,18 @@ int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void 
     return hipGetLastError();
 }
 
-int sec_launch_encode(int rows, int U, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
+int sec_launch_encode(int rows, int U, int lanes, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
                       const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, void *stream)
 {
     if (ntiles == 0)
         return hipSuccess;
+    if (lanes < 64 || lanes % 64 || lanes > (U == 1 ? 1024 : sec::kLanes))
+        return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
     switch (U) {
-    case 1: return dispatch_enc<1>(rows, in, par, descs, tiles, ntiles, tabs, s);
-    case 2: return dispatch_enc<2>(rows, in, par, descs, tiles, ntiles, tabs, s);
-    case 4: return dispatch_enc<4>(rows, in, par, descs, tiles, ntiles, tabs, s);
+    case 1: return dispatch_enc<1>(rows, in, par, descs, tiles, ntiles, tabs, (u32)lanes, s);
+    case 2: return dispatch_enc<2>(rows, in, par, descs, tiles, ntiles, tabs, (u32)lanes, s);
+    case 4: return dispatch_enc<4>(rows, in, par, descs, tiles, ntiles, tabs, (u32)lanes, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -559,17 +563,20 @@ int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *
     return hipGetLastError();
 }
 
-int sec_launch_decode(int rows, int U, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
+int sec_launch_decode(int rows, int U, int lanes, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
                       const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, const uint64_t *slot_off,
                       const uint32_t *slot_row, const uint32_t *miss_row, void *stream)
 {
     if (ntiles == 0)
         return hipSuccess;
+    if (lanes < 64 || lanes % 64 || lanes > (U == 1 ? 1024 : sec::kLanes))
+        return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
+    const u32 L = (u32)lanes;
     switch (U) {
-    case 1: return dispatch_dec<1>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
-    case 2: return dispatch_dec<2>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
-    case 4: return dispatch_dec<4>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, s);
+    case 1: return dispatch_dec<1>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
+    case 2: return dispatch_dec<2>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
+    case 4: return dispatch_dec<4>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
     default: return hipErrorInvalidValue;
     }
 }

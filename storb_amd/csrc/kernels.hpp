@@ -1,7 +1,8 @@
 // kernels.hpp — device-side descriptors shared by kernels.hip and api.cpp.
 //
-// Work decomposition.  A "tile" is one workgroup of 256 lanes over a run of
-// 256*16*U consecutive byte positions t of ONE chunk's blocks (U = 1, 2 or 4),
+// Work decomposition.  A "tile" is one workgroup of L lanes over a run of
+// L*16*U consecutive byte positions t of ONE chunk's blocks (U = 1, 2 or 4;
+// L = 256, or for U = 1 tiles any multiple of 64 up to 1024, sized to the chunk),
 // and a group of up to 8 output rows (parity rows for encode, missing data rows
 // for decode).  Each lane owns 16 consecutive positions per u-step, so every
 // wave reads one coalesced 1 KiB run from each of the k input blocks and
@@ -73,11 +74,11 @@ struct MsgDesc {
 // launchers (kernels.hip); all enqueue on `stream` and return hipError_t as int
 extern "C++" {
 int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void *stream);
-int sec_launch_encode(int rows, int U, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
+int sec_launch_encode(int rows, int U, int lanes, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
                       const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
                            uint32_t nitems, const uint32_t *tabs, void *stream);
-int sec_launch_decode(int rows, int U, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
+int sec_launch_decode(int rows, int U, int lanes, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
                       const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
                       const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,
                       void *stream);
