@@ -271,3 +271,65 @@ def test_encode_ragged_tails_many_shapes(engine):
     par = engine.encode_host(chunks, km)
     for c, (k, m), p in zip(chunks, km, par):
         assert p == oracle_parity(c, k, m), (k, m, len(c))
+
+
+def test_host_pipeline_many_slabs(monkeypatch):
+    """SEC_F_HOST batches cut into many 1 MiB slabs (chunks straddling slab limits, a chunk
+    bigger than a slab, two pipeline slots cycling) — encode, decode and SHA-1."""
+    import hashlib
+
+    from storb_amd.engine import Engine
+
+    monkeypatch.setenv("SEC_SLAB_BYTES", str(1 << 20))
+    monkeypatch.setenv("SEC_SLAB_BYTES_DIGEST", str(1 << 20))
+    eng = Engine(0)  # fresh context: plans are built with the small slabs
+    try:
+        rng = random.Random(31)
+        sizes = [rng.randrange(1000, 600000) for _ in range(30)] + [3 << 20, 5, 4096 * 10 + 3]
+        chunks, km = [], []
+        for i, n in enumerate(sizes):
+            k, m = [(4, 6), (10, 14), (2, 3), (8, 11)][i % 4]
+            if -(-n // k) * (k - 1) > n:
+                k, m = 1, 2
+            chunks.append(rng.randbytes(n))
+            km.append((k, m))
+        par, digs = eng.encode_host(chunks, km, digests=True)
+        items = []
+        for c, (k, m), p, d in zip(chunks, km, par, digs):
+            blocks = cfec.easy_encode(c, k, m)
+            assert p == blocks[k:]
+            assert d == [hashlib.sha1(b).digest() for b in blocks]
+            sn = rng.sample(range(m), k)
+            items.append((k, m, [blocks[s] for s in sn], sn, len(blocks[0]) * k - len(c)))
+        assert eng.decode_host(items) == b"".join(chunks)
+        assert eng.sha1_host(chunks) == [hashlib.sha1(c).digest() for c in chunks]
+    finally:
+        eng.close()
+
+
+def test_engines_in_threads():
+    """One context per host thread (the C ABI's threading contract), running concurrently."""
+    import threading
+
+    from storb_amd.engine import get_engine
+
+    errors = []
+
+    def work(seed):
+        try:
+            rng = random.Random(seed)
+            eng = get_engine(0)
+            for _ in range(3):
+                chunks = [rng.randbytes(rng.randrange(4096, 300000)) for _ in range(8)]
+                par = eng.encode_host(chunks, [(4, 6)] * 8)
+                for c, p in zip(chunks, par):
+                    assert p == oracle_parity(c, 4, 6)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=work, args=(s,)) for s in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
