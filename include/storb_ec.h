@@ -55,7 +55,9 @@ enum sec_status {
     SEC_ENODEV = -9,     /* no HIP device / bad device ordinal                         */
     SEC_EHIP = -10,      /* HIP runtime error; sec_last_hip_error() has the text       */
     SEC_ENOMEM = -11,    /* device / pinned allocation failed                          */
-    SEC_ESINGULAR = -12  /* decode matrix singular (cannot happen for valid inputs)    */
+    SEC_ESINGULAR = -12, /* decode matrix singular (cannot happen for valid inputs)    */
+    SEC_EMODULUS = -13,  /* bignum modulus not an odd 2048-bit integer                 */
+    SEC_ENOTAG = -14     /* sec_apdp_tag_batch on a key without sec_bn_key_set_tag     */
 };
 
 /* flags for sec_encode_batch / sec_decode_batch */
@@ -108,7 +110,7 @@ int sec_sync(sec_ctx *ctx);
  * event pair around its encode / decode kernels on the launch stream. */
 int sec_ctx_set_timing(sec_ctx *ctx, int enable);
 /* Waits for recorded pairs, returns the summed milliseconds and launch count of
- * kind 0 = encode, 1 = decode, and clears them. */
+ * kind 0 = encode, 1 = decode, 2 = SHA-1, 3 = bignum (APDP), and clears them. */
 int sec_timing_collect(sec_ctx *ctx, int kind, double *total_ms, int64_t *launches);
 
 /* ---- matrices (host arithmetic, no device needed) ------------------------ */
@@ -160,6 +162,42 @@ int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *di
  * live where the parity does (device, or host with SEC_F_HOST). */
 int sec_encode_digest_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
                             const uint8_t *in, uint8_t *parity, uint8_t *digests, unsigned flags);
+
+/* ---- APDP proofs of data possession: 2048-bit modular arithmetic ----------
+ * Replaces the gmpy2 calls of storb's ChallengeSystem
+ * (/root/reference/storb/challenge/__init__.py:304-350 generate_tag,
+ * :401-463 generate_proof, :465-528 verify_proof; gmpy2 2.2.1,
+ * /root/reference/uv.lock).  Integers cross the boundary as 256-byte big-endian
+ * strings (int.to_bytes(256, "big")).  The modulus is an RSA-2048 modulus:
+ * odd, exactly 2048 bits (DEFAULT_RSA_KEY_SIZE, storb/constants.py:26);
+ * anything else is SEC_EMODULUS.  Results are fully reduced (< n).
+ * Device mode: every data pointer is device memory; SEC_F_HOST: host memory. */
+typedef struct sec_bn_key sec_bn_key;
+
+int sec_bn_key_create(sec_ctx *ctx, const uint8_t n_be[256], sec_bn_key **out);
+void sec_bn_key_destroy(sec_bn_key *key);
+/* generate_tag's per-key constants: g, fdh = full_domain_hash(prf(prf_key, 0))
+ * (each taken mod n) and the private exponent d (< 2^2048).  Host memory. */
+int sec_bn_key_set_tag(sec_ctx *ctx, sec_bn_key *key, const uint8_t g_be[256],
+                       const uint8_t fdh_be[256], const uint8_t d_be[256]);
+
+/* out[i] = int.from_bytes(message i, "big") mod n (256 B each); messages as in
+ * sec_sha1_batch (bytes past `avail` read as zero).  block_int of
+ * generate_tag / generate_proof. */
+int sec_bn_reduce_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs, int64_t nmsgs,
+                        uint8_t *out, unsigned flags);
+/* out[i] = bases[i] ^ exps[i] mod n.  bases: 256 B each (any value < 2^2048);
+ * exps: exp_bytes each, big-endian (1 <= exp_bytes <= 4096). */
+int sec_bn_modexp_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *bases,
+                        const uint8_t *exps, uint32_t exp_bytes, int64_t count, uint8_t *out,
+                        unsigned flags);
+/* out[i] = a[i] * b[i] mod n (256 B each, any values < 2^2048). */
+int sec_bn_mulmod_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *a, const uint8_t *b,
+                        int64_t count, uint8_t *out, unsigned flags);
+/* APDP tags, fused per message: X = message mod n; tag = (fdh * g^X)^d mod n
+ * (generate_tag's tag_value).  Needs sec_bn_key_set_tag; 256 B per tag. */
+int sec_apdp_tag_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs, int64_t nmsgs,
+                       uint8_t *tags, unsigned flags);
 
 /* ---- memory helpers for hosts without a device allocator ----------------- */
 int sec_malloc(sec_ctx *ctx, size_t bytes, void **dptr);

@@ -9,3 +9,8 @@ MAX_UPLOAD_SIZE = 1 * 1024 * 1024 * 1024 * 1024  # 1 TiB (constants.py:16)
 # defined but unused by the reference (constants.py:20-21); kept for import parity
 EC_DATA_SIZE = 4
 EC_PARITY_SIZE = 2
+
+# APDP challenge system (constants.py:28-32)
+DEFAULT_RSA_KEY_SIZE = 2048
+G_CANDIDATE_RETRY = 1000  # retries for the generator g
+S_CANDIDATE_RETRY = 1000  # retries for the challenge secret s

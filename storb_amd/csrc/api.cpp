@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "copy_pool.hpp"
+#include "bignum.hpp"
 #include "gf_host.hpp"
 #include "kernels.hpp"
 #include "storb_ec.h"
@@ -281,12 +282,13 @@ struct sec_ctx {
     hipStream_t own = nullptr;
     hipStream_t ext = nullptr;
     bool timing = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[2];
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[4];
     std::vector<hipEvent_t> ev_pool;
     PinBuf pin;  // metadata image staging
     hipEvent_t pin_ev = nullptr, meta_ev = nullptr;
     TableCache enc_tabs, dec_tabs;
-    Plan enc_plan, dec_plan, sha_plan;
+    Plan enc_plan, dec_plan, sha_plan, bn_plan;
+    DevBuf bn_scratch;  // host-mode staging of sec_bn_modexp / mulmod operands
     Slot slots[kSlots];
     std::unique_ptr<sec::CopyPool> pool;
 
@@ -791,6 +793,145 @@ int run_pipeline(sec_ctx *ctx, Plan &plan, Gather gather, Scatter scatter, Launc
     return SEC_OK;
 }
 
+// ---- message batches (SHA-1 piece ids, bignum reduce, APDP tags) ------------
+// `launch(base0, descs, n, out, stream)` runs the kernel over n messages whose
+// descriptors are device-resident; out_per = output bytes per message.  Device
+// mode: one launch over caller addresses.  SEC_F_HOST: messages are staged
+// densely through pinned slabs (`slab` bytes) and the outputs copied back.
+template <class Launch>
+int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint8_t *out, size_t out_per,
+              unsigned flags, size_t slab, int kind, const char *what, Launch launch_kernel)
+{
+    if (!ctx || nmsgs < 0 || (nmsgs > 0 && (!msgs || !out)) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC)) ||
+        nmsgs >= (int64_t)UINT32_MAX)
+        return SEC_EINVAL;
+    if (nmsgs == 0)
+        return SEC_OK;
+    const bool host = flags & SEC_F_HOST;
+    RC(set_dev(ctx));
+    std::vector<uint8_t> key;
+    if (host) {  // dense staging: only lengths matter
+        key.resize((size_t)nmsgs * 16);
+        for (int64_t i = 0; i < nmsgs; ++i) {
+            const uint64_t av = std::min(msgs[i].avail, msgs[i].len);
+            memcpy(key.data() + i * 16, &msgs[i].len, 8);
+            memcpy(key.data() + i * 16 + 8, &av, 8);
+        }
+    } else {
+        key.assign((const uint8_t *)msgs, (const uint8_t *)(msgs + nmsgs));
+    }
+    key.insert(key.end(), (const uint8_t *)&flags, (const uint8_t *)&flags + sizeof(unsigned));
+    key.insert(key.end(), (const uint8_t *)&slab, (const uint8_t *)&slab + sizeof(size_t));
+    if (!(plan.valid && plan.key == key)) {
+        plan.valid = false;
+        std::vector<std::pair<int64_t, int64_t>> ranges;
+        if (host) {
+            std::vector<uint64_t> ib((size_t)nmsgs);
+            for (int64_t i = 0; i < nmsgs; ++i)
+                ib[i] = std::min(msgs[i].avail, msgs[i].len);
+            ranges = slabs_of(ib, slab);
+        } else {
+            ranges.emplace_back(0, nmsgs);
+        }
+        Image img;
+        plan.subs.clear();
+        for (auto [c0, c1] : ranges) {
+            SubPlan sp;
+            sp.c0 = c0;
+            sp.c1 = c1;
+            sp.dig_first = (uint64_t)c0;
+            std::vector<sec::MsgDesc> md;
+            for (int64_t i = c0; i < c1; ++i) {
+                const uint64_t av = std::min(msgs[i].avail, msgs[i].len);
+                md.push_back(sec::MsgDesc{host ? sp.in_bytes : msgs[i].addr, msgs[i].len, av, 0, 0});
+                sp.in_bytes += av;
+            }
+            sp.nmsgs = (uint32_t)md.size();
+            sp.out_bytes = (uint64_t)md.size() * out_per;
+            sp.off_msgs = img.put(md.data(), md.size() * sizeof(sec::MsgDesc));
+            plan.subs.push_back(std::move(sp));
+        }
+        std::vector<PendingExpand> none;
+        RC(upload_plan(ctx, plan, img, ctx->enc_tabs, none));
+        plan.key.swap(key);
+        plan.valid = true;
+    }
+    if (!host) {
+        const SubPlan &sp = plan.subs[0];
+        hipEvent_t t0;
+        RC(timing_begin(ctx, &t0, ctx->stream()));
+        int e = launch_kernel((const uint8_t *)nullptr, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, out,
+                              ctx->stream());
+        if (e)
+            return hip_fail((hipError_t)e, what);
+        RC(timing_end(ctx, t0, kind, ctx->stream()));
+        if (!(flags & SEC_F_ASYNC))
+            CK(hipStreamSynchronize(ctx->stream()));
+        return SEC_OK;
+    }
+    auto gather = [&](const SubPlan &sp, char *stage, std::vector<sec::CopyJob> &jobs) {
+        uint64_t o = 0;
+        for (int64_t i = sp.c0; i < sp.c1; ++i) {
+            const uint64_t av = std::min(msgs[i].avail, msgs[i].len);
+            jobs.push_back(sec::CopyJob{stage + o, (const void *)(uintptr_t)msgs[i].addr, av});
+            o += av;
+        }
+    };
+    auto scatter = [&](const SubPlan &sp, char *stage, std::vector<sec::CopyJob> &jobs) {
+        jobs.push_back(sec::CopyJob{out + sp.dig_first * out_per, stage, (size_t)sp.nmsgs * out_per});
+    };
+    auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
+        hipEvent_t t0;
+        RC(timing_begin(ctx, &t0, s));
+        int e = launch_kernel(din, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, dout, s);
+        if (e)
+            return hip_fail((hipError_t)e, what);
+        return timing_end(ctx, t0, kind, s);
+    };
+    return run_pipeline(ctx, plan, gather, scatter, launch);
+}
+
+// Runs `launch_kernel(dev_inputs[], dev_out, stream)` over `count` items whose inputs
+// are dense arrays (sizes in `in_bytes`) and whose output is count * out_per bytes.
+// SEC_F_HOST: inputs are uploaded into ctx->bn_scratch and the output copied back.
+template <class Launch>
+int dense_batch(sec_ctx *ctx, const std::vector<std::pair<const uint8_t *, size_t>> &ins, uint8_t *out,
+                size_t out_bytes, unsigned flags, const char *what, Launch launch_kernel)
+{
+    RC(set_dev(ctx));
+    const bool host = flags & SEC_F_HOST;
+    hipStream_t s = ctx->stream();
+    std::vector<const uint8_t *> dev;
+    uint8_t *dout = out;
+    if (host) {
+        size_t tot = align_up(out_bytes, 256);
+        for (auto &pr : ins)
+            tot += align_up(pr.second, 256);
+        RC(ctx->bn_scratch.ensure(tot));
+        size_t o = 0;
+        for (auto &pr : ins) {
+            CK(hipMemcpyAsync(ctx->bn_scratch.as<uint8_t>(o), pr.first, pr.second, hipMemcpyHostToDevice, s));
+            dev.push_back(ctx->bn_scratch.as<uint8_t>(o));
+            o += align_up(pr.second, 256);
+        }
+        dout = ctx->bn_scratch.as<uint8_t>(o);
+    } else {
+        for (auto &pr : ins)
+            dev.push_back(pr.first);
+    }
+    hipEvent_t t0;
+    RC(timing_begin(ctx, &t0, s));
+    int e = launch_kernel(dev, dout, s);
+    if (e)
+        return hip_fail((hipError_t)e, what);
+    RC(timing_end(ctx, t0, 3, s));
+    if (host)
+        CK(hipMemcpyAsync(out, dout, out_bytes, hipMemcpyDeviceToHost, s));
+    if (host || !(flags & SEC_F_ASYNC))
+        CK(hipStreamSynchronize(s));
+    return SEC_OK;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -814,6 +955,8 @@ const char *sec_strerror(int s)
     case SEC_EHIP: return "HIP runtime error";
     case SEC_ENOMEM: return "out of device or pinned memory";
     case SEC_ESINGULAR: return "decode matrix is singular";
+    case SEC_EMODULUS: return "modulus must be an odd 2048-bit integer";
+    case SEC_ENOTAG: return "key has no APDP tag constants (sec_bn_key_set_tag)";
     default: return "unknown error";
     }
 }
@@ -898,6 +1041,8 @@ void sec_ctx_destroy(sec_ctx *ctx)
     ctx->enc_plan.meta.release();
     ctx->dec_plan.meta.release();
     ctx->sha_plan.meta.release();
+    ctx->bn_plan.meta.release();
+    ctx->bn_scratch.release();
     if (ctx->own)
         (void)hipStreamDestroy(ctx->own);
     delete ctx;
@@ -934,7 +1079,7 @@ int sec_ctx_set_timing(sec_ctx *ctx, int enable)
 
 int sec_timing_collect(sec_ctx *ctx, int kind, double *total_ms, int64_t *launches)
 {
-    if (!ctx || kind < 0 || kind > 1 || !total_ms || !launches)
+    if (!ctx || kind < 0 || kind > 3 || !total_ms || !launches)
         return SEC_EINVAL;
     RC(set_dev(ctx));
     double tot = 0;
@@ -1103,86 +1248,144 @@ int sec_encode_digest_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t n
 
 int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *digests, unsigned flags)
 {
-    if (!ctx || nmsgs < 0 || (nmsgs > 0 && (!msgs || !digests)) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC)) ||
-        nmsgs >= (int64_t)UINT32_MAX)
+    if (!ctx)
         return SEC_EINVAL;
-    if (nmsgs == 0)
-        return SEC_OK;
-    const bool host = flags & SEC_F_HOST;
+    return msg_batch(ctx, ctx->sha_plan, msgs, nmsgs, digests, 20, flags,
+                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 2, "sec_sha1_kernel",
+                     [](const uint8_t *base0, const sec::MsgDesc *md, uint32_t n, uint8_t *o, hipStream_t s) {
+                         return sec_launch_sha1(base0, nullptr, md, n, o, s);
+                     });
+}
+
+// ---------------------------------------------------------------------------
+// APDP bignum (bignum.hip).  The key lives on the device of the context that
+// created it: a TagKey whose first member is the BnKey.
+}  // extern "C"
+
+struct sec_bn_key {
+    int device = 0;
+    DevBuf dk;
+    bool has_tag = false;
+};
+
+extern "C" {
+
+int sec_bn_key_create(sec_ctx *ctx, const uint8_t *n_be, sec_bn_key **out)
+{
+    if (!ctx || !n_be || !out)
+        return SEC_EINVAL;
+    *out = nullptr;
+    if (!(n_be[0] & 0x80) || !(n_be[255] & 1))
+        return SEC_EMODULUS;
     RC(set_dev(ctx));
-    Plan &plan = ctx->sha_plan;
-    std::vector<uint8_t> key;
-    if (host) {  // dense staging: only lengths matter
-        key.resize((size_t)nmsgs * 16);
-        for (int64_t i = 0; i < nmsgs; ++i) {
-            const uint64_t av = std::min(msgs[i].avail, msgs[i].len);
-            memcpy(key.data() + i * 16, &msgs[i].len, 8);
-            memcpy(key.data() + i * 16 + 8, &av, 8);
-        }
-    } else {
-        key.assign((const uint8_t *)msgs, (const uint8_t *)(msgs + nmsgs));
-    }
-    key.insert(key.end(), (const uint8_t *)&flags, (const uint8_t *)&flags + sizeof(unsigned));
-    if (!(plan.valid && plan.key == key)) {
-        plan.valid = false;
-        std::vector<std::pair<int64_t, int64_t>> ranges;
-        if (host) {
-            std::vector<uint64_t> ib((size_t)nmsgs);
-            for (int64_t i = 0; i < nmsgs; ++i)
-                ib[i] = std::min(msgs[i].avail, msgs[i].len);
-            ranges = slabs_of(ib, env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20));
-        } else {
-            ranges.emplace_back(0, nmsgs);
-        }
-        Image img;
-        plan.subs.clear();
-        for (auto [c0, c1] : ranges) {
-            SubPlan sp;
-            sp.c0 = c0;
-            sp.c1 = c1;
-            sp.dig_first = (uint64_t)c0;
-            std::vector<sec::MsgDesc> md;
-            for (int64_t i = c0; i < c1; ++i) {
-                const uint64_t av = std::min(msgs[i].avail, msgs[i].len);
-                md.push_back(sec::MsgDesc{host ? sp.in_bytes : msgs[i].addr, msgs[i].len, av, 0, 0});
-                sp.in_bytes += av;
-            }
-            sp.nmsgs = (uint32_t)md.size();
-            sp.out_bytes = (uint64_t)md.size() * 20;
-            sp.off_msgs = img.put(md.data(), md.size() * sizeof(sec::MsgDesc));
-            plan.subs.push_back(std::move(sp));
-        }
-        std::vector<PendingExpand> none;
-        RC(upload_plan(ctx, plan, img, ctx->enc_tabs, none));
-        plan.key.swap(key);
-        plan.valid = true;
-    }
-    if (!host) {
-        const SubPlan &sp = plan.subs[0];
-        int e = sec_launch_sha1(nullptr, nullptr, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, digests,
-                                ctx->stream());
-        if (e)
-            return hip_fail((hipError_t)e, "sec_sha1_kernel");
-        if (!(flags & SEC_F_ASYNC))
-            CK(hipStreamSynchronize(ctx->stream()));
+    const uint32_t n0 = (uint32_t)n_be[252] << 24 | (uint32_t)n_be[253] << 16 | (uint32_t)n_be[254] << 8 | n_be[255];
+    uint32_t x = n0;  // n0 * n0 == 1 mod 8: 3 correct bits, doubling per Newton step
+    for (int i = 0; i < 4; ++i)
+        x *= 2u - n0 * x;
+    std::unique_ptr<sec_bn_key> key(new sec_bn_key());
+    key->device = ctx->device;
+    RC(key->dk.ensure(sizeof(sec::TagKey) + 256));
+    uint8_t *nd = key->dk.as<uint8_t>(sizeof(sec::TagKey));
+    hipStream_t s = ctx->stream();
+    CK(hipMemcpyAsync(nd, n_be, 256, hipMemcpyHostToDevice, s));
+    int e = sec_launch_bn_setup(nd, 0u - x, key->dk.as<sec::BnKey>(), s);
+    if (e)
+        return hip_fail((hipError_t)e, "sec_bn_setup_kernel");
+    CK(hipStreamSynchronize(s));
+    *out = key.release();
+    return SEC_OK;
+}
+
+void sec_bn_key_destroy(sec_bn_key *key)
+{
+    if (!key)
+        return;
+    (void)hipSetDevice(key->device);
+    key->dk.release();
+    delete key;
+}
+
+int sec_bn_key_set_tag(sec_ctx *ctx, sec_bn_key *key, const uint8_t *g_be, const uint8_t *fdh_be,
+                       const uint8_t *d_be)
+{
+    if (!ctx || !key || !g_be || !fdh_be || !d_be || key->device != ctx->device)
+        return SEC_EINVAL;
+    RC(set_dev(ctx));
+    uint8_t host[768];
+    memcpy(host, g_be, 256);
+    memcpy(host + 256, fdh_be, 256);
+    memcpy(host + 512, d_be, 256);
+    RC(key->dk.ensure(sizeof(sec::TagKey) + 768));
+    uint8_t *p = key->dk.as<uint8_t>(sizeof(sec::TagKey));
+    hipStream_t s = ctx->stream();
+    CK(hipMemcpyAsync(p, host, 768, hipMemcpyHostToDevice, s));
+    int e = sec_launch_tag_setup(p, p + 256, p + 512, key->dk.as<sec::TagKey>(), s);
+    if (e)
+        return hip_fail((hipError_t)e, "sec_tag_setup_kernel");
+    CK(hipStreamSynchronize(s));
+    key->has_tag = true;
+    return SEC_OK;
+}
+
+int sec_bn_reduce_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs, int64_t nmsgs, uint8_t *out,
+                        unsigned flags)
+{
+    if (!ctx || !key || key->device != ctx->device)
+        return SEC_EINVAL;
+    const sec::BnKey *dk = key->dk.as<sec::BnKey>();
+    return msg_batch(ctx, ctx->bn_plan, msgs, nmsgs, out, 256, flags,
+                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 3, "sec_bn_reduce_kernel",
+                     [dk](const uint8_t *base0, const sec::MsgDesc *md, uint32_t n, uint8_t *o, hipStream_t s) {
+                         return sec_launch_bn_reduce(dk, base0, md, n, o, s);
+                     });
+}
+
+int sec_apdp_tag_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs, int64_t nmsgs, uint8_t *tags,
+                       unsigned flags)
+{
+    if (!ctx || !key || key->device != ctx->device)
+        return SEC_EINVAL;
+    if (!key->has_tag)
+        return SEC_ENOTAG;
+    const sec::TagKey *tk = key->dk.as<sec::TagKey>();
+    return msg_batch(ctx, ctx->bn_plan, msgs, nmsgs, tags, 256, flags,
+                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 3, "sec_apdp_tag_kernel",
+                     [tk](const uint8_t *base0, const sec::MsgDesc *md, uint32_t n, uint8_t *o, hipStream_t s) {
+                         return sec_launch_apdp_tag(tk, base0, md, n, o, s);
+                     });
+}
+
+int sec_bn_modexp_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *bases, const uint8_t *exps,
+                        uint32_t exp_bytes, int64_t count, uint8_t *out, unsigned flags)
+{
+    if (!ctx || !key || key->device != ctx->device || count < 0 || count >= (int64_t)INT32_MAX ||
+        (count > 0 && (!bases || !exps || !out)) || exp_bytes < 1 || exp_bytes > 4096 ||
+        (flags & ~(SEC_F_HOST | SEC_F_ASYNC)))
+        return SEC_EINVAL;
+    if (count == 0)
         return SEC_OK;
-    }
-    auto gather = [&](const SubPlan &sp, char *stage, std::vector<sec::CopyJob> &jobs) {
-        uint64_t o = 0;
-        for (int64_t i = sp.c0; i < sp.c1; ++i) {
-            const uint64_t av = std::min(msgs[i].avail, msgs[i].len);
-            jobs.push_back(sec::CopyJob{stage + o, (const void *)(uintptr_t)msgs[i].addr, av});
-            o += av;
-        }
-    };
-    auto scatter = [&](const SubPlan &sp, char *stage, std::vector<sec::CopyJob> &jobs) {
-        jobs.push_back(sec::CopyJob{digests + sp.dig_first * 20, stage, (size_t)sp.nmsgs * 20});
-    };
-    auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
-        int e = sec_launch_sha1(din, nullptr, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, dout, s);
-        return e ? hip_fail((hipError_t)e, "sec_sha1_kernel") : SEC_OK;
-    };
-    return run_pipeline(ctx, plan, gather, scatter, launch);
+    const sec::BnKey *dk = key->dk.as<sec::BnKey>();
+    return dense_batch(ctx, {{bases, (size_t)count * 256}, {exps, (size_t)count * exp_bytes}}, out,
+                       (size_t)count * 256, flags, "sec_bn_modexp_kernel",
+                       [&](const std::vector<const uint8_t *> &in, uint8_t *o, hipStream_t s) {
+                           return sec_launch_bn_modexp(dk, in[0], in[1], exp_bytes, (uint32_t)count, o, s);
+                       });
+}
+
+int sec_bn_mulmod_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *a, const uint8_t *b, int64_t count,
+                        uint8_t *out, unsigned flags)
+{
+    if (!ctx || !key || key->device != ctx->device || count < 0 || count >= (int64_t)INT32_MAX ||
+        (count > 0 && (!a || !b || !out)) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC)))
+        return SEC_EINVAL;
+    if (count == 0)
+        return SEC_OK;
+    const sec::BnKey *dk = key->dk.as<sec::BnKey>();
+    return dense_batch(ctx, {{a, (size_t)count * 256}, {b, (size_t)count * 256}}, out, (size_t)count * 256, flags,
+                       "sec_bn_mulmod_kernel",
+                       [&](const std::vector<const uint8_t *> &in, uint8_t *o, hipStream_t s) {
+                           return sec_launch_bn_mulmod(dk, in[0], in[1], (uint32_t)count, o, s);
+                       });
 }
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,353 @@
+// bignum.hip — 2048-bit modular arithmetic on CDNA4 for storb's APDP proofs of data
+// possession (F4: /root/reference/storb/challenge/__init__.py:304-350 generate_tag,
+// :401-463 generate_proof; DEFAULT_RSA_KEY_SIZE = 2048 at storb/constants.py:26).
+//
+// One wave = one 2048-bit integer: lane j holds 32-bit limb j (little-endian limbs), so a
+// 64-lane wavefront is exactly one RSA-2048 residue.  Montgomery multiplication (R =
+// 2^2048) runs as 64 row steps: the row's limb a_i is broadcast with v_readlane, every
+// lane does two 32x32->64 multiply-adds (a_i*b_j and m*n_j), and the running sum moves
+// down one lane per step (ds_bpermute).  Carries stay in a redundant per-lane word and
+// are resolved once per product with two wave ballots (generate / propagate masks;
+// carry-lookahead done as 64-bit integer arithmetic on the masks).  The work is
+// integer-multiply / issue bound, not memory bound: ~1k VALU per product and ~6k
+// products per APDP tag.
+#include <hip/hip_runtime.h>
+
+#include "bignum.hpp"
+
+using u8 = uint8_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+
+namespace {
+
+__device__ __forceinline__ u32 lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+__device__ __forceinline__ u32 bcast(u32 x, u32 i) { return __builtin_amdgcn_readlane(x, i); }
+
+__device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
+
+// lane j <- x[j+1]; lane 63 <- 0
+__device__ __forceinline__ u32 down1(u32 x, u32 l)
+{
+    const u32 y = (u32)__builtin_amdgcn_ds_bpermute((int)(((l + 1) & 63) << 2), (int)x);
+    return l == 63 ? 0u : y;
+}
+
+// lane j <- x[j-1]; lane 0 <- 0
+__device__ __forceinline__ u32 up1(u32 x, u32 l)
+{
+    const u32 y = (u32)__builtin_amdgcn_ds_bpermute((int)(((l + 63) & 63) << 2), (int)x);
+    return l == 0 ? 0u : y;
+}
+
+// Carry-in mask of a multi-limb add: limb j generates (G) or propagates (P) a carry
+// (never both).  *out = carry out of limb 63.
+__device__ __forceinline__ u64 carry_in(u64 G, u64 P, bool *out)
+{
+    const u64 X = G << 1;
+    const u64 S = X + P;
+    *out = (S < X) || (G >> 63);
+    return S ^ P;
+}
+
+// limb-vector + one carry bit per limb position already folded into `u` (64-bit sums
+// whose high words are 0 or 1): normalise to 32-bit limbs, return the carry out.
+__device__ __forceinline__ u32 resolve(u64 u, u32 l, u32 *t)
+{
+    u32 v = (u32)u;
+    bool co;
+    const u64 C = carry_in(ballot((u >> 32) != 0), ballot(v == 0xFFFFFFFFu), &co);
+    *t = v + (u32)((C >> l) & 1u);
+    return co ? 1u : 0u;
+}
+
+// a >= n, where `top` is a's limb 64
+__device__ __forceinline__ bool geq(u32 a, u32 n, u32 top)
+{
+    if (top)
+        return true;
+    const u64 ne = ballot(a != n);
+    if (!ne)
+        return true;
+    const u32 h = 63 - (u32)__builtin_clzll(ne);
+    return bcast(a, h) > bcast(n, h);
+}
+
+// (a - n) mod 2^2048
+__device__ __forceinline__ u32 sub_n(u32 a, u32 n, u32 l)
+{
+    bool dummy;
+    const u64 B = carry_in(ballot(a < n), ballot(a == n), &dummy);
+    return a - n - (u32)((B >> l) & 1u);
+}
+
+// Montgomery product a*b*R^-1 mod n for a, b < n.
+__device__ u32 mont_mul(u32 a, u32 b, u32 n, u32 n0inv, u32 l)
+{
+    u32 t = 0, c = 0;  // value = sum t_j 2^32j + sum c_j 2^32(j+1), c_j <= 3
+#pragma unroll 8
+    for (u32 i = 0; i < 64; ++i) {
+        const u32 ai = bcast(a, i);
+        const u64 p1 = (u64)ai * b + t;
+        const u32 m = bcast((u32)p1, 0) * n0inv;
+        const u64 p2 = (u64)m * n + (u32)p1;  // limb 0 of p2 is 0 mod 2^32
+        const u64 s = (u64)down1((u32)p2, l) + (p1 >> 32) + (p2 >> 32) + c;
+        t = (u32)s;
+        c = (u32)(s >> 32);
+    }
+    // resolve the redundant carries: limb j += c_{j-1}; c_63 is limb 64
+    u32 top = bcast(c, 63);
+    top += resolve((u64)t + up1(c, l), l, &t);
+    if (geq(t, n, top))  // the product is < 2n
+        t = sub_n(t, n, l);
+    return t;
+}
+
+// (a + x) mod n for a < n and x < 2^2048 (so a + x < 3n: n has its top bit set)
+__device__ u32 add_mod(u32 a, u32 x, u32 n, u32 l)
+{
+    u32 t;
+    u32 top = resolve((u64)a + x, l, &t);
+    for (int k = 0; k < 2; ++k)
+        if (geq(t, n, top)) {
+            t = sub_n(t, n, l);  // exact mod 2^2048 even when top == 1
+            top = 0;
+        }
+    return t;
+}
+
+// 4-bit fixed-window exponentiation in Montgomery form; the exponent's nibbles come from
+// `nib(i)` for i = nnib-1 .. 0 (most significant first).  tab: 16 x 64 u32 of LDS.
+template <class Nib>
+__device__ u32 mont_pow(u32 base_m, u32 one_m, u32 n, u32 n0inv, u32 l, u32 nnib, Nib nib, u32 *tab)
+{
+    tab[l] = one_m;
+    tab[64 + l] = base_m;
+    u32 x = base_m;
+    for (u32 w = 2; w < 16; ++w) {
+        x = mont_mul(x, base_m, n, n0inv, l);
+        tab[w * 64 + l] = x;
+    }
+    u32 r = one_m;
+    bool started = false;
+    for (u32 i = nnib; i-- > 0;) {
+        const u32 v = nib(i);
+        if (started)
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                r = mont_mul(r, r, n, n0inv, l);
+        if (v) {
+            r = started ? mont_mul(r, tab[v * 64 + l], n, n0inv, l) : tab[v * 64 + l];
+            started = true;
+        }
+    }
+    return r;
+}
+
+// limb j of a 256-byte big-endian integer
+__device__ __forceinline__ u32 load_be_limb(const u8 *be, u32 l)
+{
+    const u8 *p = be + 252 - 4 * l;
+    return (u32)p[0] << 24 | (u32)p[1] << 16 | (u32)p[2] << 8 | (u32)p[3];
+}
+
+__device__ __forceinline__ void store_be_limb(u8 *be, u32 l, u32 v)
+{
+    u8 *p = be + 252 - 4 * l;
+    p[0] = (u8)(v >> 24);
+    p[1] = (u8)(v >> 16);
+    p[2] = (u8)(v >> 8);
+    p[3] = (u8)v;
+}
+
+// limb j of the big-endian integer formed by bytes [start, start+len) of a message
+// whose bytes at or beyond `avail` read as zero (len <= 256)
+__device__ __forceinline__ u32 chunk_limb(const u8 *p, uint64_t start, uint32_t len, uint64_t avail, u32 l)
+{
+    const int64_t end = (int64_t)start + len - 4 * (int64_t)l;  // exclusive end of this limb's bytes
+    u32 v = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int64_t pos = end - 4 + b;
+        const u32 byte = (pos >= (int64_t)start && (uint64_t)pos < avail) ? (u32)p[pos] : 0u;
+        v = (v << 8) | byte;
+    }
+    return v;
+}
+
+// int.from_bytes(msg, "big") mod n: Horner over 256-byte chunks from the most
+// significant, r <- r * 2^2048 + chunk  (r * 2^2048 = mont_mul(r, R^2)).
+__device__ u32 reduce_msg(const u8 *p, uint64_t len, uint64_t avail, u32 n, u32 r2, u32 n0inv, u32 l)
+{
+    u32 r = 0;
+    if (len == 0)
+        return r;
+    const uint64_t nch = (len + 255) / 256;
+    const uint32_t first = (uint32_t)(len - 256 * (nch - 1));
+    uint64_t off = 0;
+    for (uint64_t c = 0; c < nch; ++c) {
+        const uint32_t clen = c == 0 ? first : 256u;
+        const u32 x = chunk_limb(p, off, clen, avail, l);
+        if (c > 0)
+            r = mont_mul(r, r2, n, n0inv, l);
+        r = add_mod(r, x, n, l);
+        off += clen;
+    }
+    return r;
+}
+
+// ---- kernels (one 64-lane workgroup = one wave = one integer) ---------------------
+
+// BnKey from a big-endian modulus: R mod n = 2^2048 - n (n > 2^2047), R^2 mod n by
+// 2048 modular doublings.
+__global__ __launch_bounds__(64) void sec_bn_setup_kernel(const u8 *__restrict__ n_be, u32 n0inv, sec::BnKey *key)
+{
+    const u32 l = lane_id();
+    const u32 n = load_be_limb(n_be, l);
+    u32 one;
+    {  // 0 - n mod 2^2048
+        bool dummy;
+        const u64 B = carry_in(ballot(0u < n), ballot(n == 0u), &dummy);
+        one = 0u - n - (u32)((B >> l) & 1u);
+    }
+    u32 r2 = one;
+    for (int i = 0; i < 2048; ++i)
+        r2 = add_mod(r2, r2, n, l);
+    key->n[l] = n;
+    key->one[l] = one;
+    key->r2[l] = r2;
+    if (l == 0)
+        key->n0inv = n0inv;
+}
+
+__global__ __launch_bounds__(64) void sec_tag_setup_kernel(const u8 *__restrict__ g_be, const u8 *__restrict__ fdh_be,
+                                                           const u8 *__restrict__ d_be, sec::TagKey *tk)
+{
+    const u32 l = lane_id();
+    const u32 n = tk->k.n[l], r2 = tk->k.r2[l], n0inv = tk->k.n0inv;
+    tk->g_m[l] = mont_mul(load_be_limb(g_be, l), r2, n, n0inv, l);
+    tk->fdh_m[l] = mont_mul(load_be_limb(fdh_be, l), r2, n, n0inv, l);
+    tk->d[l] = load_be_limb(d_be, l);
+}
+
+__global__ __launch_bounds__(64) void sec_bn_reduce_kernel(const sec::BnKey *__restrict__ key, const u8 *base0,
+                                                           const sec::MsgDesc *__restrict__ msgs, u32 nmsgs, u8 *out)
+{
+    const u32 i = blockIdx.x;
+    if (i >= nmsgs)
+        return;
+    const u32 l = lane_id();
+    const sec::MsgDesc m = msgs[i];
+    const u32 x = reduce_msg(base0 + m.off, m.len, m.avail, key->n[l], key->r2[l], key->n0inv, l);
+    store_be_limb(out + (u64)i * 256, l, x);
+}
+
+// out_i = bases_i ^ exps_i mod n; bases < n (256 B big-endian), exps fixed-width big-endian
+__global__ __launch_bounds__(64) void sec_bn_modexp_kernel(const sec::BnKey *__restrict__ key, const u8 *bases,
+                                                           const u8 *exps, u32 exp_bytes, u32 count, u8 *out)
+{
+    __shared__ u32 tab[16 * 64];
+    const u32 i = blockIdx.x;
+    if (i >= count)
+        return;
+    const u32 l = lane_id();
+    const u32 n = key->n[l], n0inv = key->n0inv, one = key->one[l];
+    const u32 bm = mont_mul(load_be_limb(bases + (u64)i * 256, l), key->r2[l], n, n0inv, l);
+    const u8 *e = exps + (u64)i * exp_bytes;
+    auto nib = [&](u32 k) -> u32 {  // nibble k counted from the least significant
+        const u8 byte = e[exp_bytes - 1 - k / 2];
+        return (k & 1) ? (u32)(byte >> 4) : (u32)(byte & 15);
+    };
+    const u32 r = mont_pow(bm, one, n, n0inv, l, 2 * exp_bytes, nib, tab);
+    store_be_limb(out + (u64)i * 256, l, mont_mul(r, l == 0 ? 1u : 0u, n, n0inv, l));
+}
+
+// out_i = a_i * b_i mod n: (a_i R) * b_i * R^-1
+__global__ __launch_bounds__(64) void sec_bn_mulmod_kernel(const sec::BnKey *__restrict__ key, const u8 *a,
+                                                           const u8 *b, u32 count, u8 *out)
+{
+    const u32 i = blockIdx.x;
+    if (i >= count)
+        return;
+    const u32 l = lane_id();
+    const u32 n = key->n[l], n0inv = key->n0inv;
+    const u32 am = mont_mul(load_be_limb(a + (u64)i * 256, l), key->r2[l], n, n0inv, l);
+    store_be_limb(out + (u64)i * 256, l, mont_mul(load_be_limb(b + (u64)i * 256, l), am, n, n0inv, l));
+}
+
+// APDP generate_tag for one piece: X = piece mod n; tag = (fdh * g^X)^d mod n.
+__global__ __launch_bounds__(64) void sec_apdp_tag_kernel(const sec::TagKey *__restrict__ tk, const u8 *base0,
+                                                          const sec::MsgDesc *__restrict__ msgs, u32 nmsgs,
+                                                          u8 *tags)
+{
+    __shared__ u32 tab[16 * 64];
+    const u32 i = blockIdx.x;
+    if (i >= nmsgs)
+        return;
+    const u32 l = lane_id();
+    const sec::MsgDesc m = msgs[i];
+    const u32 n = tk->k.n[l], n0inv = tk->k.n0inv, one = tk->k.one[l];
+    const u32 X = reduce_msg(base0 + m.off, m.len, m.avail, n, tk->k.r2[l], n0inv, l);
+    auto xnib = [&](u32 k) -> u32 { return (bcast(X, k / 8) >> (4 * (k % 8))) & 15u; };
+    const u32 t1 = mont_pow(tk->g_m[l], one, n, n0inv, l, 512, xnib, tab);
+    const u32 base = mont_mul(tk->fdh_m[l], t1, n, n0inv, l);
+    const u32 d = tk->d[l];
+    auto dnib = [&](u32 k) -> u32 { return (bcast(d, k / 8) >> (4 * (k % 8))) & 15u; };
+    const u32 tag_m = mont_pow(base, one, n, n0inv, l, 512, dnib, tab);
+    store_be_limb(tags + (u64)i * 256, l, mont_mul(tag_m, l == 0 ? 1u : 0u, n, n0inv, l));
+}
+
+}  // namespace
+
+int sec_launch_bn_setup(const uint8_t *n_be, uint32_t n0inv, sec::BnKey *key, void *stream)
+{
+    hipLaunchKernelGGL(sec_bn_setup_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, n_be, n0inv, key);
+    return hipGetLastError();
+}
+
+int sec_launch_tag_setup(const uint8_t *g_be, const uint8_t *fdh_be, const uint8_t *d_be, sec::TagKey *tk,
+                         void *stream)
+{
+    hipLaunchKernelGGL(sec_tag_setup_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, g_be, fdh_be, d_be, tk);
+    return hipGetLastError();
+}
+
+int sec_launch_bn_reduce(const sec::BnKey *key, const uint8_t *base0, const sec::MsgDesc *msgs, uint32_t nmsgs,
+                         uint8_t *out, void *stream)
+{
+    if (nmsgs == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_bn_reduce_kernel, dim3(nmsgs), dim3(64), 0, (hipStream_t)stream, key, base0, msgs, nmsgs,
+                       out);
+    return hipGetLastError();
+}
+
+int sec_launch_bn_modexp(const sec::BnKey *key, const uint8_t *bases, const uint8_t *exps, uint32_t exp_bytes,
+                         uint32_t count, uint8_t *out, void *stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_bn_modexp_kernel, dim3(count), dim3(64), 0, (hipStream_t)stream, key, bases, exps,
+                       exp_bytes, count, out);
+    return hipGetLastError();
+}
+
+int sec_launch_bn_mulmod(const sec::BnKey *key, const uint8_t *a, const uint8_t *b, uint32_t count, uint8_t *out,
+                         void *stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_bn_mulmod_kernel, dim3(count), dim3(64), 0, (hipStream_t)stream, key, a, b, count, out);
+    return hipGetLastError();
+}
+
+int sec_launch_apdp_tag(const sec::TagKey *tk, const uint8_t *base0, const sec::MsgDesc *msgs, uint32_t nmsgs,
+                        uint8_t *tags, void *stream)
+{
+    if (nmsgs == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_apdp_tag_kernel, dim3(nmsgs), dim3(64), 0, (hipStream_t)stream, tk, base0, msgs, nmsgs,
+                       tags);
+    return hipGetLastError();
+}

@@ -74,6 +74,9 @@ def device_count() -> int:
     return n.value if rc == 0 else 0
 
 
+_TIMING_KINDS = {"encode": 0, "decode": 1, "sha1": 2, "bignum": 3}
+
+
 class Engine:
     """A libstorbec context on one device.  Not thread-safe; use ``get_engine()`` per thread."""
 
@@ -113,10 +116,11 @@ class Engine:
         self._check(self.lib.sec_ctx_set_timing(self._ctx, int(bool(enable))))
 
     def collect_timing(self, kind: str) -> tuple[float, int]:
-        """(summed kernel ms, launch count) recorded since the last collect; kind 'encode'|'decode'."""
+        """(summed kernel ms, launch count) recorded since the last collect;
+        kind 'encode' | 'decode' | 'sha1' | 'bignum'."""
         ms = ctypes.c_double(0)
         n = ctypes.c_int64(0)
-        self._check(self.lib.sec_timing_collect(self._ctx, {"encode": 0, "decode": 1}[kind], ctypes.byref(ms),
+        self._check(self.lib.sec_timing_collect(self._ctx, _TIMING_KINDS[kind], ctypes.byref(ms),
                                           ctypes.byref(n)))
         return ms.value, n.value
 
