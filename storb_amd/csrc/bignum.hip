@@ -27,18 +27,37 @@ __device__ __forceinline__ u32 bcast(u32 x, u32 i) { return __builtin_amdgcn_rea
 
 __device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
 
+// Cross-lane limb shifts.  SEC_BN_DPP=1: DPP wave_shl:1 / wave_shr:1 (a VALU modifier, no
+// LDS round trip; the lane without a source reads the zero `old`).  0: ds_bpermute.
+#ifndef SEC_BN_DPP
+#define SEC_BN_DPP 1
+#endif
+#ifndef SEC_BN_UNROLL
+#define SEC_BN_UNROLL 8
+#endif
+
 // lane j <- x[j+1]; lane 63 <- 0
 __device__ __forceinline__ u32 down1(u32 x, u32 l)
 {
+#if SEC_BN_DPP
+    (void)l;
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
+#else
     const u32 y = (u32)__builtin_amdgcn_ds_bpermute((int)(((l + 1) & 63) << 2), (int)x);
     return l == 63 ? 0u : y;
+#endif
 }
 
 // lane j <- x[j-1]; lane 0 <- 0
 __device__ __forceinline__ u32 up1(u32 x, u32 l)
 {
+#if SEC_BN_DPP
+    (void)l;
+    return (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
+#else
     const u32 y = (u32)__builtin_amdgcn_ds_bpermute((int)(((l + 63) & 63) << 2), (int)x);
     return l == 0 ? 0u : y;
+#endif
 }
 
 // Carry-in mask of a multi-limb add: limb j generates (G) or propagates (P) a carry
@@ -82,11 +101,110 @@ __device__ __forceinline__ u32 sub_n(u32 a, u32 n, u32 l)
     return a - n - (u32)((B >> l) & 1u);
 }
 
-// Montgomery product a*b*R^-1 mod n for a, b < n.
+#ifndef SEC_BN_MM
+#define SEC_BN_MM 3
+#endif
+
+// Montgomery product a*b*R^-1 mod n for a < 2^2048, b < n (result < n).
+//
+// Row i adds a_i*b + m*n (m making limb 0 vanish) and shifts down one limb.  Lane j keeps
+// t_j plus carry bits owed to limb j+1, kept as the carry-outs of its own add chain (k1,
+// k2) rather than normalised each row: the next row's add chain takes them back as
+// carry-ins.  p2 = m*n_j + p1_j (the whole first product as the 64-bit addend) may carry
+// out of 64 bits; that bit belongs to limb j+1 after the shift (the next lane, moved with
+// a ballot), and lane 63's goes in through the DPP shift's `old` operand next row.
+#if SEC_BN_MM == 3
+// The same rows as SEC_BN_MM == 2, scheduled by hand: 7 VALU + 5 SALU per row (the
+// compiler's rendering of the C++ spends ~16 VALU, mostly moves that rebuild 64-bit
+// operand pairs).  Hard registers, so the pair {t, 0} (v[40:41]) is the first product's
+// addend without a copy:
+//   v[40:41] {t, 0}   v[42:43] p1   v[44:45] p2   v47 carry bit of p2 from lane j-1
+//   s40 a_i   s41 m   s[42:43] p2 carry-outs (K)   s[44:45] K << 1
+//   vcc, s[48:49] the two add-chain carries (k1, k2)   s[50:51] scratch
+//   s[52:53] p1's (always zero) carry-out   s[54:55] lane-63 mask
+// The shifted limb comes in as the DPP operand of the first add (wave_shl:1; lane 63
+// reads 0 under bound_ctrl).  Lane 63's K lands in k2's bit 63 one row later (before
+// k2 is next read): the value is < 2n < 2^2049 after every row, so at most one of the
+// position-64 bits (k1, k2, K of lane 63) is set.
+// Hazards: >= 1 wait state between mad1's write of v42 and v_readlane of it (the two
+// SALU ops of the lane-63 merge); >= 2 between mad2's write of v44 and its DPP read
+// (s_lshl + v_cndmask).
+__device__ __forceinline__ u32 mont_mul(u32 a, u32 b, u32 n, u32 n0inv, u32 l)
+{
+    u32 t;
+    u64 k1, k2;
+    asm volatile(
+        "v_mov_b32 v40, 0\n"
+        "v_mov_b32 v41, 0\n"
+        "s_mov_b64 vcc, 0\n"
+        "s_mov_b64 s[48:49], 0\n"
+        "s_mov_b64 s[42:43], 0\n"
+        "s_mov_b32 s54, 0\n"
+        "s_mov_b32 s55, 0x80000000\n"
+        ".irp i, 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19,20,21,22,23,24,25,26,27,28,29,30,31,"
+        "32,33,34,35,36,37,38,39,40,41,42,43,44,45,46,47,48,49,50,51,52,53,54,55,56,57,58,59,60,61,62,63\n"
+        "v_readlane_b32 s40, %[a], \\i\n"
+        "v_mad_u64_u32 v[42:43], s[52:53], s40, %[b], v[40:41]\n"
+        "s_and_b64 s[50:51], s[42:43], s[54:55]\n"
+        "s_or_b64 s[48:49], s[48:49], s[50:51]\n"
+        "v_readlane_b32 s41, v42, 0\n"
+        "s_mul_i32 s41, s41, %[n0]\n"
+        "v_mad_u64_u32 v[44:45], s[42:43], s41, %[n], v[42:43]\n"
+        "s_lshl_b64 s[44:45], s[42:43], 1\n"
+        "v_cndmask_b32_e64 v47, 0, 1, s[44:45]\n"
+        "v_addc_co_u32_dpp v40, vcc, v44, v45, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_addc_co_u32_e64 v40, s[48:49], v40, v47, s[48:49]\n"
+        ".endr\n"
+        "s_and_b64 s[50:51], s[42:43], s[54:55]\n"
+        "s_or_b64 s[48:49], s[48:49], s[50:51]\n"
+        "v_mov_b32 %[t], v40\n"
+        "s_mov_b64 %[k1], vcc\n"
+        "s_mov_b64 %[k2], s[48:49]\n"
+        : [t] "=v"(t), [k1] "=s"(k1), [k2] "=s"(k2)
+        : [a] "v"(a), [b] "v"(b), [n] "v"(n), [n0] "s"(n0inv)
+        : "v40", "v41", "v42", "v43", "v44", "v45", "v47", "s40", "s41", "s42", "s43", "s44", "s45", "s48",
+          "s49", "s50", "s51", "s52", "s53", "s54", "s55", "vcc");
+    const u32 c = (u32)((k1 >> l) & 1u) + (u32)((k2 >> l) & 1u);
+    u32 top = bcast(c, 63);
+    top += resolve((u64)t + up1(c, l), l, &t);
+    if (geq(t, n, top))  // the product is < 2n
+        t = sub_n(t, n, l);
+    return t;
+}
+#elif SEC_BN_MM == 2
+__device__ u32 mont_mul(u32 a, u32 b, u32 n, u32 n0inv, u32 l)
+{
+    u32 t = 0, k1 = 0, k2 = 0, kt = 0;
+#pragma unroll SEC_BN_UNROLL
+    for (u32 i = 0; i < 64; ++i) {
+        const u32 ai = bcast(a, i);
+        const u64 p1 = (u64)ai * b + t;  // < 2^64
+        const u32 m = bcast((u32)p1, 0) * n0inv;
+        const u64 mn = (u64)m * n;
+        const u64 p2 = mn + p1;  // limb 0 of lane 0 is 0 mod 2^32
+        const bool K = p2 < p1;
+        const u32 d = (u32)__builtin_amdgcn_update_dpp((int)kt, (int)(u32)p2, 0x130, 0xf, 0xf, false);
+        const u32 kin = (u32)((ballot(K) << 1) >> l) & 1u;
+        unsigned c1, c2;
+        u32 x = __builtin_addc(d, (u32)(p2 >> 32), k1, &c1);
+        x = __builtin_addc(x, kin, k2, &c2);
+        t = x;
+        k1 = c1;
+        k2 = c2;
+        kt = K ? 1u : 0u;
+    }
+    const u32 c = k1 + k2;
+    u32 top = bcast(c, 63) + bcast(kt, 63);
+    top += resolve((u64)t + up1(c, l), l, &t);
+    if (geq(t, n, top))  // the product is < 2n
+        t = sub_n(t, n, l);
+    return t;
+}
+#else
 __device__ u32 mont_mul(u32 a, u32 b, u32 n, u32 n0inv, u32 l)
 {
     u32 t = 0, c = 0;  // value = sum t_j 2^32j + sum c_j 2^32(j+1), c_j <= 3
-#pragma unroll 8
+#pragma unroll SEC_BN_UNROLL
     for (u32 i = 0; i < 64; ++i) {
         const u32 ai = bcast(a, i);
         const u64 p1 = (u64)ai * b + t;
@@ -103,6 +221,7 @@ __device__ u32 mont_mul(u32 a, u32 b, u32 n, u32 n0inv, u32 l)
         t = sub_n(t, n, l);
     return t;
 }
+#endif
 
 // (a + x) mod n for a < n and x < 2^2048 (so a + x < 3n: n has its top bit set)
 __device__ u32 add_mod(u32 a, u32 x, u32 n, u32 l)
@@ -119,28 +238,34 @@ __device__ u32 add_mod(u32 a, u32 x, u32 n, u32 l)
 
 // 4-bit fixed-window exponentiation in Montgomery form; the exponent's nibbles come from
 // `nib(i)` for i = nnib-1 .. 0 (most significant first).  tab: 16 x 64 u32 of LDS.
+// Two mont_mul call sites only (table, then one loop for squarings and products): each
+// inlined product is ~1k instructions, so call sites are kept few for the I-cache.
 template <class Nib>
 __device__ u32 mont_pow(u32 base_m, u32 one_m, u32 n, u32 n0inv, u32 l, u32 nnib, Nib nib, u32 *tab)
 {
     tab[l] = one_m;
     tab[64 + l] = base_m;
     u32 x = base_m;
+#pragma unroll 1
     for (u32 w = 2; w < 16; ++w) {
         x = mont_mul(x, base_m, n, n0inv, l);
         tab[w * 64 + l] = x;
     }
-    u32 r = one_m;
-    bool started = false;
-    for (u32 i = nnib; i-- > 0;) {
-        const u32 v = nib(i);
-        if (started)
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-                r = mont_mul(r, r, n, n0inv, l);
+    u32 i = nnib, r = one_m;
+    while (i > 0) {  // leading zero nibbles cost nothing
+        const u32 v = nib(--i);
         if (v) {
-            r = started ? mont_mul(r, tab[v * 64 + l], n, n0inv, l) : tab[v * 64 + l];
-            started = true;
+            r = tab[v * 64 + l];
+            break;
         }
+    }
+#pragma unroll 1
+    for (; i > 0; --i) {
+        const u32 v = nib(i - 1);
+        const u32 ops = v ? 5u : 4u;  // 4 squarings, then the table product
+#pragma unroll 1
+        for (u32 s = 0; s < ops; ++s)
+            r = mont_mul(r, s < 4 ? r : tab[v * 64 + l], n, n0inv, l);
     }
     return r;
 }
@@ -289,12 +414,16 @@ __global__ __launch_bounds__(64) void sec_apdp_tag_kernel(const sec::TagKey *__r
     const sec::MsgDesc m = msgs[i];
     const u32 n = tk->k.n[l], n0inv = tk->k.n0inv, one = tk->k.one[l];
     const u32 X = reduce_msg(base0 + m.off, m.len, m.avail, n, tk->k.r2[l], n0inv, l);
-    auto xnib = [&](u32 k) -> u32 { return (bcast(X, k / 8) >> (4 * (k % 8))) & 15u; };
-    const u32 t1 = mont_pow(tk->g_m[l], one, n, n0inv, l, 512, xnib, tab);
-    const u32 base = mont_mul(tk->fdh_m[l], t1, n, n0inv, l);
-    const u32 d = tk->d[l];
-    auto dnib = [&](u32 k) -> u32 { return (bcast(d, k / 8) >> (4 * (k % 8))) & 15u; };
-    const u32 tag_m = mont_pow(base, one, n, n0inv, l, 512, dnib, tab);
+    // pass 0: t1 = g^X; pass 1: tag = (fdh * t1)^d  (one mont_pow instance for both)
+    u32 base = tk->g_m[l], e = X, r = 0;
+#pragma unroll 1
+    for (int pass = 0; pass < 2; ++pass) {
+        r = mont_pow(base, one, n, n0inv, l, 512,
+                     [&](u32 k) -> u32 { return (bcast(e, k / 8) >> (4 * (k % 8))) & 15u; }, tab);
+        base = mont_mul(tk->fdh_m[l], r, n, n0inv, l);
+        e = tk->d[l];
+    }
+    const u32 tag_m = r;
     store_be_limb(tags + (u64)i * 256, l, mont_mul(tag_m, l == 0 ? 1u : 0u, n, n0inv, l));
 }
 

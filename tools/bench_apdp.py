@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--piece-bytes", type=int, default=262144)
     ap.add_argument("--modexps", type=int, default=16384)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--quick", action="store_true", help="kernels only (no CPU baseline / API legs)")
     args = ap.parse_args()
 
     import torch
@@ -99,6 +100,9 @@ def main():
     res["tag_fused"] = {"kernel_ms": round(ms, 3), "tags_per_s": round(P / ms * 1e3, 1),
                         "piece_GBs": round(P * L / ms / 1e6, 2)}
 
+    if args.quick:
+        print(json.dumps(res))
+        return
     # CPU: the reference's generate_tag arithmetic restated (CPython pow), one core
     cpu_rng = random.Random(3)
     cnt, t_start = 0, time.perf_counter()
