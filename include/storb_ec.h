@@ -57,7 +57,8 @@ enum sec_status {
     SEC_ENOMEM = -11,    /* device / pinned allocation failed                          */
     SEC_ESINGULAR = -12, /* decode matrix singular (cannot happen for valid inputs)    */
     SEC_EMODULUS = -13,  /* bignum modulus not an odd 2048-bit integer                 */
-    SEC_ENOTAG = -14     /* sec_apdp_tag_batch on a key without sec_bn_key_set_tag     */
+    SEC_ENOTAG = -14,    /* APDP call on a key without sec_bn_key_set_tag              */
+    SEC_ENOCRT = -15     /* CRT call on a key without sec_bn_key_set_crt               */
 };
 
 /* flags for sec_encode_batch / sec_decode_batch */
@@ -176,10 +177,19 @@ typedef struct sec_bn_key sec_bn_key;
 
 int sec_bn_key_create(sec_ctx *ctx, const uint8_t n_be[256], sec_bn_key **out);
 void sec_bn_key_destroy(sec_bn_key *key);
-/* generate_tag's per-key constants: g, fdh = full_domain_hash(prf(prf_key, 0))
- * (each taken mod n) and the private exponent d (< 2^2048).  Host memory. */
-int sec_bn_key_set_tag(sec_ctx *ctx, sec_bn_key *key, const uint8_t g_be[256],
-                       const uint8_t fdh_be[256], const uint8_t d_be[256]);
+/* The key owner's factors (the validator's RSA key): n = p*q with p, q odd and exactly
+ * 1024 bits (128 B big-endian each), cp = q*(q^-1 mod p) and cq = p*(p^-1 mod q) (256 B,
+ * mod n).  Enables sec_bn_crt_modexp_batch and CRT tags.  The caller guarantees
+ * n = p*q; p or q not odd 1024-bit integers give SEC_EMODULUS. */
+int sec_bn_key_set_crt(sec_ctx *ctx, sec_bn_key *key, const uint8_t p_be[128], const uint8_t q_be[128],
+                       const uint8_t cp_be[256], const uint8_t cq_be[256]);
+/* generate_tag's per-key constants: g, fdh = full_domain_hash(prf(prf_key, 0)) (each taken
+ * mod n) and the private exponent d (< 2^2048), 256 B each.  dp, dq (128 B each, or both
+ * NULL): exponents for p and q congruent to d mod p-1 and q-1, nonzero when d is (e.g.
+ * (d-1) mod (p-1) + 1); given with a CRT key, tags run as two 1024-bit halves.  Builds the
+ * key's 16 MiB fixed-base table of g (sec_apdp_gpow_batch, tags).  Host memory. */
+int sec_bn_key_set_tag(sec_ctx *ctx, sec_bn_key *key, const uint8_t g_be[256], const uint8_t fdh_be[256],
+                       const uint8_t d_be[256], const uint8_t *dp_be, const uint8_t *dq_be);
 
 /* out[i] = int.from_bytes(message i, "big") mod n (256 B each); messages as in
  * sec_sha1_batch (bytes past `avail` read as zero).  block_int of
@@ -191,11 +201,24 @@ int sec_bn_reduce_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs
 int sec_bn_modexp_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *bases,
                         const uint8_t *exps, uint32_t exp_bytes, int64_t count, uint8_t *out,
                         unsigned flags);
+/* out[i] = bases[i] ^ e[i] mod n by CRT, given exps_p[i] / exps_q[i] (exp_bytes each,
+ * big-endian, 1 <= exp_bytes <= 4096) congruent to e[i] mod p-1 / q-1 and nonzero when
+ * e[i] is (e.g. (e-1) mod (p-1) + 1): exact for every base, including multiples of p or
+ * q.  Needs sec_bn_key_set_crt. */
+int sec_bn_crt_modexp_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *bases,
+                            const uint8_t *exps_p, const uint8_t *exps_q, uint32_t exp_bytes,
+                            int64_t count, uint8_t *out, unsigned flags);
+/* out[i] = g ^ exps[i] mod n from the fixed-base table (issue_challenge's g_s,
+ * challenge/__init__.py:387); exps: exp_bytes each, 1 <= exp_bytes <= 256.  Needs
+ * sec_bn_key_set_tag. */
+int sec_apdp_gpow_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *exps, uint32_t exp_bytes,
+                        int64_t count, uint8_t *out, unsigned flags);
 /* out[i] = a[i] * b[i] mod n (256 B each, any values < 2^2048). */
 int sec_bn_mulmod_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *a, const uint8_t *b,
                         int64_t count, uint8_t *out, unsigned flags);
 /* APDP tags, fused per message: X = message mod n; tag = (fdh * g^X)^d mod n
- * (generate_tag's tag_value).  Needs sec_bn_key_set_tag; 256 B per tag. */
+ * (generate_tag's tag_value), g^X from the fixed-base table, the d power by CRT when
+ * the key has it.  Needs sec_bn_key_set_tag; 256 B per tag. */
 int sec_apdp_tag_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs, int64_t nmsgs,
                        uint8_t *tags, unsigned flags);
 

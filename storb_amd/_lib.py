@@ -30,6 +30,7 @@ SEC_ENOMEM = -11
 SEC_ESINGULAR = -12
 SEC_EMODULUS = -13
 SEC_ENOTAG = -14
+SEC_ENOCRT = -15
 
 SEC_F_HOST = 1
 SEC_F_ASYNC = 2
@@ -86,10 +87,14 @@ _SIGS = {
     "sec_encode_digest_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_uint]),
     "sec_bn_key_create": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(_vp)]),
     "sec_bn_key_destroy": (None, [_vp]),
-    "sec_bn_key_set_tag": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "sec_bn_key_set_crt": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "sec_bn_key_set_tag": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sec_bn_reduce_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp, ctypes.c_uint]),
     "sec_bn_modexp_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_int64, _vp,
                                            ctypes.c_uint]),
+    "sec_bn_crt_modexp_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_int64, _vp,
+                                               ctypes.c_uint]),
+    "sec_apdp_gpow_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint32, ctypes.c_int64, _vp, ctypes.c_uint]),
     "sec_bn_mulmod_batch": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_int64, _vp, ctypes.c_uint]),
     "sec_apdp_tag_batch": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, _vp, ctypes.c_uint]),
     "sec_malloc": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),

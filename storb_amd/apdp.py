@@ -16,9 +16,12 @@ Deliberate differences:
 * only 2048-bit keys (the reference's ``DEFAULT_RSA_KEY_SIZE``): the kernels are
   one-wave-per-2048-bit-integer; ``initialize_keys(rsa_bits=other)`` raises APDPError.
 * ``g`` and ``s`` come from ``secrets`` rather than ``random`` (same ranges).
-* the modular inverse in ``verify_proof`` is ``den^(phi(n)-1)`` on the GPU (the verifier
-  holds p and q), checked by ``den * inv == 1``; a non-invertible denominator raises
-  APDPError as gmpy2's ``powmod(x, -1, n)`` does.
+* the validator holds p and q, so its exponentiations (the d power of ``generate_tag``,
+  everything in ``verify_proof``) run by CRT as two 1024-bit halves, and g's powers
+  (``g^X`` in tags, ``g^s`` in challenges) come from a per-key fixed-base table; the
+  results are the same integers.  The modular inverse in ``verify_proof`` is
+  ``den^(p-2)`` / ``den^(q-2)`` per factor, checked by ``den * inv == 1``; a
+  non-invertible denominator raises APDPError as gmpy2's ``powmod(x, -1, n)`` does.
 * ``generate_proof`` / ``verify_proof`` take ``n`` (and ``e``) as optional: they default to
   the system's own key, which is how the reference's own tests call them
   (challenge_test.py:79,82).  A modulus other than the key's makes ``verify_proof`` return
@@ -277,7 +280,8 @@ class ChallengeSystem:
         self.key = APDPKey()
         self._local = threading.local()
 
-    # ModKeys live on the calling thread's engine, one per modulus
+    # ModKeys live on the calling thread's engine, one per modulus.  The system's own key
+    # also gets its factors (CRT) and, for tags / challenges, g's fixed-base table.
     def _modkey(self, n: int, tag: bool = False) -> ModKey:
         cache = getattr(self._local, "keys", None)
         if cache is None or getattr(self._local, "engine", None) is not get_engine():
@@ -288,11 +292,15 @@ class ChallengeSystem:
             if not (n.bit_length() == 8 * NBYTES and n & 1):
                 raise APDPError(f"storb_amd supports odd {8 * NBYTES}-bit moduli only.")
             mk = cache[n] = ModKey(n)
+        rsa = self.key.rsa
+        if rsa is not None and rsa.public_key().public_numbers().n == n and mk.p is None:
+            priv = rsa.private_numbers()
+            mk.set_crt(priv.p, priv.q)
         if tag:
-            sig = (self.key.g, self.key.prf_key, self.key.rsa.private_numbers().d)
+            sig = (self.key.g, self.key.prf_key, rsa.private_numbers().d)
             if getattr(mk, "_tag_sig", None) != sig:
-                fdh = CryptoUtils.full_domain_hash(self.key.rsa, CryptoUtils.prf(self.key.prf_key, 0))
-                mk.set_tag(self.key.g, fdh, self.key.rsa.private_numbers().d)
+                fdh = CryptoUtils.full_domain_hash(rsa, CryptoUtils.prf(self.key.prf_key, 0))
+                mk.set_tag(self.key.g, fdh, rsa.private_numbers().d)
                 mk._tag_sig = sig
         return mk
 
@@ -350,7 +358,7 @@ class ChallengeSystem:
                 if attempt > S_CANDIDATE_RETRY:
                     raise APDPError("Failed to find suitable s in Z*_n")
             ss.append(s)
-        g_ss = self._modkey(n).powmod([self.key.g] * len(ss), ss) if ss else []
+        g_ss = self._modkey(n, tag=True).gpow(ss) if ss else []
         out = []
         for tag, s, g_s in zip(parsed, ss, g_ss):
             try:
@@ -413,18 +421,18 @@ class ChallengeSystem:
         if n != pub.n:
             return [False] * len(items)
         priv = rsa_key.private_numbers()
-        phi = (priv.p - 1) * (priv.q - 1)
-        mk = self._modkey(n)
+        mk = self._modkey(n)  # the system's own key: CRT over p, q
         k = len(items)
         coefs = [int.from_bytes(CryptoUtils.prf(ch.prf_key, 0), "big") % n for _, ch, _ in items]
         fdhs = [CryptoUtils.full_domain_hash(rsa_key, t.prf_value) for _, _, t in items]
-        r1 = mk.powmod([_fit(p.tag_value, n) for p, _, _ in items] + fdhs, [e] * k + coefs)
+        r1 = mk.crt_powmod([_fit(p.tag_value, n) for p, _, _ in items] + fdhs, [e] * k + coefs)
         taus, dens = r1[:k], r1[k:]
-        invs = mk.powmod(dens, [phi - 1] * k)
+        # den^-1: den^(p-2) mod p and den^(q-2) mod q (Fermat per factor), checked below
+        invs = mk.crt_powmod_pq(dens, [priv.p - 2] * k, [priv.q - 2] * k)
         r2 = mk.mulmod(dens + taus, invs + invs)
         if any(v != 1 for v in r2[:k]):
             raise APDPError("Failed to invert denominator modulo n.")
-        tau_s = mk.powmod(r2[k:], [ch.s for _, ch, _ in items])
+        tau_s = mk.crt_powmod(r2[k:], [ch.s for _, ch, _ in items])
         out = []
         for (proof, _, _), v in zip(items, tau_s):
             expected = base64.b64encode(hashlib.sha256(int_to_bytes(v)).digest()).decode("utf-8")

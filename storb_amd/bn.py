@@ -52,6 +52,7 @@ class ModKey:
         self._check(self.lib.sec_bn_key_create(self.engine._ctx, nb, ctypes.byref(h)))
         self._key = h
         self.has_tag = False
+        self.p = self.q = None
 
     def _check(self, rc: int) -> None:
         self.engine._check(rc)
@@ -67,11 +68,33 @@ class ModKey:
         except Exception:
             pass
 
+    def set_crt(self, p: int, q: int) -> None:
+        """The key owner's factors (n = p*q, both 1024-bit): enables CRT exponentiation."""
+        if p * q != self.n or p.bit_length() != 1024 or q.bit_length() != 1024:
+            raise ValueError("p, q must be the 1024-bit factors of n")
+        cp = q * pow(q, -1, p) % self.n
+        cq = p * pow(p, -1, q) % self.n
+        self._check(self.lib.sec_bn_key_set_crt(self.engine._ctx, self._key, p.to_bytes(128, "big"),
+                                                q.to_bytes(128, "big"), cp.to_bytes(NBYTES, "big"),
+                                                cq.to_bytes(NBYTES, "big")))
+        self.p, self.q = p, q
+
+    @staticmethod
+    def _half_exp(e: int, m: int) -> int:
+        """An exponent congruent to e mod m and nonzero when e is: exact for every base."""
+        return 0 if e == 0 else (e - 1) % m + 1
+
     def set_tag(self, g: int, fdh: int, d: int) -> None:
-        """generate_tag's per-key constants: generator g, FDH of the PRF value, private d."""
+        """generate_tag's per-key constants: generator g, FDH of the PRF value, private d.
+        With set_crt done first, tags raise to d as two 1024-bit halves."""
         n = self.n
+        dp = dq = None
+        if self.p is not None:
+            dp = self._half_exp(d, self.p - 1).to_bytes(128, "big")
+            dq = self._half_exp(d, self.q - 1).to_bytes(128, "big")
         self._check(self.lib.sec_bn_key_set_tag(self.engine._ctx, self._key, (g % n).to_bytes(NBYTES, "big"),
-                                                (fdh % n).to_bytes(NBYTES, "big"), d.to_bytes(NBYTES, "big")))
+                                                (fdh % n).to_bytes(NBYTES, "big"), d.to_bytes(NBYTES, "big"),
+                                                dp, dq))
         self.has_tag = True
 
     # -- raw batches: device pointers (or host with host=True) ----------------------
@@ -94,6 +117,22 @@ class ModKey:
         o, _ko = addr(out)
         self._check(self.lib.sec_bn_modexp_batch(self.engine._ctx, self._key, b or None, e or None, exp_bytes,
                                                  count, o or None, _flags(host, asynchronous)))
+
+    def crt_modexp_batch(self, bases, exps_p, exps_q, exp_bytes: int, count: int, out, *, host: bool = False,
+                         asynchronous: bool = False) -> None:
+        b, _kb = addr(bases)
+        ep, _kp = addr(exps_p)
+        eq, _kq = addr(exps_q)
+        o, _ko = addr(out)
+        self._check(self.lib.sec_bn_crt_modexp_batch(self.engine._ctx, self._key, b or None, ep or None, eq or None,
+                                                     exp_bytes, count, o or None, _flags(host, asynchronous)))
+
+    def gpow_batch(self, exps, exp_bytes: int, count: int, out, *, host: bool = False,
+                   asynchronous: bool = False) -> None:
+        e, _ke = addr(exps)
+        o, _ko = addr(out)
+        self._check(self.lib.sec_apdp_gpow_batch(self.engine._ctx, self._key, e or None, exp_bytes, count,
+                                                 o or None, _flags(host, asynchronous)))
 
     def mulmod_batch(self, a, b, count: int, out, *, host: bool = False, asynchronous: bool = False) -> None:
         pa, _ka = addr(a)
@@ -147,6 +186,42 @@ class ModKey:
             raise ValueError("exponent wider than 32768 bits")
         out = np.empty((len(bases), NBYTES), dtype=np.uint8)
         self.modexp_batch(to_be(bases), to_be(exps, width), width, len(bases), out, host=True)
+        return from_be(out)
+
+    def crt_powmod_pq(self, bases, exps_p, exps_q) -> list[int]:
+        """x with x = b^ep mod p and x = b^eq mod q, per item (needs set_crt)."""
+        if not (len(bases) == len(exps_p) == len(exps_q)):
+            raise ValueError("operands differ in length")
+        if not bases:
+            return []
+        width = max(1, max((int(e).bit_length() + 7) // 8 for e in list(exps_p) + list(exps_q)))
+        if width > 4096:
+            raise ValueError("exponent wider than 32768 bits")
+        out = np.empty((len(bases), NBYTES), dtype=np.uint8)
+        self.crt_modexp_batch(to_be(bases), to_be(exps_p, width), to_be(exps_q, width), width, len(bases), out,
+                              host=True)
+        return from_be(out)
+
+    def crt_powmod(self, bases, exps) -> list[int]:
+        """``[pow(b, e, n) ...]`` by CRT over the key's factors (needs set_crt)."""
+        if self.p is None:
+            raise ECRuntimeError("ModKey.crt_powmod needs set_crt(p, q) first")
+        if any(e < 0 for e in exps):
+            raise ValueError("negative exponent")
+        return self.crt_powmod_pq(bases, [self._half_exp(e, self.p - 1) for e in exps],
+                                  [self._half_exp(e, self.q - 1) for e in exps])
+
+    def gpow(self, exps) -> list[int]:
+        """``[pow(g, e, n) ...]`` from the key's fixed-base table of g (needs set_tag), e < 2^2048."""
+        if not self.has_tag:
+            raise ECRuntimeError("ModKey.gpow needs set_tag(g, fdh, d) first")
+        if not exps:
+            return []
+        if any(e < 0 or e >= 1 << (8 * NBYTES) for e in exps):
+            raise ValueError("exponent outside [0, 2^2048)")
+        width = max(1, max((int(e).bit_length() + 7) // 8 for e in exps))
+        out = np.empty((len(exps), NBYTES), dtype=np.uint8)
+        self.gpow_batch(to_be(exps, width), width, len(exps), out, host=True)
         return from_be(out)
 
     def mulmod(self, a, b) -> list[int]:

@@ -957,6 +957,7 @@ const char *sec_strerror(int s)
     case SEC_ESINGULAR: return "decode matrix is singular";
     case SEC_EMODULUS: return "modulus must be an odd 2048-bit integer";
     case SEC_ENOTAG: return "key has no APDP tag constants (sec_bn_key_set_tag)";
+    case SEC_ENOCRT: return "key has no CRT factors (sec_bn_key_set_crt)";
     default: return "unknown error";
     }
 }
@@ -1264,9 +1265,26 @@ int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *di
 
 struct sec_bn_key {
     int device = 0;
-    DevBuf dk;
-    bool has_tag = false;
+    DevBuf dk;     // TagKey, then 1 KiB of upload staging
+    DevBuf table;  // fixed-base table of g (sec::kGTabWords u32), once set_tag ran
+    bool has_tag = false, has_crt = false;
 };
+
+namespace {
+constexpr size_t kKeyStage = sizeof(sec::TagKey);
+
+uint32_t neg_inv32(const uint8_t *be, size_t nbytes)  // -n^-1 mod 2^32 from n's low limb
+{
+    const uint8_t *p = be + nbytes - 4;
+    const uint32_t n0 = (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+    uint32_t x = n0;  // n0 * n0 == 1 mod 8: 3 correct bits, doubling per Newton step
+    for (int i = 0; i < 4; ++i)
+        x *= 2u - n0 * x;
+    return 0u - x;
+}
+
+bool odd_top(const uint8_t *be, size_t nbytes) { return (be[0] & 0x80) && (be[nbytes - 1] & 1); }
+}  // namespace
 
 extern "C" {
 
@@ -1275,20 +1293,17 @@ int sec_bn_key_create(sec_ctx *ctx, const uint8_t *n_be, sec_bn_key **out)
     if (!ctx || !n_be || !out)
         return SEC_EINVAL;
     *out = nullptr;
-    if (!(n_be[0] & 0x80) || !(n_be[255] & 1))
+    if (!odd_top(n_be, 256))
         return SEC_EMODULUS;
     RC(set_dev(ctx));
-    const uint32_t n0 = (uint32_t)n_be[252] << 24 | (uint32_t)n_be[253] << 16 | (uint32_t)n_be[254] << 8 | n_be[255];
-    uint32_t x = n0;  // n0 * n0 == 1 mod 8: 3 correct bits, doubling per Newton step
-    for (int i = 0; i < 4; ++i)
-        x *= 2u - n0 * x;
     std::unique_ptr<sec_bn_key> key(new sec_bn_key());
     key->device = ctx->device;
-    RC(key->dk.ensure(sizeof(sec::TagKey) + 256));
-    uint8_t *nd = key->dk.as<uint8_t>(sizeof(sec::TagKey));
+    RC(key->dk.ensure(kKeyStage + 1024));
+    CK(hipMemsetAsync(key->dk.p, 0, sizeof(sec::TagKey), ctx->stream()));
+    uint8_t *nd = key->dk.as<uint8_t>(kKeyStage);
     hipStream_t s = ctx->stream();
     CK(hipMemcpyAsync(nd, n_be, 256, hipMemcpyHostToDevice, s));
-    int e = sec_launch_bn_setup(nd, 0u - x, key->dk.as<sec::BnKey>(), s);
+    int e = sec_launch_bn_setup(nd, neg_inv32(n_be, 256), 2048, key->dk.as<sec::BnKey>(), s);
     if (e)
         return hip_fail((hipError_t)e, "sec_bn_setup_kernel");
     CK(hipStreamSynchronize(s));
@@ -1302,26 +1317,69 @@ void sec_bn_key_destroy(sec_bn_key *key)
         return;
     (void)hipSetDevice(key->device);
     key->dk.release();
+    key->table.release();
     delete key;
 }
 
-int sec_bn_key_set_tag(sec_ctx *ctx, sec_bn_key *key, const uint8_t *g_be, const uint8_t *fdh_be,
-                       const uint8_t *d_be)
+int sec_bn_key_set_crt(sec_ctx *ctx, sec_bn_key *key, const uint8_t *p_be, const uint8_t *q_be, const uint8_t *cp_be,
+                       const uint8_t *cq_be)
 {
-    if (!ctx || !key || !g_be || !fdh_be || !d_be || key->device != ctx->device)
+    if (!ctx || !key || !p_be || !q_be || !cp_be || !cq_be || key->device != ctx->device)
         return SEC_EINVAL;
+    if (!odd_top(p_be, 128) || !odd_top(q_be, 128))
+        return SEC_EMODULUS;
     RC(set_dev(ctx));
     uint8_t host[768];
+    memcpy(host, p_be, 128);
+    memcpy(host + 128, q_be, 128);
+    memcpy(host + 256, cp_be, 256);
+    memcpy(host + 512, cq_be, 256);
+    uint8_t *st = key->dk.as<uint8_t>(kKeyStage);
+    sec::TagKey *tk = key->dk.as<sec::TagKey>();
+    hipStream_t s = ctx->stream();
+    CK(hipMemcpyAsync(st, host, sizeof(host), hipMemcpyHostToDevice, s));
+    int e = sec_launch_bn_setup(st, neg_inv32(p_be, 128), 1024, &tk->p, s);
+    if (!e)
+        e = sec_launch_bn_setup(st + 128, neg_inv32(q_be, 128), 1024, &tk->q, s);
+    if (!e)
+        e = sec_launch_crt_setup(st + 256, st + 512, tk, s);
+    if (e)
+        return hip_fail((hipError_t)e, "sec_bn_key_set_crt");
+    const uint32_t off = 0;  // tags need dp / dq too: CRT tags switch on in set_tag
+    CK(hipMemcpyAsync(&tk->crt, &off, sizeof(off), hipMemcpyHostToDevice, s));
+    CK(hipStreamSynchronize(s));
+    key->has_crt = true;
+    return SEC_OK;
+}
+
+int sec_bn_key_set_tag(sec_ctx *ctx, sec_bn_key *key, const uint8_t *g_be, const uint8_t *fdh_be,
+                       const uint8_t *d_be, const uint8_t *dp_be, const uint8_t *dq_be)
+{
+    if (!ctx || !key || !g_be || !fdh_be || !d_be || key->device != ctx->device || (!dp_be != !dq_be))
+        return SEC_EINVAL;
+    const bool crt = dp_be != nullptr;
+    if (crt && !key->has_crt)
+        return SEC_ENOCRT;
+    RC(set_dev(ctx));
+    uint8_t host[1024] = {0};
     memcpy(host, g_be, 256);
     memcpy(host + 256, fdh_be, 256);
     memcpy(host + 512, d_be, 256);
-    RC(key->dk.ensure(sizeof(sec::TagKey) + 768));
-    uint8_t *p = key->dk.as<uint8_t>(sizeof(sec::TagKey));
+    if (crt) {
+        memcpy(host + 768, dp_be, 128);
+        memcpy(host + 896, dq_be, 128);
+    }
+    RC(key->table.ensure(sec::kGTabWords * sizeof(uint32_t)));
+    uint8_t *st = key->dk.as<uint8_t>(kKeyStage);
+    sec::TagKey *tk = key->dk.as<sec::TagKey>();
     hipStream_t s = ctx->stream();
-    CK(hipMemcpyAsync(p, host, 768, hipMemcpyHostToDevice, s));
-    int e = sec_launch_tag_setup(p, p + 256, p + 512, key->dk.as<sec::TagKey>(), s);
+    CK(hipMemcpyAsync(st, host, sizeof(host), hipMemcpyHostToDevice, s));
+    int e = sec_launch_tag_setup(st, st + 256, st + 512, crt ? st + 768 : nullptr, crt ? st + 896 : nullptr, tk,
+                                 key->table.as<uint32_t>(), s);
     if (e)
-        return hip_fail((hipError_t)e, "sec_tag_setup_kernel");
+        return hip_fail((hipError_t)e, "sec_tag_setup");
+    const uint32_t flag = crt ? 1u : 0u;
+    CK(hipMemcpyAsync(&tk->crt, &flag, sizeof(flag), hipMemcpyHostToDevice, s));
     CK(hipStreamSynchronize(s));
     key->has_tag = true;
     return SEC_OK;
@@ -1348,10 +1406,11 @@ int sec_apdp_tag_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs,
     if (!key->has_tag)
         return SEC_ENOTAG;
     const sec::TagKey *tk = key->dk.as<sec::TagKey>();
+    const uint32_t *table = key->table.as<uint32_t>();
     return msg_batch(ctx, ctx->bn_plan, msgs, nmsgs, tags, 256, flags,
                      env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 3, "sec_apdp_tag_kernel",
-                     [tk](const uint8_t *base0, const sec::MsgDesc *md, uint32_t n, uint8_t *o, hipStream_t s) {
-                         return sec_launch_apdp_tag(tk, base0, md, n, o, s);
+                     [tk, table](const uint8_t *base0, const sec::MsgDesc *md, uint32_t n, uint8_t *o, hipStream_t s) {
+                         return sec_launch_apdp_tag(tk, table, base0, md, n, o, s);
                      });
 }
 
@@ -1369,6 +1428,44 @@ int sec_bn_modexp_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *base
                        (size_t)count * 256, flags, "sec_bn_modexp_kernel",
                        [&](const std::vector<const uint8_t *> &in, uint8_t *o, hipStream_t s) {
                            return sec_launch_bn_modexp(dk, in[0], in[1], exp_bytes, (uint32_t)count, o, s);
+                       });
+}
+
+int sec_bn_crt_modexp_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *bases, const uint8_t *exps_p,
+                            const uint8_t *exps_q, uint32_t exp_bytes, int64_t count, uint8_t *out, unsigned flags)
+{
+    if (!ctx || !key || key->device != ctx->device || count < 0 || count >= (int64_t)INT32_MAX ||
+        (count > 0 && (!bases || !exps_p || !exps_q || !out)) || exp_bytes < 1 || exp_bytes > 4096 ||
+        (flags & ~(SEC_F_HOST | SEC_F_ASYNC)))
+        return SEC_EINVAL;
+    if (!key->has_crt)
+        return SEC_ENOCRT;
+    if (count == 0)
+        return SEC_OK;
+    const sec::TagKey *tk = key->dk.as<sec::TagKey>();
+    const size_t eb = (size_t)count * exp_bytes;
+    return dense_batch(ctx, {{bases, (size_t)count * 256}, {exps_p, eb}, {exps_q, eb}}, out, (size_t)count * 256,
+                       flags, "sec_bn_crt_modexp_kernel",
+                       [&](const std::vector<const uint8_t *> &in, uint8_t *o, hipStream_t s) {
+                           return sec_launch_bn_crt_modexp(tk, in[0], in[1], in[2], exp_bytes, (uint32_t)count, o, s);
+                       });
+}
+
+int sec_apdp_gpow_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *exps, uint32_t exp_bytes, int64_t count,
+                        uint8_t *out, unsigned flags)
+{
+    if (!ctx || !key || key->device != ctx->device || count < 0 || count >= (int64_t)INT32_MAX ||
+        (count > 0 && (!exps || !out)) || exp_bytes < 1 || exp_bytes > 256 || (flags & ~(SEC_F_HOST | SEC_F_ASYNC)))
+        return SEC_EINVAL;
+    if (!key->has_tag)
+        return SEC_ENOTAG;
+    if (count == 0)
+        return SEC_OK;
+    const sec::TagKey *tk = key->dk.as<sec::TagKey>();
+    const uint32_t *table = key->table.as<uint32_t>();
+    return dense_batch(ctx, {{exps, (size_t)count * exp_bytes}}, out, (size_t)count * 256, flags,
+                       "sec_apdp_gpow_kernel", [&](const std::vector<const uint8_t *> &in, uint8_t *o, hipStream_t s) {
+                           return sec_launch_apdp_gpow(tk, table, in[0], exp_bytes, (uint32_t)count, o, s);
                        });
 }
 

@@ -1,16 +1,22 @@
-// bignum.hip — 2048-bit modular arithmetic on CDNA4 for storb's APDP proofs of data
+// bignum.hip — RSA-2048 modular arithmetic on CDNA4 for storb's APDP proofs of data
 // possession (F4: /root/reference/storb/challenge/__init__.py:304-350 generate_tag,
-// :401-463 generate_proof; DEFAULT_RSA_KEY_SIZE = 2048 at storb/constants.py:26).
+// :352-399 issue_challenge, :401-463 generate_proof, :465-528 verify_proof;
+// DEFAULT_RSA_KEY_SIZE = 2048 at storb/constants.py:26).
 //
-// One wave = one 2048-bit integer: lane j holds 32-bit limb j (little-endian limbs), so a
-// 64-lane wavefront is exactly one RSA-2048 residue.  Montgomery multiplication (R =
-// 2^2048) runs as 64 row steps: the row's limb a_i is broadcast with v_readlane, every
-// lane does two 32x32->64 multiply-adds (a_i*b_j and m*n_j), and the running sum moves
-// down one lane per step (ds_bpermute).  Carries stay in a redundant per-lane word and
-// are resolved once per product with two wave ballots (generate / propagate masks;
-// carry-lookahead done as 64-bit integer arithmetic on the masks).  The work is
-// integer-multiply / issue bound, not memory bound: ~1k VALU per product and ~6k
-// products per APDP tag.
+// One wave = one integer: lane j holds 32-bit limb j (little-endian limbs), so a 64-lane
+// wavefront is one RSA-2048 residue, and a 1024-bit CRT half (mod p or q) uses lanes 0..31
+// with lanes 32..63 zero.  Montgomery multiplication (R = 2^(32*ROWS)) runs as ROWS row
+// steps: the row's limb a_i is broadcast with v_readlane, every lane does two
+// 32x32->64 multiply-adds (a_i*b_j and m*n_j), and the running sum moves down one lane
+// per row (DPP wave_shl:1).  Carries stay redundant per lane and are resolved once per
+// product with two wave ballots (generate / propagate masks; carry-lookahead done as
+// 64-bit integer arithmetic on the masks).  The work is integer-multiply issue bound, not
+// memory bound.
+//
+// Where the key owner holds p and q (the validator: tags and verification) exponentiations
+// by secret-sized exponents run as two 1024-bit halves (CRT): half the rows per product
+// and half the exponent bits.  g^X for tags and g^s for challenges use a fixed-base table
+// of g^(v * 256^k) (255 products instead of ~2.6k).
 #include <hip/hip_runtime.h>
 
 #include "bignum.hpp"
@@ -27,37 +33,17 @@ __device__ __forceinline__ u32 bcast(u32 x, u32 i) { return __builtin_amdgcn_rea
 
 __device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
 
-// Cross-lane limb shifts.  SEC_BN_DPP=1: DPP wave_shl:1 / wave_shr:1 (a VALU modifier, no
-// LDS round trip; the lane without a source reads the zero `old`).  0: ds_bpermute.
-#ifndef SEC_BN_DPP
-#define SEC_BN_DPP 1
-#endif
-#ifndef SEC_BN_UNROLL
-#define SEC_BN_UNROLL 8
-#endif
+// lane j <- x[j+1]; lane 63 <- 0 (DPP wave_shl:1; the lane without a source keeps `old`)
+__device__ __forceinline__ u32 down1(u32 x) { return (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false); }
 
-// lane j <- x[j+1]; lane 63 <- 0
-__device__ __forceinline__ u32 down1(u32 x, u32 l)
-{
-#if SEC_BN_DPP
-    (void)l;
-    return (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
-#else
-    const u32 y = (u32)__builtin_amdgcn_ds_bpermute((int)(((l + 1) & 63) << 2), (int)x);
-    return l == 63 ? 0u : y;
-#endif
-}
+// lane j <- x[j-1]; lane 0 <- 0 (DPP wave_shr:1)
+__device__ __forceinline__ u32 up1(u32 x) { return (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false); }
 
-// lane j <- x[j-1]; lane 0 <- 0
-__device__ __forceinline__ u32 up1(u32 x, u32 l)
+// lane j <- x[j+32] for j < 32, 0 above: the high 1024 bits as a 1024-bit integer
+__device__ __forceinline__ u32 high_half(u32 x, u32 l)
 {
-#if SEC_BN_DPP
-    (void)l;
-    return (u32)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
-#else
-    const u32 y = (u32)__builtin_amdgcn_ds_bpermute((int)(((l + 63) & 63) << 2), (int)x);
-    return l == 0 ? 0u : y;
-#endif
+    const u32 y = (u32)__builtin_amdgcn_ds_bpermute((int)(((l + 32) & 63) << 2), (int)x);
+    return l < 32 ? y : 0u;
 }
 
 // Carry-in mask of a multi-limb add: limb j generates (G) or propagates (P) a carry
@@ -101,23 +87,34 @@ __device__ __forceinline__ u32 sub_n(u32 a, u32 n, u32 l)
     return a - n - (u32)((B >> l) & 1u);
 }
 
+// Final step of a Montgomery product: value = t + sum_j c_j 2^32(j+1) < 2n.
+__device__ __forceinline__ u32 mont_finish(u32 t, u32 c, u32 n, u32 l)
+{
+    u32 top = bcast(c, 63);
+    top += resolve((u64)t + up1(c), l, &t);
+    if (geq(t, n, top))
+        t = sub_n(t, n, l);
+    return t;
+}
+
 #ifndef SEC_BN_MM
 #define SEC_BN_MM 3
 #endif
 
-// Montgomery product a*b*R^-1 mod n for a < 2^2048, b < n (result < n).
+// Montgomery product a*b*R^-1 mod n, R = 2^(32*ROWS), for a < R, b < n (result < n).
+// ROWS = 64 (RSA-2048) or 32 (a 1024-bit CRT half; limbs 32..63 of a, b, n are zero).
 //
 // Row i adds a_i*b + m*n (m making limb 0 vanish) and shifts down one limb.  Lane j keeps
 // t_j plus carry bits owed to limb j+1, kept as the carry-outs of its own add chain (k1,
 // k2) rather than normalised each row: the next row's add chain takes them back as
 // carry-ins.  p2 = m*n_j + p1_j (the whole first product as the 64-bit addend) may carry
-// out of 64 bits; that bit belongs to limb j+1 after the shift (the next lane, moved with
-// a ballot), and lane 63's goes in through the DPP shift's `old` operand next row.
+// out of 64 bits; that bit belongs to limb j+1 after the shift (the next lane: the carry
+// mask shifted left by one).
 #if SEC_BN_MM == 3
-// The same rows as SEC_BN_MM == 2, scheduled by hand: 7 VALU + 5 SALU per row (the
-// compiler's rendering of the C++ spends ~16 VALU, mostly moves that rebuild 64-bit
-// operand pairs).  Hard registers, so the pair {t, 0} (v[40:41]) is the first product's
-// addend without a copy:
+// Hand-scheduled rows: 7 VALU + 5 SALU each (the compiler's rendering of the same
+// arithmetic in C++ spends ~16 VALU, mostly moves that rebuild 64-bit operand pairs).
+// Hard registers, so the pair {t, 0} (v[40:41]) is the first product's addend without a
+// copy:
 //   v[40:41] {t, 0}   v[42:43] p1   v[44:45] p2   v47 carry bit of p2 from lane j-1
 //   s40 a_i   s41 m   s[42:43] p2 carry-outs (K)   s[44:45] K << 1
 //   vcc, s[48:49] the two add-chain carries (k1, k2)   s[50:51] scratch
@@ -129,101 +126,74 @@ __device__ __forceinline__ u32 sub_n(u32 a, u32 n, u32 l)
 // Hazards: >= 1 wait state between mad1's write of v42 and v_readlane of it (the two
 // SALU ops of the lane-63 merge); >= 2 between mad2's write of v44 and its DPP read
 // (s_lshl + v_cndmask).
+#define SEC_BN_IRP32 "0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19,20,21,22,23,24,25,26,27,28,29,30,31"
+#define SEC_BN_IRP64 \
+    SEC_BN_IRP32 ",32,33,34,35,36,37,38,39,40,41,42,43,44,45,46,47,48,49,50,51,52,53,54,55,56,57,58,59,60,61,62,63"
+#define SEC_BN_ROWS_ASM(LIST)                                                                                    \
+    asm volatile("v_mov_b32 v40, 0\n"                                                                           \
+                 "v_mov_b32 v41, 0\n"                                                                           \
+                 "s_mov_b64 vcc, 0\n"                                                                           \
+                 "s_mov_b64 s[48:49], 0\n"                                                                      \
+                 "s_mov_b64 s[42:43], 0\n"                                                                      \
+                 "s_mov_b32 s54, 0\n"                                                                           \
+                 "s_mov_b32 s55, 0x80000000\n"                                                                  \
+                 ".irp i, " LIST "\n"                                                                           \
+                 "v_readlane_b32 s40, %[a], \\i\n"                                                              \
+                 "v_mad_u64_u32 v[42:43], s[52:53], s40, %[b], v[40:41]\n"                                      \
+                 "s_and_b64 s[50:51], s[42:43], s[54:55]\n"                                                     \
+                 "s_or_b64 s[48:49], s[48:49], s[50:51]\n"                                                      \
+                 "v_readlane_b32 s41, v42, 0\n"                                                                 \
+                 "s_mul_i32 s41, s41, %[n0]\n"                                                                  \
+                 "v_mad_u64_u32 v[44:45], s[42:43], s41, %[n], v[42:43]\n"                                      \
+                 "s_lshl_b64 s[44:45], s[42:43], 1\n"                                                           \
+                 "v_cndmask_b32_e64 v47, 0, 1, s[44:45]\n"                                                      \
+                 "v_addc_co_u32_dpp v40, vcc, v44, v45, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
+                 "v_addc_co_u32_e64 v40, s[48:49], v40, v47, s[48:49]\n"                                        \
+                 ".endr\n"                                                                                      \
+                 "s_and_b64 s[50:51], s[42:43], s[54:55]\n"                                                     \
+                 "s_or_b64 s[48:49], s[48:49], s[50:51]\n"                                                      \
+                 "v_mov_b32 %[t], v40\n"                                                                        \
+                 "s_mov_b64 %[k1], vcc\n"                                                                       \
+                 "s_mov_b64 %[k2], s[48:49]\n"                                                                  \
+                 : [t] "=v"(t), [k1] "=s"(k1), [k2] "=s"(k2)                                                    \
+                 : [a] "v"(a), [b] "v"(b), [n] "v"(n), [n0] "s"(n0inv)                                          \
+                 : "v40", "v41", "v42", "v43", "v44", "v45", "v47", "s40", "s41", "s42", "s43", "s44", "s45",   \
+                   "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "vcc")
+
+template <int ROWS>
 __device__ __forceinline__ u32 mont_mul(u32 a, u32 b, u32 n, u32 n0inv, u32 l)
 {
+    static_assert(ROWS == 64 || ROWS == 32, "RSA-2048 or a 1024-bit CRT half");
     u32 t;
     u64 k1, k2;
-    asm volatile(
-        "v_mov_b32 v40, 0\n"
-        "v_mov_b32 v41, 0\n"
-        "s_mov_b64 vcc, 0\n"
-        "s_mov_b64 s[48:49], 0\n"
-        "s_mov_b64 s[42:43], 0\n"
-        "s_mov_b32 s54, 0\n"
-        "s_mov_b32 s55, 0x80000000\n"
-        ".irp i, 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14,15,16,17,18,19,20,21,22,23,24,25,26,27,28,29,30,31,"
-        "32,33,34,35,36,37,38,39,40,41,42,43,44,45,46,47,48,49,50,51,52,53,54,55,56,57,58,59,60,61,62,63\n"
-        "v_readlane_b32 s40, %[a], \\i\n"
-        "v_mad_u64_u32 v[42:43], s[52:53], s40, %[b], v[40:41]\n"
-        "s_and_b64 s[50:51], s[42:43], s[54:55]\n"
-        "s_or_b64 s[48:49], s[48:49], s[50:51]\n"
-        "v_readlane_b32 s41, v42, 0\n"
-        "s_mul_i32 s41, s41, %[n0]\n"
-        "v_mad_u64_u32 v[44:45], s[42:43], s41, %[n], v[42:43]\n"
-        "s_lshl_b64 s[44:45], s[42:43], 1\n"
-        "v_cndmask_b32_e64 v47, 0, 1, s[44:45]\n"
-        "v_addc_co_u32_dpp v40, vcc, v44, v45, vcc wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_addc_co_u32_e64 v40, s[48:49], v40, v47, s[48:49]\n"
-        ".endr\n"
-        "s_and_b64 s[50:51], s[42:43], s[54:55]\n"
-        "s_or_b64 s[48:49], s[48:49], s[50:51]\n"
-        "v_mov_b32 %[t], v40\n"
-        "s_mov_b64 %[k1], vcc\n"
-        "s_mov_b64 %[k2], s[48:49]\n"
-        : [t] "=v"(t), [k1] "=s"(k1), [k2] "=s"(k2)
-        : [a] "v"(a), [b] "v"(b), [n] "v"(n), [n0] "s"(n0inv)
-        : "v40", "v41", "v42", "v43", "v44", "v45", "v47", "s40", "s41", "s42", "s43", "s44", "s45", "s48",
-          "s49", "s50", "s51", "s52", "s53", "s54", "s55", "vcc");
+    if constexpr (ROWS == 64)
+        SEC_BN_ROWS_ASM(SEC_BN_IRP64);
+    else
+        SEC_BN_ROWS_ASM(SEC_BN_IRP32);
     const u32 c = (u32)((k1 >> l) & 1u) + (u32)((k2 >> l) & 1u);
-    u32 top = bcast(c, 63);
-    top += resolve((u64)t + up1(c, l), l, &t);
-    if (geq(t, n, top))  // the product is < 2n
-        t = sub_n(t, n, l);
-    return t;
-}
-#elif SEC_BN_MM == 2
-__device__ u32 mont_mul(u32 a, u32 b, u32 n, u32 n0inv, u32 l)
-{
-    u32 t = 0, k1 = 0, k2 = 0, kt = 0;
-#pragma unroll SEC_BN_UNROLL
-    for (u32 i = 0; i < 64; ++i) {
-        const u32 ai = bcast(a, i);
-        const u64 p1 = (u64)ai * b + t;  // < 2^64
-        const u32 m = bcast((u32)p1, 0) * n0inv;
-        const u64 mn = (u64)m * n;
-        const u64 p2 = mn + p1;  // limb 0 of lane 0 is 0 mod 2^32
-        const bool K = p2 < p1;
-        const u32 d = (u32)__builtin_amdgcn_update_dpp((int)kt, (int)(u32)p2, 0x130, 0xf, 0xf, false);
-        const u32 kin = (u32)((ballot(K) << 1) >> l) & 1u;
-        unsigned c1, c2;
-        u32 x = __builtin_addc(d, (u32)(p2 >> 32), k1, &c1);
-        x = __builtin_addc(x, kin, k2, &c2);
-        t = x;
-        k1 = c1;
-        k2 = c2;
-        kt = K ? 1u : 0u;
-    }
-    const u32 c = k1 + k2;
-    u32 top = bcast(c, 63) + bcast(kt, 63);
-    top += resolve((u64)t + up1(c, l), l, &t);
-    if (geq(t, n, top))  // the product is < 2n
-        t = sub_n(t, n, l);
-    return t;
+    return mont_finish(t, c, n, l);
 }
 #else
+// The same product in plain C++ (A/B reference for the asm rows).
+template <int ROWS>
 __device__ u32 mont_mul(u32 a, u32 b, u32 n, u32 n0inv, u32 l)
 {
     u32 t = 0, c = 0;  // value = sum t_j 2^32j + sum c_j 2^32(j+1), c_j <= 3
-#pragma unroll SEC_BN_UNROLL
-    for (u32 i = 0; i < 64; ++i) {
+#pragma unroll 8
+    for (u32 i = 0; i < (u32)ROWS; ++i) {
         const u32 ai = bcast(a, i);
         const u64 p1 = (u64)ai * b + t;
         const u32 m = bcast((u32)p1, 0) * n0inv;
         const u64 p2 = (u64)m * n + (u32)p1;  // limb 0 of p2 is 0 mod 2^32
-        const u64 s = (u64)down1((u32)p2, l) + (p1 >> 32) + (p2 >> 32) + c;
+        const u64 s = (u64)down1((u32)p2) + (p1 >> 32) + (p2 >> 32) + c;
         t = (u32)s;
         c = (u32)(s >> 32);
     }
-    // resolve the redundant carries: limb j += c_{j-1}; c_63 is limb 64
-    u32 top = bcast(c, 63);
-    top += resolve((u64)t + up1(c, l), l, &t);
-    if (geq(t, n, top))  // the product is < 2n
-        t = sub_n(t, n, l);
-    return t;
+    return mont_finish(t, c, n, l);
 }
 #endif
 
-// (a + x) mod n for a < n and x < 2^2048 (so a + x < 3n: n has its top bit set)
+// (a + x) mod n for a < n and x < 2^bits (so a + x < 3n: n has its top bit set)
 __device__ u32 add_mod(u32 a, u32 x, u32 n, u32 l)
 {
     u32 t;
@@ -236,22 +206,35 @@ __device__ u32 add_mod(u32 a, u32 x, u32 n, u32 l)
     return t;
 }
 
+// One modulus as the kernels read it (lane l's limbs of sec::BnKey).
+struct Mod {
+    u32 n, r2, one, n0inv;
+};
+
+__device__ __forceinline__ Mod load_mod(const sec::BnKey *k, u32 l) { return Mod{k->n[l], k->r2[l], k->one[l], k->n0inv}; }
+
+template <int ROWS>
+__device__ __forceinline__ u32 mmul(const Mod &M, u32 a, u32 b, u32 l)
+{
+    return mont_mul<ROWS>(a, b, M.n, M.n0inv, l);
+}
+
 // 4-bit fixed-window exponentiation in Montgomery form; the exponent's nibbles come from
 // `nib(i)` for i = nnib-1 .. 0 (most significant first).  tab: 16 x 64 u32 of LDS.
 // Two mont_mul call sites only (table, then one loop for squarings and products): each
 // inlined product is ~1k instructions, so call sites are kept few for the I-cache.
-template <class Nib>
-__device__ u32 mont_pow(u32 base_m, u32 one_m, u32 n, u32 n0inv, u32 l, u32 nnib, Nib nib, u32 *tab)
+template <int ROWS, class Nib>
+__device__ u32 mont_pow(const Mod &M, u32 base_m, u32 l, u32 nnib, Nib nib, u32 *tab)
 {
-    tab[l] = one_m;
+    tab[l] = M.one;
     tab[64 + l] = base_m;
     u32 x = base_m;
 #pragma unroll 1
     for (u32 w = 2; w < 16; ++w) {
-        x = mont_mul(x, base_m, n, n0inv, l);
+        x = mmul<ROWS>(M, x, base_m, l);
         tab[w * 64 + l] = x;
     }
-    u32 i = nnib, r = one_m;
+    u32 i = nnib, r = M.one;
     while (i > 0) {  // leading zero nibbles cost nothing
         const u32 v = nib(--i);
         if (v) {
@@ -265,17 +248,47 @@ __device__ u32 mont_pow(u32 base_m, u32 one_m, u32 n, u32 n0inv, u32 l, u32 nnib
         const u32 ops = v ? 5u : 4u;  // 4 squarings, then the table product
 #pragma unroll 1
         for (u32 s = 0; s < ops; ++s)
-            r = mont_mul(r, s < 4 ? r : tab[v * 64 + l], n, n0inv, l);
+            r = mmul<ROWS>(M, r, s < 4 ? r : tab[v * 64 + l], l);
     }
     return r;
 }
 
-// limb j of a 256-byte big-endian integer
-__device__ __forceinline__ u32 load_be_limb(const u8 *be, u32 l)
+// Fixed-base power g^e from the comb table T[k][v] = g^(v * 256^k) (Montgomery form,
+// entry (k, v) at (k * 256 + v) * 64 u32): one product per nonzero exponent byte.
+// `byte(k)` = byte k of e counted from the least significant, k < nbytes <= 256.  The
+// next entry is loaded before the current product so its latency hides under it.
+template <class Byte>
+__device__ u32 fixed_pow(const Mod &M, const u32 *__restrict__ table, u32 nbytes, Byte byte, u32 l)
 {
-    const u8 *p = be + 252 - 4 * l;
+    u32 r = M.one;
+    bool started = false;
+    u32 v = nbytes ? byte(0) : 0u;
+    u32 e = v ? table[(u64)v * 64 + l] : 0u;
+#pragma unroll 1
+    for (u32 k = 0; k < nbytes; ++k) {
+        const u32 cv = v, ce = e;
+        if (k + 1 < nbytes) {
+            v = byte(k + 1);
+            e = v ? table[((u64)(k + 1) * 256 + v) * 64 + l] : 0u;
+        }
+        if (cv) {
+            r = started ? mmul<64>(M, r, ce, l) : ce;
+            started = true;
+        }
+    }
+    return r;
+}
+
+// limb l of an nbytes-long big-endian integer (nbytes a multiple of 4, <= 256)
+__device__ __forceinline__ u32 load_be(const u8 *be, u32 nbytes, u32 l)
+{
+    if (4 * l >= nbytes)
+        return 0u;
+    const u8 *p = be + nbytes - 4 - 4 * l;
     return (u32)p[0] << 24 | (u32)p[1] << 16 | (u32)p[2] << 8 | (u32)p[3];
 }
+
+__device__ __forceinline__ u32 load_be_limb(const u8 *be, u32 l) { return load_be(be, 256, l); }
 
 __device__ __forceinline__ void store_be_limb(u8 *be, u32 l, u32 v)
 {
@@ -285,6 +298,12 @@ __device__ __forceinline__ void store_be_limb(u8 *be, u32 l, u32 v)
     p[2] = (u8)(v >> 8);
     p[3] = (u8)v;
 }
+
+// byte k (from the least significant) of the integer held one limb per lane
+__device__ __forceinline__ u32 limb_byte(u32 x, u32 k) { return (bcast(x, k / 4) >> (8 * (k % 4))) & 0xFFu; }
+
+// nibble k (from the least significant) of the integer held one limb per lane
+__device__ __forceinline__ u32 limb_nib(u32 x, u32 k) { return (bcast(x, k / 8) >> (4 * (k % 8))) & 15u; }
 
 // limb j of the big-endian integer formed by bytes [start, start+len) of a message
 // whose bytes at or beyond `avail` read as zero (len <= 256)
@@ -303,7 +322,7 @@ __device__ __forceinline__ u32 chunk_limb(const u8 *p, uint64_t start, uint32_t 
 
 // int.from_bytes(msg, "big") mod n: Horner over 256-byte chunks from the most
 // significant, r <- r * 2^2048 + chunk  (r * 2^2048 = mont_mul(r, R^2)).
-__device__ u32 reduce_msg(const u8 *p, uint64_t len, uint64_t avail, u32 n, u32 r2, u32 n0inv, u32 l)
+__device__ u32 reduce_msg(const Mod &M, const u8 *p, uint64_t len, uint64_t avail, u32 l)
 {
     u32 r = 0;
     if (len == 0)
@@ -311,49 +330,130 @@ __device__ u32 reduce_msg(const u8 *p, uint64_t len, uint64_t avail, u32 n, u32 
     const uint64_t nch = (len + 255) / 256;
     const uint32_t first = (uint32_t)(len - 256 * (nch - 1));
     uint64_t off = 0;
+#pragma unroll 1
     for (uint64_t c = 0; c < nch; ++c) {
         const uint32_t clen = c == 0 ? first : 256u;
         const u32 x = chunk_limb(p, off, clen, avail, l);
         if (c > 0)
-            r = mont_mul(r, r2, n, n0inv, l);
-        r = add_mod(r, x, n, l);
+            r = mmul<64>(M, r, M.r2, l);
+        r = add_mod(r, x, M.n, l);
         off += clen;
     }
     return r;
 }
 
+// x (any value < 2^2048, plain) mod a 1024-bit half h, in h's Montgomery form:
+// (hi * 2^1024 + lo) mod h with hi * 2^1024 = mont_mul(hi, R_h^2), then * R_h.
+__device__ u32 to_half_m(const Mod &H, u32 x, u32 l)
+{
+    const u32 hi = high_half(x, l), lo = l < 32 ? x : 0u;
+    const u32 r = add_mod(mmul<32>(H, hi, H.r2, l), lo, H.n, l);
+    return mmul<32>(H, r, H.r2, l);
+}
+
+// CRT exponentiation: x^e mod n from (x mod p)^ep and (x mod q)^eq recombined as
+// tp * cp + tq * cq mod n (cp = q * (q^-1 mod p), cq = p * (p^-1 mod q), Montgomery form
+// mod n in the key).  x plain (< 2^2048); nib_p / nib_q: 4-bit digits of ep / eq.
+template <class NibP, class NibQ>
+__device__ u32 crt_pow(const sec::TagKey *__restrict__ tk, const Mod &N, u32 x, u32 nnib, NibP nib_p, NibQ nib_q,
+                       u32 *tab, u32 l)
+{
+    u32 acc = 0;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+        const Mod H = load_mod(h ? &tk->q : &tk->p, l);
+        const u32 xm = to_half_m(H, x, l);
+        const u32 rm = h ? mont_pow<32>(H, xm, l, nnib, nib_q, tab) : mont_pow<32>(H, xm, l, nnib, nib_p, tab);
+        const u32 t = mmul<32>(H, rm, l == 0 ? 1u : 0u, l);  // plain, < h
+        acc = add_mod(acc, mmul<64>(N, t, h ? tk->cq_m[l] : tk->cp_m[l], l), N.n, l);
+    }
+    return acc;
+}
+
 // ---- kernels (one 64-lane workgroup = one wave = one integer) ---------------------
 
-// BnKey from a big-endian modulus: R mod n = 2^2048 - n (n > 2^2047), R^2 mod n by
-// 2048 modular doublings.
-__global__ __launch_bounds__(64) void sec_bn_setup_kernel(const u8 *__restrict__ n_be, u32 n0inv, sec::BnKey *key)
+// BnKey from a big-endian modulus of `bits` (2048 or 1024, top bit set, odd):
+// R mod n = 2^bits - n, R^2 mod n by `bits` modular doublings.
+__global__ __launch_bounds__(64) void sec_bn_setup_kernel(const u8 *__restrict__ n_be, u32 n0inv, u32 bits,
+                                                          sec::BnKey *key)
 {
     const u32 l = lane_id();
-    const u32 n = load_be_limb(n_be, l);
+    const u32 n = load_be(n_be, bits / 8, l);
     u32 one;
-    {  // 0 - n mod 2^2048
+    {  // 0 - n mod 2^2048, then cut to 2^bits
         bool dummy;
         const u64 B = carry_in(ballot(0u < n), ballot(n == 0u), &dummy);
         one = 0u - n - (u32)((B >> l) & 1u);
+        if (32 * l >= bits)
+            one = 0;
     }
     u32 r2 = one;
-    for (int i = 0; i < 2048; ++i)
+    for (u32 i = 0; i < bits; ++i)
         r2 = add_mod(r2, r2, n, l);
     key->n[l] = n;
     key->one[l] = one;
     key->r2[l] = r2;
-    if (l == 0)
+    if (l == 0) {
         key->n0inv = n0inv;
+        key->bits = bits;
+    }
 }
 
+// generate_tag's constants: g, fdh in Montgomery form; d, dp, dq plain
 __global__ __launch_bounds__(64) void sec_tag_setup_kernel(const u8 *__restrict__ g_be, const u8 *__restrict__ fdh_be,
-                                                           const u8 *__restrict__ d_be, sec::TagKey *tk)
+                                                           const u8 *__restrict__ d_be, const u8 *__restrict__ dp_be,
+                                                           const u8 *__restrict__ dq_be, sec::TagKey *tk)
 {
     const u32 l = lane_id();
-    const u32 n = tk->k.n[l], r2 = tk->k.r2[l], n0inv = tk->k.n0inv;
-    tk->g_m[l] = mont_mul(load_be_limb(g_be, l), r2, n, n0inv, l);
-    tk->fdh_m[l] = mont_mul(load_be_limb(fdh_be, l), r2, n, n0inv, l);
+    const Mod N = load_mod(&tk->k, l);
+    tk->g_m[l] = mmul<64>(N, load_be_limb(g_be, l), N.r2, l);
+    tk->fdh_m[l] = mmul<64>(N, load_be_limb(fdh_be, l), N.r2, l);
     tk->d[l] = load_be_limb(d_be, l);
+    tk->dp[l] = dp_be ? load_be(dp_be, 128, l) : 0u;
+    tk->dq[l] = dq_be ? load_be(dq_be, 128, l) : 0u;
+}
+
+// CRT recombination constants cp, cq (plain big-endian mod n) into Montgomery form
+__global__ __launch_bounds__(64) void sec_crt_setup_kernel(const u8 *__restrict__ cp_be, const u8 *__restrict__ cq_be,
+                                                           sec::TagKey *tk)
+{
+    const u32 l = lane_id();
+    const Mod N = load_mod(&tk->k, l);
+    tk->cp_m[l] = mmul<64>(N, load_be_limb(cp_be, l), N.r2, l);
+    tk->cq_m[l] = mmul<64>(N, load_be_limb(cq_be, l), N.r2, l);
+}
+
+// Fixed-base table, step 1 (one wave): T[k][1] = g^(256^k) for k < 256 by 8 squarings per
+// step, and T[k][0] = 1.
+__global__ __launch_bounds__(64) void sec_gtab_base_kernel(const sec::TagKey *__restrict__ tk, u32 *table)
+{
+    const u32 l = lane_id();
+    const Mod N = load_mod(&tk->k, l);
+    u32 G = tk->g_m[l];
+#pragma unroll 1
+    for (u32 k = 0; k < 256; ++k) {
+        table[(k * 256 + 1) * 64 + l] = G;
+        table[(k * 256) * 64 + l] = N.one;
+        if (k + 1 < 256)
+#pragma unroll 1
+            for (int s = 0; s < 8; ++s)
+                G = mmul<64>(N, G, G, l);
+    }
+}
+
+// Fixed-base table, step 2 (one wave per k): T[k][v] = T[k][v-1] * T[k][1] for v < 256
+__global__ __launch_bounds__(64) void sec_gtab_fill_kernel(const sec::TagKey *__restrict__ tk, u32 *table)
+{
+    const u32 l = lane_id();
+    const u32 k = blockIdx.x;
+    const Mod N = load_mod(&tk->k, l);
+    const u32 G = table[(k * 256 + 1) * 64 + l];
+    u32 x = G;
+#pragma unroll 1
+    for (u32 v = 2; v < 256; ++v) {
+        x = mmul<64>(N, x, G, l);
+        table[(k * 256 + v) * 64 + l] = x;
+    }
 }
 
 __global__ __launch_bounds__(64) void sec_bn_reduce_kernel(const sec::BnKey *__restrict__ key, const u8 *base0,
@@ -364,11 +464,11 @@ __global__ __launch_bounds__(64) void sec_bn_reduce_kernel(const sec::BnKey *__r
         return;
     const u32 l = lane_id();
     const sec::MsgDesc m = msgs[i];
-    const u32 x = reduce_msg(base0 + m.off, m.len, m.avail, key->n[l], key->r2[l], key->n0inv, l);
+    const u32 x = reduce_msg(load_mod(key, l), base0 + m.off, m.len, m.avail, l);
     store_be_limb(out + (u64)i * 256, l, x);
 }
 
-// out_i = bases_i ^ exps_i mod n; bases < n (256 B big-endian), exps fixed-width big-endian
+// out_i = bases_i ^ exps_i mod n; bases < 2^2048 (256 B big-endian), exps fixed-width big-endian
 __global__ __launch_bounds__(64) void sec_bn_modexp_kernel(const sec::BnKey *__restrict__ key, const u8 *bases,
                                                            const u8 *exps, u32 exp_bytes, u32 count, u8 *out)
 {
@@ -377,15 +477,37 @@ __global__ __launch_bounds__(64) void sec_bn_modexp_kernel(const sec::BnKey *__r
     if (i >= count)
         return;
     const u32 l = lane_id();
-    const u32 n = key->n[l], n0inv = key->n0inv, one = key->one[l];
-    const u32 bm = mont_mul(load_be_limb(bases + (u64)i * 256, l), key->r2[l], n, n0inv, l);
+    const Mod N = load_mod(key, l);
+    const u32 bm = mmul<64>(N, load_be_limb(bases + (u64)i * 256, l), N.r2, l);
     const u8 *e = exps + (u64)i * exp_bytes;
     auto nib = [&](u32 k) -> u32 {  // nibble k counted from the least significant
         const u8 byte = e[exp_bytes - 1 - k / 2];
         return (k & 1) ? (u32)(byte >> 4) : (u32)(byte & 15);
     };
-    const u32 r = mont_pow(bm, one, n, n0inv, l, 2 * exp_bytes, nib, tab);
-    store_be_limb(out + (u64)i * 256, l, mont_mul(r, l == 0 ? 1u : 0u, n, n0inv, l));
+    const u32 r = mont_pow<64>(N, bm, l, 2 * exp_bytes, nib, tab);
+    store_be_limb(out + (u64)i * 256, l, mmul<64>(N, r, l == 0 ? 1u : 0u, l));
+}
+
+// CRT exponentiation with per-item exponents ep (mod p-1) and eq (mod q-1), exp_bytes each
+__global__ __launch_bounds__(64) void sec_bn_crt_modexp_kernel(const sec::TagKey *__restrict__ tk, const u8 *bases,
+                                                               const u8 *exps_p, const u8 *exps_q, u32 exp_bytes,
+                                                               u32 count, u8 *out)
+{
+    __shared__ u32 tab[16 * 64];
+    const u32 i = blockIdx.x;
+    if (i >= count)
+        return;
+    const u32 l = lane_id();
+    const Mod N = load_mod(&tk->k, l);
+    const u8 *ep = exps_p + (u64)i * exp_bytes, *eq = exps_q + (u64)i * exp_bytes;
+    auto nib_of = [exp_bytes](const u8 *e, u32 k) -> u32 {
+        const u8 byte = e[exp_bytes - 1 - k / 2];
+        return (k & 1) ? (u32)(byte >> 4) : (u32)(byte & 15);
+    };
+    const u32 r = crt_pow(
+        tk, N, load_be_limb(bases + (u64)i * 256, l), 2 * exp_bytes, [&](u32 k) { return nib_of(ep, k); },
+        [&](u32 k) { return nib_of(eq, k); }, tab, l);
+    store_be_limb(out + (u64)i * 256, l, r);
 }
 
 // out_i = a_i * b_i mod n: (a_i R) * b_i * R^-1
@@ -396,15 +518,30 @@ __global__ __launch_bounds__(64) void sec_bn_mulmod_kernel(const sec::BnKey *__r
     if (i >= count)
         return;
     const u32 l = lane_id();
-    const u32 n = key->n[l], n0inv = key->n0inv;
-    const u32 am = mont_mul(load_be_limb(a + (u64)i * 256, l), key->r2[l], n, n0inv, l);
-    store_be_limb(out + (u64)i * 256, l, mont_mul(load_be_limb(b + (u64)i * 256, l), am, n, n0inv, l));
+    const Mod N = load_mod(key, l);
+    const u32 am = mmul<64>(N, load_be_limb(a + (u64)i * 256, l), N.r2, l);
+    store_be_limb(out + (u64)i * 256, l, mmul<64>(N, load_be_limb(b + (u64)i * 256, l), am, l));
 }
 
-// APDP generate_tag for one piece: X = piece mod n; tag = (fdh * g^X)^d mod n.
-__global__ __launch_bounds__(64) void sec_apdp_tag_kernel(const sec::TagKey *__restrict__ tk, const u8 *base0,
-                                                          const sec::MsgDesc *__restrict__ msgs, u32 nmsgs,
-                                                          u8 *tags)
+// g^e mod n through the fixed-base table (issue_challenge's g_s = g^s); e: exp_bytes <= 256
+__global__ __launch_bounds__(64) void sec_apdp_gpow_kernel(const sec::TagKey *__restrict__ tk, const u32 *table,
+                                                           const u8 *exps, u32 exp_bytes, u32 count, u8 *out)
+{
+    const u32 i = blockIdx.x;
+    if (i >= count)
+        return;
+    const u32 l = lane_id();
+    const Mod N = load_mod(&tk->k, l);
+    const u8 *e = exps + (u64)i * exp_bytes;
+    const u32 r = fixed_pow(N, table, exp_bytes, [&](u32 k) -> u32 { return e[exp_bytes - 1 - k]; }, l);
+    store_be_limb(out + (u64)i * 256, l, mmul<64>(N, r, l == 0 ? 1u : 0u, l));
+}
+
+// APDP generate_tag for one piece: X = piece mod n; tag = (fdh * g^X)^d mod n, with g^X
+// from the fixed-base table and the d power by CRT when the key has p and q.
+__global__ __launch_bounds__(64) void sec_apdp_tag_kernel(const sec::TagKey *__restrict__ tk, const u32 *table,
+                                                          const u8 *base0, const sec::MsgDesc *__restrict__ msgs,
+                                                          u32 nmsgs, u8 *tags)
 {
     __shared__ u32 tab[16 * 64];
     const u32 i = blockIdx.x;
@@ -412,33 +549,45 @@ __global__ __launch_bounds__(64) void sec_apdp_tag_kernel(const sec::TagKey *__r
         return;
     const u32 l = lane_id();
     const sec::MsgDesc m = msgs[i];
-    const u32 n = tk->k.n[l], n0inv = tk->k.n0inv, one = tk->k.one[l];
-    const u32 X = reduce_msg(base0 + m.off, m.len, m.avail, n, tk->k.r2[l], n0inv, l);
-    // pass 0: t1 = g^X; pass 1: tag = (fdh * t1)^d  (one mont_pow instance for both)
-    u32 base = tk->g_m[l], e = X, r = 0;
-#pragma unroll 1
-    for (int pass = 0; pass < 2; ++pass) {
-        r = mont_pow(base, one, n, n0inv, l, 512,
-                     [&](u32 k) -> u32 { return (bcast(e, k / 8) >> (4 * (k % 8))) & 15u; }, tab);
-        base = mont_mul(tk->fdh_m[l], r, n, n0inv, l);
-        e = tk->d[l];
+    const Mod N = load_mod(&tk->k, l);
+    const u32 X = reduce_msg(N, base0 + m.off, m.len, m.avail, l);
+    const u32 gx = fixed_pow(N, table, 256, [&](u32 k) { return limb_byte(X, k); }, l);
+    const u32 base_m = mmul<64>(N, tk->fdh_m[l], gx, l);
+    u32 tag;
+    if (tk->crt) {
+        const u32 dp = tk->dp[l], dq = tk->dq[l];
+        tag = crt_pow(
+            tk, N, mmul<64>(N, base_m, l == 0 ? 1u : 0u, l), 256, [&](u32 k) { return limb_nib(dp, k); },
+            [&](u32 k) { return limb_nib(dq, k); }, tab, l);
+    } else {
+        const u32 d = tk->d[l];
+        const u32 r = mont_pow<64>(N, base_m, l, 512, [&](u32 k) { return limb_nib(d, k); }, tab);
+        tag = mmul<64>(N, r, l == 0 ? 1u : 0u, l);
     }
-    const u32 tag_m = r;
-    store_be_limb(tags + (u64)i * 256, l, mont_mul(tag_m, l == 0 ? 1u : 0u, n, n0inv, l));
+    store_be_limb(tags + (u64)i * 256, l, tag);
 }
 
 }  // namespace
 
-int sec_launch_bn_setup(const uint8_t *n_be, uint32_t n0inv, sec::BnKey *key, void *stream)
+int sec_launch_bn_setup(const uint8_t *n_be, uint32_t n0inv, uint32_t bits, sec::BnKey *key, void *stream)
 {
-    hipLaunchKernelGGL(sec_bn_setup_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, n_be, n0inv, key);
+    hipLaunchKernelGGL(sec_bn_setup_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, n_be, n0inv, bits, key);
     return hipGetLastError();
 }
 
-int sec_launch_tag_setup(const uint8_t *g_be, const uint8_t *fdh_be, const uint8_t *d_be, sec::TagKey *tk,
-                         void *stream)
+int sec_launch_tag_setup(const uint8_t *g_be, const uint8_t *fdh_be, const uint8_t *d_be, const uint8_t *dp_be,
+                         const uint8_t *dq_be, sec::TagKey *tk, uint32_t *table, void *stream)
 {
-    hipLaunchKernelGGL(sec_tag_setup_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, g_be, fdh_be, d_be, tk);
+    hipLaunchKernelGGL(sec_tag_setup_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, g_be, fdh_be, d_be, dp_be,
+                       dq_be, tk);
+    hipLaunchKernelGGL(sec_gtab_base_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, tk, table);
+    hipLaunchKernelGGL(sec_gtab_fill_kernel, dim3(256), dim3(64), 0, (hipStream_t)stream, tk, table);
+    return hipGetLastError();
+}
+
+int sec_launch_crt_setup(const uint8_t *cp_be, const uint8_t *cq_be, sec::TagKey *tk, void *stream)
+{
+    hipLaunchKernelGGL(sec_crt_setup_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, cp_be, cq_be, tk);
     return hipGetLastError();
 }
 
@@ -462,6 +611,16 @@ int sec_launch_bn_modexp(const sec::BnKey *key, const uint8_t *bases, const uint
     return hipGetLastError();
 }
 
+int sec_launch_bn_crt_modexp(const sec::TagKey *tk, const uint8_t *bases, const uint8_t *exps_p,
+                             const uint8_t *exps_q, uint32_t exp_bytes, uint32_t count, uint8_t *out, void *stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_bn_crt_modexp_kernel, dim3(count), dim3(64), 0, (hipStream_t)stream, tk, bases, exps_p,
+                       exps_q, exp_bytes, count, out);
+    return hipGetLastError();
+}
+
 int sec_launch_bn_mulmod(const sec::BnKey *key, const uint8_t *a, const uint8_t *b, uint32_t count, uint8_t *out,
                          void *stream)
 {
@@ -471,12 +630,22 @@ int sec_launch_bn_mulmod(const sec::BnKey *key, const uint8_t *a, const uint8_t 
     return hipGetLastError();
 }
 
-int sec_launch_apdp_tag(const sec::TagKey *tk, const uint8_t *base0, const sec::MsgDesc *msgs, uint32_t nmsgs,
-                        uint8_t *tags, void *stream)
+int sec_launch_apdp_gpow(const sec::TagKey *tk, const uint32_t *table, const uint8_t *exps, uint32_t exp_bytes,
+                         uint32_t count, uint8_t *out, void *stream)
+{
+    if (count == 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_apdp_gpow_kernel, dim3(count), dim3(64), 0, (hipStream_t)stream, tk, table, exps,
+                       exp_bytes, count, out);
+    return hipGetLastError();
+}
+
+int sec_launch_apdp_tag(const sec::TagKey *tk, const uint32_t *table, const uint8_t *base0, const sec::MsgDesc *msgs,
+                        uint32_t nmsgs, uint8_t *tags, void *stream)
 {
     if (nmsgs == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(sec_apdp_tag_kernel, dim3(nmsgs), dim3(64), 0, (hipStream_t)stream, tk, base0, msgs, nmsgs,
-                       tags);
+    hipLaunchKernelGGL(sec_apdp_tag_kernel, dim3(nmsgs), dim3(64), 0, (hipStream_t)stream, tk, table, base0, msgs,
+                       nmsgs, tags);
     return hipGetLastError();
 }

@@ -110,6 +110,53 @@ def test_tags_match_oracle(key, engine):
     assert k.tags(datas) == [apdp_ref.tag_value(n, g, d, prf_key, x) for x in datas]
 
 
+def test_crt_powmod_matches_pow(key, engine):
+    n, e, d, p, q = key
+    k = bn.ModKey(n, engine)
+    with pytest.raises(ECRuntimeError):
+        k.crt_powmod([5], [3])
+    k.set_crt(p, q)
+    rng = random.Random(12)
+    bases = [rng.randrange(R) for _ in range(30)] + [0, 1, n - 1, p, 2 * q, p * 7, R - 1]
+    exps = [rng.getrandbits(2048) for _ in range(30)] + [0, 5, 1, p - 1, (p - 1) * (q - 1), 3, 65537]
+    exps[:4] = [0, 1, p - 1, (p - 1) * 5]
+    assert k.crt_powmod(bases, exps) == [pow(b, x, n) for b, x in zip(bases, exps)]
+    # per-factor exponents directly: Fermat inverses
+    dens = [rng.randrange(2, n) for _ in range(10)]
+    inv = k.crt_powmod_pq(dens, [p - 2] * 10, [q - 2] * 10)
+    assert inv == [pow(x, -1, n) for x in dens]
+
+
+def test_crt_set_rejects_bad_factors(key, engine):
+    n, e, d, p, q = key
+    k = bn.ModKey(n, engine)
+    with pytest.raises(ValueError):
+        k.set_crt(p, q + 2)
+    import ctypes
+    bad = (p - 1).to_bytes(128, "big")  # even
+    z = b"\0" * 256
+    assert engine.lib.sec_bn_key_set_crt(engine._ctx, k._key, bad, q.to_bytes(128, "big"), z, z) == -13
+    assert engine.lib.sec_apdp_gpow_batch(engine._ctx, k._key, z, 1, 1, ctypes.c_void_p(1), 1) == -14
+    assert engine.lib.sec_bn_crt_modexp_batch(engine._ctx, k._key, z, z, z, 1, 1, ctypes.c_void_p(1), 1) == -15
+
+
+@pytest.mark.parametrize("crt", [False, True])
+def test_tags_and_gpow_fixed_base(key, engine, crt):
+    n, e, d, p, q = key
+    g = pow(1234567, 2, n)
+    prf_key = b"y" * 44
+    fdh = apdp_ref.full_domain_hash(n, apdp_ref.prf(prf_key, 0))
+    k = bn.ModKey(n, engine)
+    if crt:
+        k.set_crt(p, q)
+    k.set_tag(g, fdh, d)
+    rng = random.Random(21 + crt)
+    datas = [rng.randbytes(ln) for ln in (1, 2, 255, 256, 257, 3000, 65536)] + [b"\xff" * 256, b"\x00" * 300]
+    assert k.tags(datas) == [apdp_ref.tag_value(n, g, d, prf_key, x) for x in datas]
+    exps = [0, 1, 2, 255, 256, n - 1, R - 1] + [rng.randrange(n) for _ in range(20)] + [rng.getrandbits(40)]
+    assert k.gpow(exps) == [pow(g, x, n) for x in exps]
+
+
 def _system(key):
     n, e, d, p, q = key
     cs = apdp.ChallengeSystem()

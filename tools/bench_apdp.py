@@ -5,10 +5,14 @@ on one CPU core (oracle/apdp_ref.py, CPython pow — gmpy2 is absent from this i
     python tools/bench_apdp.py [--pieces 4096] [--piece-bytes 262144] > gpurun_out/apdp.json
 
 Cases (all with one RSA-2048 key, device-resident inputs unless noted):
-  reduce   piece mod n over `pieces` pieces        (GB/s of piece bytes)
-  modexp   base^e mod n, 2048-bit exponents        (modexps/s)
-  tag      generate_tag fused (reduce + 2 modexps) (tags/s, and piece GB/s)
+  reduce       piece mod n over `pieces` pieces                  (GB/s of piece bytes)
+  modexp       base^e mod n, 2048-bit exponents                  (modexps/s)
+  crt_modexp   the same powers by CRT over p, q (the key owner)  (modexps/s)
+  gpow         g^e from the fixed-base table (challenges' g^s)   (pows/s)
+  tag          generate_tag fused: reduce + table g^X + d power, without / with CRT (tags/s)
   proofs / verifies through storb_amd.apdp.ChallengeSystem from host memory (items/s)
+`mad_frac` = algorithmic 32x32->64 multiply-adds (8192 per 2048-bit Montgomery product)
+over the measured v_mad_u64_u32 ceiling.
 """
 
 from __future__ import annotations
@@ -24,6 +28,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+MAD_PEAK = 3.367e13  # measured v_mad_u64_u32 lane-ops/s per MI355X (tools/mad_ceiling.hip)
 
 
 def kernel_ms(eng, fn, reps):
@@ -62,8 +69,11 @@ def main():
     g = pow(7, 2, n)
     prf_key = b"bench-prf-key"
     fdh = apdp_ref.full_domain_hash(n, apdp_ref.prf(prf_key, 0))
-    mk = bn.ModKey(n, eng)
+    mk = bn.ModKey(n, eng)  # public key only: no CRT
     mk.set_tag(g, fdh, d)
+    mc = bn.ModKey(n, eng)  # key owner: CRT over p, q
+    mc.set_crt(p, q)
+    mc.set_tag(g, fdh, d)
     res = {"key_bits": 2048, "pieces": args.pieces, "piece_bytes": args.piece_bytes}
 
     P, L = args.pieces, args.piece_bytes
@@ -73,12 +83,12 @@ def main():
     msgs["len"] = L
     msgs["avail"] = L
     out = torch.empty(P * 256, dtype=torch.uint8, device="cuda")
+    host = src[:L].cpu().numpy().tobytes()
 
     ms, wall = kernel_ms(eng, lambda: mk.reduce_batch(msgs, out, asynchronous=True), 5)
     res["reduce"] = {"kernel_ms": round(ms, 3), "GBs": round(P * L / ms / 1e6, 1),
-                     "mont_mul_per_s": round(P * (L // 256) / ms * 1e3, 0)}
-    # spot check
-    host = src[:L].cpu().numpy().tobytes()
+                     "mont_mul_per_s": round(P * (L // 256) / ms * 1e3, 0),
+                     "mad_frac": round(P * (L // 256) * 8192 / ms * 1e3 / MAD_PEAK, 3)}
     assert bn.from_be(out[:256].cpu().numpy())[0] == int.from_bytes(host, "big") % n
 
     M = args.modexps
@@ -91,14 +101,29 @@ def main():
     b0 = int.from_bytes(bases[0].cpu().numpy().tobytes(), "big")
     e0 = int.from_bytes(exps[0].cpu().numpy().tobytes(), "big")
     assert bn.from_be(mo[:256].cpu().numpy())[0] == pow(b0, e0, n)
-    res["modexp_2048bit_exp"] = {"count": M, "kernel_ms": round(ms, 3),
-                                 "modexps_per_s": round(M / ms * 1e3, 0)}
+    mm = M * (2048 + 512 + 16)  # Montgomery products of a 4-bit-window 2048-bit power
+    res["modexp_2048bit_exp"] = {"count": M, "kernel_ms": round(ms, 3), "modexps_per_s": round(M / ms * 1e3, 0),
+                                 "mad_frac": round(mm * 8192 / ms * 1e3 / MAD_PEAK, 3)}
 
-    ms, wall = kernel_ms(eng, lambda: mk.tag_batch(msgs, out, asynchronous=True), 2)
-    t0 = bn.from_be(out[:256].cpu().numpy())[0]
-    assert t0 == apdp_ref.tag_value(n, g, d, prf_key, host)
-    res["tag_fused"] = {"kernel_ms": round(ms, 3), "tags_per_s": round(P / ms * 1e3, 1),
-                        "piece_GBs": round(P * L / ms / 1e6, 2)}
+    # the same powers by CRT (exponents reduced per factor on the host)
+    hexps = [int.from_bytes(exps[i].cpu().numpy().tobytes(), "big") for i in range(M)]
+    ep = torch.from_numpy(bn.to_be([bn.ModKey._half_exp(x, p - 1) for x in hexps], 128)).cuda()
+    eq = torch.from_numpy(bn.to_be([bn.ModKey._half_exp(x, q - 1) for x in hexps], 128)).cuda()
+    ms, wall = kernel_ms(eng, lambda: mc.crt_modexp_batch(bases, ep, eq, 128, M, mo, asynchronous=True), 3)
+    assert bn.from_be(mo[:256].cpu().numpy())[0] == pow(b0, e0, n)
+    res["crt_modexp_2048bit_exp"] = {"count": M, "kernel_ms": round(ms, 3), "modexps_per_s": round(M / ms * 1e3, 0)}
+
+    ms, wall = kernel_ms(eng, lambda: mc.gpow_batch(exps, 256, M, mo, asynchronous=True), 3)
+    assert bn.from_be(mo[:256].cpu().numpy())[0] == pow(g, e0, n)
+    res["gpow_fixed_base_2048bit_exp"] = {"count": M, "kernel_ms": round(ms, 3),
+                                          "pows_per_s": round(M / ms * 1e3, 0)}
+
+    expect_tag = apdp_ref.tag_value(n, g, d, prf_key, host)
+    for label, key in (("tag_fused", mk), ("tag_fused_crt", mc)):
+        ms, wall = kernel_ms(eng, lambda: key.tag_batch(msgs, out, asynchronous=True), 2)
+        assert bn.from_be(out[:256].cpu().numpy())[0] == expect_tag
+        res[label] = {"kernel_ms": round(ms, 3), "tags_per_s": round(P / ms * 1e3, 1),
+                      "piece_GBs": round(P * L / ms / 1e6, 2)}
 
     if args.quick:
         print(json.dumps(res))
@@ -112,7 +137,7 @@ def main():
     cpu_t = (time.perf_counter() - t_start) / cnt
     res["cpu_baseline_tag"] = {"tags_per_s": round(1 / cpu_t, 2), "cores": 1, "kind": "port",
                                "sample": f"{cnt} tags of {L} B pieces, CPython pow (gmpy2 absent)"}
-    res["tag_speedup_vs_cpu_core"] = round(res["tag_fused"]["tags_per_s"] * cpu_t, 1)
+    res["tag_speedup_vs_cpu_core"] = round(res["tag_fused_crt"]["tags_per_s"] * cpu_t, 1)
 
     # end-to-end through the drop-in API, host memory
     cs = apdp.ChallengeSystem()
