@@ -19,7 +19,9 @@ Also reported on the same line:
                 rocprofv3 PMC bytes per launch from profiles/ (FETCH_SIZE x2 + WRITE_SIZE,
                 gfx950 correction) when a matching summary is committed, else null
   cpu_baseline  oracle/fec_oracle.c (C restatement of zfec's fec.c: 64 KiB LUT, 8 KiB
-                strides), 1 thread, on a bounded sample of the same workload, rank 0 at N=1
+                strides) on a bounded sample of the same workload, rank 0 at N=1: one chunk
+                per task on min(16, usable cores) threads (`value`, `cores`), and 1 thread
+                (`single_thread_value`), --cpu-seconds each
   e2e           host-buffer encode+decode through the C ABI incl. pinned staging + PCIe
                 (reported beside `value`, never as it)
 """
@@ -52,7 +54,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     return ap.parse_args()
@@ -111,13 +113,14 @@ def load_traffic():
     return None
 
 
-def cpu_baseline(seconds: float) -> dict:
-    """oracle/fec_oracle.c, 1 thread: encode + decode ({1,3} erased) of 1 MiB chunks, RS(4,2)."""
+def _cpu_worker(seconds: float, seed: int) -> tuple[int, float]:
+    """One thread of the CPU baseline: encode + decode loops over its own buffers.  ctypes
+    drops the GIL inside the C calls, so threads run concurrently."""
     from oracle import cfec
 
     lib = cfec.lib()
     u8p = ctypes.POINTER(ctypes.c_uint8)
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(seed)
     nsample = 8
     chunks = [rng.integers(0, 256, CHUNK, dtype=np.uint8).tobytes() for _ in range(nsample)]
     B = CHUNK // K
@@ -125,14 +128,14 @@ def cpu_baseline(seconds: float) -> dict:
     out = (ctypes.c_uint8 * CHUNK)()
     keep = [s for s in range(M) if s not in ERASED]
     sn = (ctypes.c_int * K)(*keep)
+    base = ctypes.addressof(blocks)
+    ptrs = (ctypes.c_char_p * K)(*[ctypes.c_char_p(base + s * B) for s in keep])
     done = 0
     t0 = time.perf_counter()
     while True:
         c = chunks[done % nsample]
         if lib.fo_easy_encode(K, M, c, CHUNK, ctypes.cast(blocks, u8p)) != B:
             raise RuntimeError("oracle encode failed")
-        base = ctypes.addressof(blocks)
-        ptrs = (ctypes.c_char_p * K)(*[ctypes.c_char_p(base + s * B) for s in keep])
         if lib.fo_easy_decode(K, M, ptrs, sn, B, 0, ctypes.cast(out, u8p)):
             raise RuntimeError("oracle decode failed")
         if done == 0 and bytes(out) != c:
@@ -140,10 +143,40 @@ def cpu_baseline(seconds: float) -> dict:
         done += 1
         el = time.perf_counter() - t0
         if el >= seconds:
-            break
-    return {"value": round(2 * done * CHUNK / el / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"{done} x (encode + decode {{1,3}} erased) of 1 MiB RS(4,2) chunks, {nsample} distinct "
-                      f"chunks cycled, {el:.1f} s, oracle/fec_oracle.c (zfec fec.c restatement, 1 thread)"}
+            return done, el
+
+
+def cpu_threads() -> int:
+    """Threads for the multi-core baseline: the cores this process may use, at most 16 (the
+    GPU box's CPU share per GPU; os.cpu_count() there reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(seconds: float) -> dict:
+    """oracle/fec_oracle.c: encode + decode ({1,3} erased) of 1 MiB RS(4,2) chunks, one chunk
+    per task; `seconds` on 1 thread, then `seconds` on cpu_threads() threads."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import cfec
+
+    cfec.lib()  # build / load once before the threads start
+    d1, e1 = _cpu_worker(seconds, 0)
+    single = 2 * d1 * CHUNK / e1 / GIB
+    T = cpu_threads()
+    with ThreadPoolExecutor(T) as ex:
+        res = list(ex.map(lambda i: _cpu_worker(seconds, i), range(T)))
+    done = sum(d for d, _ in res)
+    el = max(e for _, e in res)
+    multi = 2 * done * CHUNK / el / GIB
+    return {"value": round(multi, 4), "unit": "GiB/s", "cores": T, "kind": "port",
+            "single_thread_value": round(single, 4),
+            "sample": f"{T} threads x {seconds:.0f} s of (encode + decode {{1,3}} erased) of 1 MiB RS(4,2) chunks "
+                      f"({done} chunks), one chunk per task; 1 thread: {d1} chunks in {e1:.1f} s; "
+                      f"oracle/fec_oracle.c (zfec fec.c restatement: 64 KiB LUT, 8 KiB strides)"}
 
 
 def main():
