@@ -137,8 +137,10 @@ struct SubPlan {
     size_t off_desc = 0, off_tiles = 0, off_tail = 0, off_soff = 0, off_srow = 0, off_mrow = 0;
     uint32_t ntail = 0;
     uint64_t in_bytes = 0, out_bytes = 0;  // dense slab sizes (host mode)
-    size_t off_msgs = 0;                   // SHA-1 messages of this unit
+    size_t off_msgs = 0;                   // messages of this unit (SHA-1, bignum)
     uint32_t nmsgs = 0;
+    size_t off_segs = 0, off_seginfo = 0;  // bignum: segments of the messages, per-message (first, count)
+    uint32_t nsegs = 0, max_seg = 0;       // segment count; most segments of one message
     uint64_t dig_first = 0;                // first digest slot of this unit
     uint64_t dig_off = 0;                  // host mode: digests' offset in the slab output
 };
@@ -289,6 +291,8 @@ struct sec_ctx {
     TableCache enc_tabs, dec_tabs;
     Plan enc_plan, dec_plan, sha_plan, bn_plan;
     DevBuf bn_scratch;  // host-mode staging of sec_bn_modexp / mulmod operands
+    DevBuf bn_part;     // partial residues of segmented reductions (one region per slot)
+    size_t bn_part_stride = 0;
     Slot slots[kSlots];
     std::unique_ptr<sec::CopyPool> pool;
 
@@ -798,9 +802,13 @@ int run_pipeline(sec_ctx *ctx, Plan &plan, Gather gather, Scatter scatter, Launc
 // descriptors are device-resident; out_per = output bytes per message.  Device
 // mode: one launch over caller addresses.  SEC_F_HOST: messages are staged
 // densely through pinned slabs (`slab` bytes) and the outputs copied back.
+// `launch_kernel(base0, plan, sp, sub_index, out, stream)` runs the kernel(s) over the
+// sub-plan's messages (descriptors device-resident at plan.meta + sp.off_msgs).
+// seg_bytes > 0 also splits each message into segments of seg_bytes counted from its end
+// (the least significant bytes of a big-endian integer) for the bignum reductions.
 template <class Launch>
 int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint8_t *out, size_t out_per,
-              unsigned flags, size_t slab, int kind, const char *what, Launch launch_kernel)
+              unsigned flags, size_t slab, int kind, const char *what, uint64_t seg_bytes, Launch launch_kernel)
 {
     if (!ctx || nmsgs < 0 || (nmsgs > 0 && (!msgs || !out)) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC)) ||
         nmsgs >= (int64_t)UINT32_MAX)
@@ -822,6 +830,7 @@ int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint
     }
     key.insert(key.end(), (const uint8_t *)&flags, (const uint8_t *)&flags + sizeof(unsigned));
     key.insert(key.end(), (const uint8_t *)&slab, (const uint8_t *)&slab + sizeof(size_t));
+    key.insert(key.end(), (const uint8_t *)&seg_bytes, (const uint8_t *)&seg_bytes + sizeof(uint64_t));
     if (!(plan.valid && plan.key == key)) {
         plan.valid = false;
         std::vector<std::pair<int64_t, int64_t>> ranges;
@@ -849,6 +858,20 @@ int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint
             sp.nmsgs = (uint32_t)md.size();
             sp.out_bytes = (uint64_t)md.size() * out_per;
             sp.off_msgs = img.put(md.data(), md.size() * sizeof(sec::MsgDesc));
+            if (seg_bytes) {
+                std::vector<sec::SegDesc> segs;
+                std::vector<sec::SegInfo> info;
+                for (int64_t i = c0; i < c1; ++i) {
+                    const uint64_t ns = std::max<uint64_t>(1, (msgs[i].len + seg_bytes - 1) / seg_bytes);
+                    info.push_back(sec::SegInfo{(uint32_t)segs.size(), (uint32_t)ns});
+                    for (uint64_t j = 0; j < ns; ++j)
+                        segs.push_back(sec::SegDesc{(uint32_t)(i - c0), (uint32_t)j});
+                    sp.max_seg = std::max<uint32_t>(sp.max_seg, (uint32_t)ns);
+                }
+                sp.nsegs = (uint32_t)segs.size();
+                sp.off_segs = img.put(segs.data(), segs.size() * sizeof(sec::SegDesc));
+                sp.off_seginfo = img.put(info.data(), info.size() * sizeof(sec::SegInfo));
+            }
             plan.subs.push_back(std::move(sp));
         }
         std::vector<PendingExpand> none;
@@ -860,8 +883,7 @@ int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint
         const SubPlan &sp = plan.subs[0];
         hipEvent_t t0;
         RC(timing_begin(ctx, &t0, ctx->stream()));
-        int e = launch_kernel((const uint8_t *)nullptr, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, out,
-                              ctx->stream());
+        int e = launch_kernel((const uint8_t *)nullptr, plan, sp, (size_t)0, out, ctx->stream());
         if (e)
             return hip_fail((hipError_t)e, what);
         RC(timing_end(ctx, t0, kind, ctx->stream()));
@@ -883,7 +905,7 @@ int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint
     auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
         hipEvent_t t0;
         RC(timing_begin(ctx, &t0, s));
-        int e = launch_kernel(din, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, dout, s);
+        int e = launch_kernel(din, plan, sp, (size_t)(&sp - plan.subs.data()), dout, s);
         if (e)
             return hip_fail((hipError_t)e, what);
         return timing_end(ctx, t0, kind, s);
@@ -1044,6 +1066,7 @@ void sec_ctx_destroy(sec_ctx *ctx)
     ctx->sha_plan.meta.release();
     ctx->bn_plan.meta.release();
     ctx->bn_scratch.release();
+    ctx->bn_part.release();
     if (ctx->own)
         (void)hipStreamDestroy(ctx->own);
     delete ctx;
@@ -1252,9 +1275,10 @@ int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *di
     if (!ctx)
         return SEC_EINVAL;
     return msg_batch(ctx, ctx->sha_plan, msgs, nmsgs, digests, 20, flags,
-                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 2, "sec_sha1_kernel",
-                     [](const uint8_t *base0, const sec::MsgDesc *md, uint32_t n, uint8_t *o, hipStream_t s) {
-                         return sec_launch_sha1(base0, nullptr, md, n, o, s);
+                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 2, "sec_sha1_kernel", 0,
+                     [](const uint8_t *base0, const Plan &plan, const SubPlan &sp, size_t, uint8_t *o, hipStream_t s) {
+                         return sec_launch_sha1(base0, nullptr, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, o,
+                                                s);
                      });
 }
 
@@ -1268,6 +1292,8 @@ struct sec_bn_key {
     DevBuf dk;     // TagKey, then 1 KiB of upload staging
     DevBuf table;  // fixed-base table of g (sec::kGTabWords u32), once set_tag ran
     bool has_tag = false, has_crt = false;
+    mutable DevBuf rpow;              // R^(j S) mod n (Montgomery form), j < rpow_count
+    mutable uint32_t rpow_count = 0;  // grown on demand by the segmented reductions
 };
 
 namespace {
@@ -1284,6 +1310,44 @@ uint32_t neg_inv32(const uint8_t *be, size_t nbytes)  // -n^-1 mod 2^32 from n's
 }
 
 bool odd_top(const uint8_t *be, size_t nbytes) { return (be[0] & 0x80) && (be[nbytes - 1] & 1); }
+
+// Segmented reductions: every message is cut into kSegBytes segments from its end, one
+// wave each (so a batch of few, large pieces still fills the chip); partial residues
+// r_j * R^(j S) go to ctx->bn_part, then one wave per message sums them.
+constexpr uint64_t kSegBytes = (uint64_t)sec::kSegChunks * 256;
+
+int bn_prepare(sec_ctx *ctx, const sec_bn_key *key, const Plan &plan, bool host)
+{
+    uint32_t need = 0;
+    size_t part = 0;
+    for (const SubPlan &sp : plan.subs) {
+        need = std::max(need, sp.max_seg);
+        part = std::max(part, (size_t)sp.nsegs * 256);
+    }
+    if (need > key->rpow_count) {  // grow R^(j S) to cover the longest message
+        const uint32_t cap = std::max<uint32_t>(need, 2 * key->rpow_count);
+        DevBuf grown;
+        RC(grown.ensure((size_t)cap * 256));
+        if (key->rpow_count)
+            CK(hipMemcpyAsync(grown.p, key->rpow.p, (size_t)key->rpow_count * 256, hipMemcpyDeviceToDevice,
+                              ctx->stream()));
+        int e = sec_launch_bn_rpow(key->dk.as<sec::BnKey>(), key->rpow_count, cap, grown.as<uint32_t>(), ctx->stream());
+        if (e)
+            return hip_fail((hipError_t)e, "sec_bn_rpow_kernel");
+        CK(hipStreamSynchronize(ctx->stream()));
+        key->rpow.release();
+        key->rpow = grown;
+        grown.p = nullptr;
+        key->rpow_count = cap;
+    }
+    ctx->bn_part_stride = part;
+    return ctx->bn_part.ensure(std::max<size_t>(part, 256) * (host ? kSlots : 1));
+}
+
+uint8_t *bn_part(sec_ctx *ctx, size_t sub_index, bool host)
+{
+    return ctx->bn_part.as<uint8_t>(host ? (sub_index % kSlots) * ctx->bn_part_stride : 0);
+}
 }  // namespace
 
 extern "C" {
@@ -1318,6 +1382,7 @@ void sec_bn_key_destroy(sec_bn_key *key)
     (void)hipSetDevice(key->device);
     key->dk.release();
     key->table.release();
+    key->rpow.release();
     delete key;
 }
 
@@ -1390,11 +1455,22 @@ int sec_bn_reduce_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs
 {
     if (!ctx || !key || key->device != ctx->device)
         return SEC_EINVAL;
+    const bool host = flags & SEC_F_HOST;
     const sec::BnKey *dk = key->dk.as<sec::BnKey>();
+    bool prepared = false;
     return msg_batch(ctx, ctx->bn_plan, msgs, nmsgs, out, 256, flags,
-                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 3, "sec_bn_reduce_kernel",
-                     [dk](const uint8_t *base0, const sec::MsgDesc *md, uint32_t n, uint8_t *o, hipStream_t s) {
-                         return sec_launch_bn_reduce(dk, base0, md, n, o, s);
+                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 3, "sec_bn_reduce", kSegBytes,
+                     [&](const uint8_t *base0, const Plan &plan, const SubPlan &sp, size_t idx, uint8_t *o,
+                         hipStream_t s) {
+                         if (!prepared) {
+                             RC(bn_prepare(ctx, key, plan, host));
+                             prepared = true;
+                         }
+                         return sec_launch_bn_reduce(dk, key->rpow.as<uint32_t>(), base0,
+                                                     plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs,
+                                                     plan.meta.as<sec::SegDesc>(sp.off_segs), sp.nsegs,
+                                                     plan.meta.as<sec::SegInfo>(sp.off_seginfo),
+                                                     bn_part(ctx, idx, host), o, s);
                      });
 }
 
@@ -1405,12 +1481,23 @@ int sec_apdp_tag_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs,
         return SEC_EINVAL;
     if (!key->has_tag)
         return SEC_ENOTAG;
+    const bool host = flags & SEC_F_HOST;
     const sec::TagKey *tk = key->dk.as<sec::TagKey>();
     const uint32_t *table = key->table.as<uint32_t>();
+    bool prepared = false;
     return msg_batch(ctx, ctx->bn_plan, msgs, nmsgs, tags, 256, flags,
-                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 3, "sec_apdp_tag_kernel",
-                     [tk, table](const uint8_t *base0, const sec::MsgDesc *md, uint32_t n, uint8_t *o, hipStream_t s) {
-                         return sec_launch_apdp_tag(tk, table, base0, md, n, o, s);
+                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 3, "sec_apdp_tag", kSegBytes,
+                     [&](const uint8_t *base0, const Plan &plan, const SubPlan &sp, size_t idx, uint8_t *o,
+                         hipStream_t s) {
+                         if (!prepared) {
+                             RC(bn_prepare(ctx, key, plan, host));
+                             prepared = true;
+                         }
+                         return sec_launch_apdp_tag(tk, table, key->rpow.as<uint32_t>(), base0,
+                                                    plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs,
+                                                    plan.meta.as<sec::SegDesc>(sp.off_segs), sp.nsegs,
+                                                    plan.meta.as<sec::SegInfo>(sp.off_seginfo),
+                                                    bn_part(ctx, idx, host), o, s);
                      });
 }
 

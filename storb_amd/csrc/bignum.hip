@@ -456,16 +456,61 @@ __global__ __launch_bounds__(64) void sec_gtab_fill_kernel(const sec::TagKey *__
     }
 }
 
-__global__ __launch_bounds__(64) void sec_bn_reduce_kernel(const sec::BnKey *__restrict__ key, const u8 *base0,
-                                                           const sec::MsgDesc *__restrict__ msgs, u32 nmsgs, u8 *out)
+// P_j = R^(j * S) mod n in Montgomery form: Q = (R in Montgomery form)^S, P_j = Q^j
+__global__ __launch_bounds__(64) void sec_bn_rpow_kernel(const sec::BnKey *__restrict__ key, u32 j0, u32 *P)
+{
+    __shared__ u32 tab[16 * 64];
+    const u32 l = lane_id();
+    const u32 j = j0 + blockIdx.x;
+    const Mod N = load_mod(key, l);
+    const u32 Q = mont_pow<64>(N, N.r2, l, 8, [](u32 k) { return (sec::kSegChunks >> (4 * k)) & 15u; }, tab);
+    P[(u64)j * 64 + l] = mont_pow<64>(N, Q, l, 8, [j](u32 k) { return (j >> (4 * k)) & 15u; }, tab);
+}
+
+// One segment of one message: its bytes as an integer mod n, times R^(j S) (its weight
+// in the message), plain limbs into partials.
+__global__ __launch_bounds__(64) void sec_bn_reduce_seg_kernel(const sec::BnKey *__restrict__ key,
+                                                               const u32 *__restrict__ P, const u8 *base0,
+                                                               const sec::MsgDesc *__restrict__ msgs,
+                                                               const sec::SegDesc *__restrict__ segs, u32 nsegs,
+                                                               u32 *partials)
+{
+    const u32 b = blockIdx.x;
+    if (b >= nsegs)
+        return;
+    const u32 l = lane_id();
+    const sec::SegDesc sd = segs[b];
+    const sec::MsgDesc m = msgs[sd.msg];
+    const Mod N = load_mod(key, l);
+    const u64 seg = (u64)sec::kSegChunks * 256;
+    const u64 end = m.len - (u64)sd.j * seg;
+    const u64 start = end > seg ? end - seg : 0;
+    const u64 avail = m.avail > start ? m.avail - start : 0;
+    u32 r = reduce_msg(N, base0 + m.off + start, end - start, avail, l);
+    if (sd.j)
+        r = mmul<64>(N, r, P[(u64)sd.j * 64 + l], l);
+    partials[(u64)b * 64 + l] = r;
+}
+
+// message value mod n = sum of its segments' partial residues
+__device__ __forceinline__ u32 combine(const Mod &N, const u32 *__restrict__ partials, sec::SegInfo si, u32 l)
+{
+    u32 acc = 0;
+#pragma unroll 1
+    for (u32 s = 0; s < si.count; ++s)
+        acc = add_mod(acc, partials[(u64)(si.first + s) * 64 + l], N.n, l);
+    return acc;
+}
+
+__global__ __launch_bounds__(64) void sec_bn_reduce_sum_kernel(const sec::BnKey *__restrict__ key,
+                                                               const sec::SegInfo *__restrict__ info, u32 nmsgs,
+                                                               const u32 *__restrict__ partials, u8 *out)
 {
     const u32 i = blockIdx.x;
     if (i >= nmsgs)
         return;
     const u32 l = lane_id();
-    const sec::MsgDesc m = msgs[i];
-    const u32 x = reduce_msg(load_mod(key, l), base0 + m.off, m.len, m.avail, l);
-    store_be_limb(out + (u64)i * 256, l, x);
+    store_be_limb(out + (u64)i * 256, l, combine(load_mod(key, l), partials, info[i], l));
 }
 
 // out_i = bases_i ^ exps_i mod n; bases < 2^2048 (256 B big-endian), exps fixed-width big-endian
@@ -537,20 +582,20 @@ __global__ __launch_bounds__(64) void sec_apdp_gpow_kernel(const sec::TagKey *__
     store_be_limb(out + (u64)i * 256, l, mmul<64>(N, r, l == 0 ? 1u : 0u, l));
 }
 
-// APDP generate_tag for one piece: X = piece mod n; tag = (fdh * g^X)^d mod n, with g^X
-// from the fixed-base table and the d power by CRT when the key has p and q.
+// APDP generate_tag for one piece: X = piece mod n (summed from its segments' residues);
+// tag = (fdh * g^X)^d mod n, with g^X from the fixed-base table and the d power by CRT
+// when the key has p and q.
 __global__ __launch_bounds__(64) void sec_apdp_tag_kernel(const sec::TagKey *__restrict__ tk, const u32 *table,
-                                                          const u8 *base0, const sec::MsgDesc *__restrict__ msgs,
-                                                          u32 nmsgs, u8 *tags)
+                                                          const sec::SegInfo *__restrict__ info, u32 nmsgs,
+                                                          const u32 *__restrict__ partials, u8 *tags)
 {
     __shared__ u32 tab[16 * 64];
     const u32 i = blockIdx.x;
     if (i >= nmsgs)
         return;
     const u32 l = lane_id();
-    const sec::MsgDesc m = msgs[i];
     const Mod N = load_mod(&tk->k, l);
-    const u32 X = reduce_msg(N, base0 + m.off, m.len, m.avail, l);
+    const u32 X = combine(N, partials, info[i], l);  // the piece mod n (segments reduced before)
     const u32 gx = fixed_pow(N, table, 256, [&](u32 k) { return limb_byte(X, k); }, l);
     const u32 base_m = mmul<64>(N, tk->fdh_m[l], gx, l);
     u32 tag;
@@ -591,13 +636,24 @@ int sec_launch_crt_setup(const uint8_t *cp_be, const uint8_t *cq_be, sec::TagKey
     return hipGetLastError();
 }
 
-int sec_launch_bn_reduce(const sec::BnKey *key, const uint8_t *base0, const sec::MsgDesc *msgs, uint32_t nmsgs,
-                         uint8_t *out, void *stream)
+int sec_launch_bn_rpow(const sec::BnKey *key, uint32_t j0, uint32_t j1, uint32_t *P, void *stream)
+{
+    if (j1 <= j0)
+        return hipSuccess;
+    hipLaunchKernelGGL(sec_bn_rpow_kernel, dim3(j1 - j0), dim3(64), 0, (hipStream_t)stream, key, j0, P);
+    return hipGetLastError();
+}
+
+int sec_launch_bn_reduce(const sec::BnKey *key, const uint32_t *P, const uint8_t *base0, const sec::MsgDesc *msgs,
+                         uint32_t nmsgs, const sec::SegDesc *segs, uint32_t nsegs, const sec::SegInfo *info,
+                         uint8_t *partials, uint8_t *out, void *stream)
 {
     if (nmsgs == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(sec_bn_reduce_kernel, dim3(nmsgs), dim3(64), 0, (hipStream_t)stream, key, base0, msgs, nmsgs,
-                       out);
+    hipLaunchKernelGGL(sec_bn_reduce_seg_kernel, dim3(nsegs), dim3(64), 0, (hipStream_t)stream, key, P, base0, msgs,
+                       segs, nsegs, (u32 *)partials);
+    hipLaunchKernelGGL(sec_bn_reduce_sum_kernel, dim3(nmsgs), dim3(64), 0, (hipStream_t)stream, key, info, nmsgs,
+                       (const u32 *)partials, out);
     return hipGetLastError();
 }
 
@@ -640,12 +696,15 @@ int sec_launch_apdp_gpow(const sec::TagKey *tk, const uint32_t *table, const uin
     return hipGetLastError();
 }
 
-int sec_launch_apdp_tag(const sec::TagKey *tk, const uint32_t *table, const uint8_t *base0, const sec::MsgDesc *msgs,
-                        uint32_t nmsgs, uint8_t *tags, void *stream)
+int sec_launch_apdp_tag(const sec::TagKey *tk, const uint32_t *table, const uint32_t *P, const uint8_t *base0,
+                        const sec::MsgDesc *msgs, uint32_t nmsgs, const sec::SegDesc *segs, uint32_t nsegs,
+                        const sec::SegInfo *info, uint8_t *partials, uint8_t *tags, void *stream)
 {
     if (nmsgs == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(sec_apdp_tag_kernel, dim3(nmsgs), dim3(64), 0, (hipStream_t)stream, tk, table, base0, msgs,
-                       nmsgs, tags);
+    hipLaunchKernelGGL(sec_bn_reduce_seg_kernel, dim3(nsegs), dim3(64), 0, (hipStream_t)stream, &tk->k, P, base0,
+                       msgs, segs, nsegs, (u32 *)partials);
+    hipLaunchKernelGGL(sec_apdp_tag_kernel, dim3(nmsgs), dim3(64), 0, (hipStream_t)stream, tk, table, info, nmsgs,
+                       (const u32 *)partials, tags);
     return hipGetLastError();
 }

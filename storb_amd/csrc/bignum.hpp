@@ -10,6 +10,17 @@ namespace sec {
 constexpr int kBnLimbs = 64;  // 2048 bits = one 32-bit limb per lane of a wave
 constexpr int kBnBytes = 256;
 constexpr size_t kGTabWords = (size_t)256 * 256 * kBnLimbs;  // fixed-base table: 256 bytes x 256 values
+constexpr uint32_t kSegChunks = 32;  // segmented reductions: 32 x 256 B = 8 KiB per wave
+
+// Segment j of message `msg`: bytes [len - (j+1) * 8 KiB, len - j * 8 KiB) (clipped at 0),
+// i.e. counted from the least significant end of the big-endian integer.
+struct SegDesc {
+    uint32_t msg, j;
+};
+// A message's segments are entries first .. first+count-1 of the segment list.
+struct SegInfo {
+    uint32_t first, count;
+};
 
 // Per-modulus Montgomery constants, limbs little-endian; derived on the device by
 // sec_bn_setup from n alone (R = 2^bits).  A 1024-bit CRT half keeps limbs 32..63 zero.
@@ -48,8 +59,13 @@ int sec_launch_bn_setup(const uint8_t *n_be, uint32_t n0inv, uint32_t bits, sec:
 int sec_launch_tag_setup(const uint8_t *g_be, const uint8_t *fdh_be, const uint8_t *d_be, const uint8_t *dp_be,
                          const uint8_t *dq_be, sec::TagKey *tk, uint32_t *table, void *stream);
 int sec_launch_crt_setup(const uint8_t *cp_be, const uint8_t *cq_be, sec::TagKey *tk, void *stream);
-int sec_launch_bn_reduce(const sec::BnKey *key, const uint8_t *base0, const sec::MsgDesc *msgs, uint32_t nmsgs,
-                         uint8_t *out, void *stream);
+// P_j = R^(j * kSegChunks) mod n in Montgomery form, for j in [j0, j1) (one wave each).
+int sec_launch_bn_rpow(const sec::BnKey *key, uint32_t j0, uint32_t j1, uint32_t *P, void *stream);
+// int.from_bytes(message, "big") mod n per message, 256 B big-endian each: one wave per
+// segment into `partials` (256 B per segment), then one wave per message sums them.
+int sec_launch_bn_reduce(const sec::BnKey *key, const uint32_t *P, const uint8_t *base0, const sec::MsgDesc *msgs,
+                         uint32_t nmsgs, const sec::SegDesc *segs, uint32_t nsegs, const sec::SegInfo *info,
+                         uint8_t *partials, uint8_t *out, void *stream);
 int sec_launch_bn_modexp(const sec::BnKey *key, const uint8_t *bases, const uint8_t *exps, uint32_t exp_bytes,
                          uint32_t count, uint8_t *out, void *stream);
 int sec_launch_bn_crt_modexp(const sec::TagKey *tk, const uint8_t *bases, const uint8_t *exps_p,
@@ -58,6 +74,7 @@ int sec_launch_bn_mulmod(const sec::BnKey *key, const uint8_t *a, const uint8_t 
                          void *stream);
 int sec_launch_apdp_gpow(const sec::TagKey *tk, const uint32_t *table, const uint8_t *exps, uint32_t exp_bytes,
                          uint32_t count, uint8_t *out, void *stream);
-int sec_launch_apdp_tag(const sec::TagKey *tk, const uint32_t *table, const uint8_t *base0, const sec::MsgDesc *msgs,
-                        uint32_t nmsgs, uint8_t *tags, void *stream);
+int sec_launch_apdp_tag(const sec::TagKey *tk, const uint32_t *table, const uint32_t *P, const uint8_t *base0,
+                        const sec::MsgDesc *msgs, uint32_t nmsgs, const sec::SegDesc *segs, uint32_t nsegs,
+                        const sec::SegInfo *info, uint8_t *partials, uint8_t *tags, void *stream);
 }
