@@ -164,6 +164,7 @@ template <int ROWS>
 __device__ __forceinline__ u32 mont_mul(u32 a, u32 b, u32 n, u32 n0inv, u32 l)
 {
     static_assert(ROWS == 64 || ROWS == 32, "RSA-2048 or a 1024-bit CRT half");
+    n0inv = __builtin_amdgcn_readfirstlane(n0inv);  // uniform by construction; SGPR for the asm
     u32 t;
     u64 k1, k2;
     if constexpr (ROWS == 64)
@@ -257,17 +258,20 @@ __device__ u32 mont_pow(const Mod &M, u32 base_m, u32 l, u32 nnib, Nib nib, u32 
 // entry (k, v) at (k * 256 + v) * 64 u32): one product per nonzero exponent byte.
 // `byte(k)` = byte k of e counted from the least significant, k < nbytes <= 256.  The
 // next entry is loaded before the current product so its latency hides under it.
+// k0 / k1: the byte range [k0, k1) this call multiplies (the whole exponent by default).
 template <class Byte>
-__device__ u32 fixed_pow(const Mod &M, const u32 *__restrict__ table, u32 nbytes, Byte byte, u32 l)
+__device__ u32 fixed_pow(const Mod &M, const u32 *__restrict__ table, u32 nbytes, Byte byte, u32 l, u32 k0 = 0,
+                         u32 k1 = ~0u)
 {
+    k1 = k1 < nbytes ? k1 : nbytes;
     u32 r = M.one;
     bool started = false;
-    u32 v = nbytes ? byte(0) : 0u;
-    u32 e = v ? table[(u64)v * 64 + l] : 0u;
+    u32 v = k0 < k1 ? byte(k0) : 0u;
+    u32 e = v ? table[((u64)k0 * 256 + v) * 64 + l] : 0u;
 #pragma unroll 1
-    for (u32 k = 0; k < nbytes; ++k) {
+    for (u32 k = k0; k < k1; ++k) {
         const u32 cv = v, ce = e;
-        if (k + 1 < nbytes) {
+        if (k + 1 < k1) {
             v = byte(k + 1);
             e = v ? table[((u64)(k + 1) * 256 + v) * 64 + l] : 0u;
         }
@@ -351,26 +355,21 @@ __device__ u32 to_half_m(const Mod &H, u32 x, u32 l)
     return mmul<32>(H, r, H.r2, l);
 }
 
-// CRT exponentiation: x^e mod n from (x mod p)^ep and (x mod q)^eq recombined as
-// tp * cp + tq * cq mod n (cp = q * (q^-1 mod p), cq = p * (p^-1 mod q), Montgomery form
-// mod n in the key).  x plain (< 2^2048); nib_p / nib_q: 4-bit digits of ep / eq.
-template <class NibP, class NibQ>
-__device__ u32 crt_pow(const sec::TagKey *__restrict__ tk, const Mod &N, u32 x, u32 nnib, NibP nib_p, NibQ nib_q,
-                       u32 *tab, u32 l)
+// CRT: x^e mod n from (x mod p)^ep and (x mod q)^eq recombined as tp * cp + tq * cq mod n
+// (cp = q * (q^-1 mod p), cq = p * (p^-1 mod q), Montgomery form mod n in the key).
+// One half (h = 0: p, 1: q): (x mod h)^e_h times its weight; x plain (< 2^2048), `nib`:
+// 4-bit digits of e_h.  The two halves' results add up to x^e mod n.
+template <class Nib>
+__device__ u32 crt_half(const sec::TagKey *__restrict__ tk, const Mod &N, u32 x, u32 h, u32 nnib, Nib nib, u32 *tab,
+                        u32 l)
 {
-    u32 acc = 0;
-#pragma unroll 1
-    for (int h = 0; h < 2; ++h) {
-        const Mod H = load_mod(h ? &tk->q : &tk->p, l);
-        const u32 xm = to_half_m(H, x, l);
-        const u32 rm = h ? mont_pow<32>(H, xm, l, nnib, nib_q, tab) : mont_pow<32>(H, xm, l, nnib, nib_p, tab);
-        const u32 t = mmul<32>(H, rm, l == 0 ? 1u : 0u, l);  // plain, < h
-        acc = add_mod(acc, mmul<64>(N, t, h ? tk->cq_m[l] : tk->cp_m[l], l), N.n, l);
-    }
-    return acc;
+    const Mod H = load_mod(h ? &tk->q : &tk->p, l);
+    const u32 rm = mont_pow<32>(H, to_half_m(H, x, l), l, nnib, nib, tab);
+    const u32 t = mmul<32>(H, rm, l == 0 ? 1u : 0u, l);  // plain, < h
+    return mmul<64>(N, t, h ? tk->cq_m[l] : tk->cp_m[l], l);
 }
 
-// ---- kernels (one 64-lane workgroup = one wave = one integer) ---------------------
+// ---- kernels (one wave per integer unless stated) ---------------------------------
 
 // BnKey from a big-endian modulus of `bits` (2048 or 1024, top bit set, odd):
 // R mod n = 2^bits - n, R^2 mod n by `bits` modular doublings.
@@ -533,26 +532,30 @@ __global__ __launch_bounds__(64) void sec_bn_modexp_kernel(const sec::BnKey *__r
     store_be_limb(out + (u64)i * 256, l, mmul<64>(N, r, l == 0 ? 1u : 0u, l));
 }
 
-// CRT exponentiation with per-item exponents ep (mod p-1) and eq (mod q-1), exp_bytes each
-__global__ __launch_bounds__(64) void sec_bn_crt_modexp_kernel(const sec::TagKey *__restrict__ tk, const u8 *bases,
-                                                               const u8 *exps_p, const u8 *exps_q, u32 exp_bytes,
-                                                               u32 count, u8 *out)
+// CRT exponentiation with per-item exponents ep (mod p-1) and eq (mod q-1), exp_bytes each.
+// Two waves per item: wave 0 the p half, wave 1 the q half, summed through LDS.
+__global__ __launch_bounds__(128) void sec_bn_crt_modexp_kernel(const sec::TagKey *__restrict__ tk, const u8 *bases,
+                                                                const u8 *exps_p, const u8 *exps_q, u32 exp_bytes,
+                                                                u32 count, u8 *out)
 {
-    __shared__ u32 tab[16 * 64];
+    __shared__ u32 tab[2][16 * 64];
+    __shared__ u32 part[64];
     const u32 i = blockIdx.x;
     if (i >= count)
         return;
-    const u32 l = lane_id();
+    const u32 l = lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);  // wave-uniform
     const Mod N = load_mod(&tk->k, l);
-    const u8 *ep = exps_p + (u64)i * exp_bytes, *eq = exps_q + (u64)i * exp_bytes;
-    auto nib_of = [exp_bytes](const u8 *e, u32 k) -> u32 {
+    const u8 *e = (w ? exps_q : exps_p) + (u64)i * exp_bytes;
+    auto nib = [&](u32 k) -> u32 {
         const u8 byte = e[exp_bytes - 1 - k / 2];
         return (k & 1) ? (u32)(byte >> 4) : (u32)(byte & 15);
     };
-    const u32 r = crt_pow(
-        tk, N, load_be_limb(bases + (u64)i * 256, l), 2 * exp_bytes, [&](u32 k) { return nib_of(ep, k); },
-        [&](u32 k) { return nib_of(eq, k); }, tab, l);
-    store_be_limb(out + (u64)i * 256, l, r);
+    const u32 y = crt_half(tk, N, load_be_limb(bases + (u64)i * 256, l), w, 2 * exp_bytes, nib, tab[w], l);
+    if (w)
+        part[l] = y;
+    __syncthreads();
+    if (!w)
+        store_be_limb(out + (u64)i * 256, l, add_mod(y, part[l], N.n, l));
 }
 
 // out_i = a_i * b_i mod n: (a_i R) * b_i * R^-1
@@ -583,33 +586,42 @@ __global__ __launch_bounds__(64) void sec_apdp_gpow_kernel(const sec::TagKey *__
 }
 
 // APDP generate_tag for one piece: X = piece mod n (summed from its segments' residues);
-// tag = (fdh * g^X)^d mod n, with g^X from the fixed-base table and the d power by CRT
-// when the key has p and q.
-__global__ __launch_bounds__(64) void sec_apdp_tag_kernel(const sec::TagKey *__restrict__ tk, const u32 *table,
-                                                          const sec::SegInfo *__restrict__ info, u32 nmsgs,
-                                                          const u32 *__restrict__ partials, u8 *tags)
+// tag = (fdh * g^X)^d mod n.  Two waves per piece: each multiplies half of g^X's
+// fixed-base table entries (combined through LDS), then with a CRT key each raises to d
+// mod one factor and the halves are summed through LDS; without CRT wave 0 does the d
+// power alone.
+__global__ __launch_bounds__(128) void sec_apdp_tag_kernel(const sec::TagKey *__restrict__ tk, const u32 *table,
+                                                           const sec::SegInfo *__restrict__ info, u32 nmsgs,
+                                                           const u32 *__restrict__ partials, u8 *tags)
 {
-    __shared__ u32 tab[16 * 64];
+    __shared__ u32 tab[2][16 * 64];
+    __shared__ u32 part[2][64];
     const u32 i = blockIdx.x;
     if (i >= nmsgs)
         return;
-    const u32 l = lane_id();
+    const u32 l = lane_id(), w = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);  // wave-uniform
     const Mod N = load_mod(&tk->k, l);
     const u32 X = combine(N, partials, info[i], l);  // the piece mod n (segments reduced before)
-    const u32 gx = fixed_pow(N, table, 256, [&](u32 k) { return limb_byte(X, k); }, l);
+    part[w][l] = fixed_pow(N, table, 256, [&](u32 k) { return limb_byte(X, k); }, l, 128 * w, 128 * w + 128);
+    __syncthreads();
+    const u32 gx = mmul<64>(N, part[0][l], part[1][l], l);
     const u32 base_m = mmul<64>(N, tk->fdh_m[l], gx, l);
-    u32 tag;
     if (tk->crt) {
-        const u32 dp = tk->dp[l], dq = tk->dq[l];
-        tag = crt_pow(
-            tk, N, mmul<64>(N, base_m, l == 0 ? 1u : 0u, l), 256, [&](u32 k) { return limb_nib(dp, k); },
-            [&](u32 k) { return limb_nib(dq, k); }, tab, l);
-    } else {
+        const u32 dh = w ? tk->dq[l] : tk->dp[l];
+        const u32 y = crt_half(
+            tk, N, mmul<64>(N, base_m, l == 0 ? 1u : 0u, l), w, 256, [&](u32 k) { return limb_nib(dh, k); }, tab[w],
+            l);
+        __syncthreads();  // both waves are done reading part[] for gx
+        if (w)
+            part[1][l] = y;
+        __syncthreads();
+        if (!w)
+            store_be_limb(tags + (u64)i * 256, l, add_mod(y, part[1][l], N.n, l));
+    } else if (!w) {
         const u32 d = tk->d[l];
-        const u32 r = mont_pow<64>(N, base_m, l, 512, [&](u32 k) { return limb_nib(d, k); }, tab);
-        tag = mmul<64>(N, r, l == 0 ? 1u : 0u, l);
+        const u32 r = mont_pow<64>(N, base_m, l, 512, [&](u32 k) { return limb_nib(d, k); }, tab[0]);
+        store_be_limb(tags + (u64)i * 256, l, mmul<64>(N, r, l == 0 ? 1u : 0u, l));
     }
-    store_be_limb(tags + (u64)i * 256, l, tag);
 }
 
 }  // namespace
@@ -672,7 +684,7 @@ int sec_launch_bn_crt_modexp(const sec::TagKey *tk, const uint8_t *bases, const 
 {
     if (count == 0)
         return hipSuccess;
-    hipLaunchKernelGGL(sec_bn_crt_modexp_kernel, dim3(count), dim3(64), 0, (hipStream_t)stream, tk, bases, exps_p,
+    hipLaunchKernelGGL(sec_bn_crt_modexp_kernel, dim3(count), dim3(128), 0, (hipStream_t)stream, tk, bases, exps_p,
                        exps_q, exp_bytes, count, out);
     return hipGetLastError();
 }
@@ -704,7 +716,7 @@ int sec_launch_apdp_tag(const sec::TagKey *tk, const uint32_t *table, const uint
         return hipSuccess;
     hipLaunchKernelGGL(sec_bn_reduce_seg_kernel, dim3(nsegs), dim3(64), 0, (hipStream_t)stream, &tk->k, P, base0,
                        msgs, segs, nsegs, (u32 *)partials);
-    hipLaunchKernelGGL(sec_apdp_tag_kernel, dim3(nmsgs), dim3(64), 0, (hipStream_t)stream, tk, table, info, nmsgs,
+    hipLaunchKernelGGL(sec_apdp_tag_kernel, dim3(nmsgs), dim3(128), 0, (hipStream_t)stream, tk, table, info, nmsgs,
                        (const u32 *)partials, tags);
     return hipGetLastError();
 }
