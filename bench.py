@@ -187,8 +187,10 @@ def main():
     from storb_amd.engine import Engine
 
     rank, local, world = D.rank_env()
+    # rehearsal overrides (several ranks on one GPU over gloo); the driver's runs set neither
+    local = int(os.environ.get("STORB_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
-    dmod = D.init()
+    dmod = D.init(os.environ.get("STORB_DIST_BACKEND") or None)
     eng = Engine(local)
 
     n, k, m = CHUNK, K, M
