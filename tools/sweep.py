@@ -26,6 +26,8 @@ VARIANTS = {
     "base": {},  # defaults: nontemporal loads + stores, prefetch
     "nopf": {"SEC_PREFETCH": 0},
     "tmp": {"SEC_NT_LOAD": 0, "SEC_NT_STORE": 0},  # temporal (cached) loads and stores
+    "decpipe": {"SEC_DEC_BATCH": 0},  # decode: one-slot-ahead pipeline only (before batching)
+    "decb8": {"SEC_DEC_BATCH": 8},  # default is 16: all slot loads up front for k * U <= 16
 }
 
 
