@@ -234,7 +234,38 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
         tail.push_back(sec::TailItem{chunk, (uint32_t)t});
 }
 
-void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile> &tiles)
+// XCD order.  Workgroup b of a launch is dispatched to XCD b % 8, so with the tiles in chunk
+// order the eight XCDs interleave over the same region.  In XCD order each XCD instead walks
+// one contiguous eighth of the group's tiles: tile(b) = start(b % 8) + b / 8 (bijective for
+// any count).  Measured (profiles/r01_sweep2_*.jsonl): decode with full 256-lane multi-step
+// tiles (C2/C3) +2.6 %; encode within noise; one-tile-per-chunk groups (C4) -4 to -6 %.
+// So decode uses it for groups of full tiles only.  SEC_XCD_ORDER (build knob, for A/B):
+// -1 = that rule, 0 = never, 1 = every group of both kernels.
+#ifndef SEC_XCD_ORDER
+#define SEC_XCD_ORDER -1
+#endif
+
+bool use_xcd_order(bool decode, const Group &g)
+{
+    if (SEC_XCD_ORDER >= 0)
+        return SEC_XCD_ORDER == 1;
+    return decode && g.lanes == sec::kLanes && g.U > 1;
+}
+
+void xcd_order(std::vector<sec::Tile> &t)
+{
+    const size_t n = t.size(), q = n / 8, r = n % 8;
+    if (n < 16)
+        return;
+    std::vector<sec::Tile> o(n);
+    for (size_t b = 0; b < n; ++b) {
+        const size_t x = b % 8;
+        o[b] = t[x * q + std::min(x, r) + b / 8];
+    }
+    t.swap(o);
+}
+
+void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile> &tiles, bool decode)
 {
     groups.clear();
     for (auto &kv : bins) {
@@ -242,7 +273,13 @@ void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile
             continue;
         groups.push_back(Group{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first),
                                (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
+        const size_t first = tiles.size();
         tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
+        if (use_xcd_order(decode, groups.back())) {
+            std::vector<sec::Tile> g(tiles.begin() + first, tiles.end());
+            xcd_order(g);
+            std::copy(g.begin(), g.end(), tiles.begin() + first);
+        }
     }
 }
 
@@ -295,6 +332,7 @@ struct sec_ctx {
     size_t bn_part_stride = 0;
     Slot slots[kSlots];
     std::unique_ptr<sec::CopyPool> pool;
+    int64_t zero_copy_calls = 0, staged_calls = 0;  // SEC_F_HOST calls by path (sec_ctx_host_paths)
 
     hipStream_t stream() const { return ext ? ext : own; }
     hipEvent_t ev()
@@ -555,7 +593,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
                 add_work(bins, tail, (uint32_t)(i - c0), B, valid, p);
         }
         std::vector<sec::Tile> tiles;
-        flatten(bins, sp.groups, tiles);
+        flatten(bins, sp.groups, tiles, false);
         sp.ntail = (uint32_t)tail.size();
         sp.nmsgs = (uint32_t)msgs.size();
         sp.dig_off = sp.out_bytes;  // host mode: digests follow the slab's parity
@@ -726,7 +764,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i]);
         }
         std::vector<sec::Tile> tiles;
-        flatten(bins, sp.groups, tiles);
+        flatten(bins, sp.groups, tiles, true);
         sp.ntail = (uint32_t)tail.size();
         sp.off_desc = img.put(descs.data(), descs.size() * sizeof(sec::DecDesc));
         sp.off_tiles = img.put(tiles.data(), tiles.size() * sizeof(sec::Tile));
@@ -1156,6 +1194,83 @@ int sec_decode_matrix(int k, int m, const int32_t *sharenums, uint8_t *out, int3
 
 namespace {
 
+// ---- pinned caller memory: the zero-copy host path ----------------------------
+// A SEC_F_HOST encode / decode whose caller buffers all lie in page-locked host memory the
+// HIP runtime maps at the same address on the device (hipHostMalloc / sec_host_alloc,
+// hipHostRegister / sec_host_register) skips the staging pipeline: the device-mode kernels
+// run straight on the host buffers and read / write them over PCIe, with no staging copy
+// and no DMA.  Measured on C2 (tools/e2e_study.py): encode 50.9 GiB/s and decode 41.2 GiB/s
+// against 33.4 / 17.5 staged, with the link's own H2D 53.6 and both-ways 45.2 GiB/s.
+// Pageable memory keeps the staged path.
+struct PinnedRange {
+    uintptr_t lo = 0, hi = 0;  // last allocation found: [lo, hi)
+};
+
+// True when [p, p + len) lies inside ONE pinned allocation whose device address equals its
+// host address.  `cache` remembers the last allocation so runs of blocks inside one buffer
+// cost one lookup.  A failed lookup's error is cleared so later launches do not report it.
+// (addresses arrive as base + offset integers: a NULL base with absolute offsets is legal in
+// this ABI, and pointer arithmetic on NULL would let the compiler fold the NULL test away)
+bool pinned(uintptr_t a, uint64_t len, PinnedRange *cache)
+{
+    const void *p = (const void *)a;
+    if (len == 0)
+        return true;
+    if (!a)
+        return false;
+    if (cache->hi && a >= cache->lo && a + len <= cache->hi)
+        return true;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (at.type != hipMemoryTypeHost || at.devicePointer != at.hostPointer || !at.devicePointer)
+        return false;
+    void *start = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const uintptr_t lo = (uintptr_t)start, hi = lo + size;
+    if (!size || a < lo || a + len > hi)
+        return false;
+    cache->lo = lo;
+    cache->hi = hi;
+    return true;
+}
+
+bool encode_pinned(const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in, const uint8_t *parity)
+{
+    PinnedRange ci, cp;
+    for (int64_t i = 0; i < nchunks; ++i) {
+        const sec_enc_chunk &c = chunks[i];
+        const uint64_t B = (c.n + (uint64_t)c.k - 1) / (uint64_t)c.k, p = (uint64_t)(c.m - c.k);
+        if (!pinned((uintptr_t)in + c.in_off, c.n, &ci))
+            return false;
+        if (p && B && !pinned((uintptr_t)parity + c.parity_off, (p - 1) * c.parity_stride + B, &cp))
+            return false;
+    }
+    return true;
+}
+
+bool decode_pinned(const sec_dec_chunk *chunks, int64_t nchunks, const uint64_t *block_offs, const uint8_t *blocks,
+                   const uint8_t *out)
+{
+    PinnedRange cb, co;
+    for (int64_t i = 0; i < nchunks; ++i) {
+        const sec_dec_chunk &c = chunks[i];
+        if (!pinned((uintptr_t)out + c.out_off, (uint64_t)c.k * c.B - c.padlen, &co))
+            return false;
+        for (int j = 0; j < c.k; ++j)
+            if (!pinned((uintptr_t)blocks + block_offs[c.slot0 + j], c.B, &cb))
+                return false;
+    }
+    return true;
+}
+
 // sec_encode_batch (digests == nullptr, digest == false) and sec_encode_digest_batch.
 int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in, uint8_t *parity,
                 uint8_t *digests, unsigned flags, bool digest)
@@ -1166,7 +1281,7 @@ int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, cons
         return SEC_OK;
     if (nchunks >= (int64_t)UINT32_MAX)
         return SEC_EINVAL;
-    const bool host = flags & SEC_F_HOST;
+    bool host = flags & SEC_F_HOST;
     RC(set_dev(ctx));
 
     // easyfec.Encoder.encode / _fec.Encoder preconditions
@@ -1190,6 +1305,16 @@ int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, cons
         return SEC_OK;  // nothing to compute (m == k, or empty chunks)
     if ((!in && !host && total_in) || (!parity && total_par) || (digest && !digests))
         return SEC_EINVAL;
+    // pinned caller buffers: run the device path on them directly (synchronous, as every
+    // host call).  Digest mode keeps the staged path: SHA-1 is one latency-bound lane per
+    // piece, which would stall on every PCIe read.
+    if (host && !digest && encode_pinned(chunks, nchunks, in, parity)) {
+        host = false;
+        flags &= ~(SEC_F_HOST | SEC_F_ASYNC);
+        ++ctx->zero_copy_calls;
+    } else if (host) {
+        ++ctx->staged_calls;
+    }
 
     // Plan key: the whole descriptor array for device mode; only the shapes for
     // host mode (its device layout is dense, caller addresses are used by the
@@ -1583,7 +1708,7 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         return SEC_OK;
     if (nchunks >= (int64_t)UINT32_MAX)
         return SEC_EINVAL;
-    const bool host = flags & SEC_F_HOST;
+    bool host = flags & SEC_F_HOST;
     RC(set_dev(ctx));
 
     // _fec.Decoder.decode / easyfec.Decoder.decode preconditions
@@ -1604,6 +1729,14 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         return SEC_OK;
     if (!out)  // blocks may be NULL: block_offs are then absolute addresses
         return SEC_EINVAL;
+    // pinned caller buffers: the device path on them directly (see encode_pinned)
+    if (host && decode_pinned(chunks, nchunks, block_offs, blocks, out)) {
+        host = false;
+        flags &= ~(SEC_F_HOST | SEC_F_ASYNC);
+        ++ctx->zero_copy_calls;
+    } else if (host) {
+        ++ctx->staged_calls;
+    }
 
     // Plan key (see sec_encode_batch): host mode keys on shapes + sharenums only.
     Plan &plan = ctx->dec_plan;
@@ -1703,11 +1836,37 @@ int sec_host_alloc(sec_ctx *ctx, size_t bytes, void **hptr)
     return SEC_OK;
 }
 
-int sec_host_free(sec_ctx *ctx, void *hptr)
+int sec_host_free(sec_ctx *ctx, void *hptr)  // ctx unused: may be NULL (or already destroyed)
 {
-    if (!ctx)
-        return SEC_EINVAL;
+    (void)ctx;
     CK(hipHostFree(hptr));
+    return SEC_OK;
+}
+
+int sec_host_register(sec_ctx *ctx, void *hptr, size_t bytes)
+{
+    if (!ctx || !hptr || !bytes)
+        return SEC_EINVAL;
+    RC(set_dev(ctx));
+    CK(hipHostRegister(hptr, bytes, hipHostRegisterDefault));
+    return SEC_OK;
+}
+
+int sec_host_unregister(sec_ctx *ctx, void *hptr)  // ctx unused: may be NULL
+{
+    (void)ctx;
+    if (!hptr)
+        return SEC_EINVAL;
+    CK(hipHostUnregister(hptr));
+    return SEC_OK;
+}
+
+int sec_ctx_host_paths(sec_ctx *ctx, int64_t *zero_copy, int64_t *staged)
+{
+    if (!ctx || !zero_copy || !staged)
+        return SEC_EINVAL;
+    *zero_copy = ctx->zero_copy_calls;
+    *staged = ctx->staged_calls;
     return SEC_OK;
 }
 

@@ -124,11 +124,22 @@ __device__ __forceinline__ void gf_mac(u32x4 (&acc)[R][U], const u32x4 (&x)[U], 
 //   SEC_DEC_BATCH               decode: when k * U <= this many 16-byte vectors per lane,
 //                               issue every slot's loads before any store or arithmetic
 //                               (C2 decode +4 %, RS(8,3) +6.6 %, C4 +2 %; r01 sweep_dec_batch)
+//   SEC_ENC_ST / SEC_DEC_ST     store cache policy of the encode / decode kernels:
+//                               0 plain, 1 nt, 2 "nt sc1" (write-through, line dropped from
+//                               L2), 3 "sc0 sc1".  The asm forms end in s_nop 1: a store of
+//                               more than 8 bytes reads its data VGPRs after issue, and the
+//                               compiler, blind to the asm, may overwrite them at once
 #ifndef SEC_NT_LOAD
 #define SEC_NT_LOAD 1
 #endif
 #ifndef SEC_NT_STORE
 #define SEC_NT_STORE 1
+#endif
+#ifndef SEC_ENC_ST
+#define SEC_ENC_ST SEC_NT_STORE
+#endif
+#ifndef SEC_DEC_ST
+#define SEC_DEC_ST SEC_NT_STORE
 #endif
 #ifndef SEC_DEC_BATCH
 #define SEC_DEC_BATCH 16
@@ -145,13 +156,17 @@ __device__ __forceinline__ u32x4 load16(const u8 *p)
     return *reinterpret_cast<const u32x4_u *>(p);
 #endif
 }
+template <int POL>
 __device__ __forceinline__ void store16(u8 *p, u32x4 v)
 {
-#if SEC_NT_STORE
-    __builtin_nontemporal_store(v, reinterpret_cast<u32x4_u *>(p));
-#else
-    *reinterpret_cast<u32x4_u *>(p) = v;
-#endif
+    if constexpr (POL == 0)
+        *reinterpret_cast<u32x4_u *>(p) = v;
+    else if constexpr (POL == 1)
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4_u *>(p));
+    else if constexpr (POL == 2)
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // GF(2^8) product of one byte through the same 5-dword table (tail kernels)
@@ -228,7 +243,7 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_encode_kernel(const u
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            store16(dst + (u64)r * d.par_stride + pos[u], acc[r][u]);
+            store16<SEC_ENC_ST>(dst + (u64)r * d.par_stride + pos[u], acc[r][u]);
 }
 
 // One thread per (chunk, position) in [valid, B) — or [0, B) for chunks with valid < 16:
@@ -314,7 +329,7 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_decode_kernel(const u
                     u8 *o = dst + (u64)orow * B;
 #pragma unroll
                     for (int u = 0; u < U; ++u)
-                        store16(o + pos[u], xs[c][u]);
+                        store16<SEC_DEC_ST>(o + pos[u], xs[c][u]);
                 }
                 if constexpr (R > 0)
                     gf_mac<R, U>(acc, xs[c], tj + c * tstep);
@@ -325,7 +340,7 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_decode_kernel(const u
                 u8 *o = dst + (u64)miss_row[d.slot0 + tl.r0 + r] * B;
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    store16(o + pos[u], acc[r][u]);
+                    store16<SEC_DEC_ST>(o + pos[u], acc[r][u]);
             }
         }
         return;
@@ -352,7 +367,7 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_decode_kernel(const u
             u8 *o = dst + (u64)orow * B;
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                store16(o + pos[u], x[u]);
+                store16<SEC_DEC_ST>(o + pos[u], x[u]);
         }
         if constexpr (R > 0)
             gf_mac<R, U>(acc, x, tj);
@@ -366,7 +381,7 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_decode_kernel(const u
             u8 *o = dst + (u64)miss_row[d.slot0 + tl.r0 + r] * B;
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                store16(o + pos[u], acc[r][u]);
+                store16<SEC_DEC_ST>(o + pos[u], acc[r][u]);
         }
     }
 }

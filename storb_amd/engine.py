@@ -17,6 +17,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -161,6 +162,48 @@ class Engine:
         flags = (SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0)
         self._check(self.lib.sec_sha1_batch(self._ctx, _ptr(msgs), len(msgs), g or None, flags))
 
+    # -- pinned host memory: the zero-copy host path ----------------------------
+    def host_empty(self, nbytes: int) -> np.ndarray:
+        """A page-locked uint8 host array (sec_host_alloc).  ``host=True`` calls whose buffers
+        are all pinned run the kernels on them directly over PCIe, with no staging copy.
+        Freed when the array and every view of it are gone."""
+        n = int(nbytes)
+        p = ctypes.c_void_p()
+        self._check(self.lib.sec_host_alloc(self._ctx, max(n, 1), ctypes.byref(p)))
+        raw = (ctypes.c_uint8 * max(n, 1)).from_address(p.value)
+        weakref.finalize(raw, self.lib.sec_host_free, None, p.value).atexit = False  # the OS reclaims at exit
+        return np.frombuffer(raw, dtype=np.uint8, count=n)
+
+    def register(self, buf) -> None:
+        """Page-lock an existing writable host buffer (hipHostRegister) so ``host=True`` calls
+        on it take the zero-copy path.  Call ``unregister`` before the buffer is freed."""
+        a, keep = addr(buf)
+        self._check(self.lib.sec_host_register(self._ctx, a, keep.nbytes if keep is not None else len(buf)))
+
+    def unregister(self, buf) -> None:
+        a, _ = addr(buf)
+        self._check(self.lib.sec_host_unregister(None, a))
+
+    def host_paths(self) -> tuple[int, int]:
+        """(zero-copy, staged) counts of the ``host=True`` encode / decode calls so far."""
+        z, st = ctypes.c_int64(0), ctypes.c_int64(0)
+        self._check(self.lib.sec_ctx_host_paths(self._ctx, ctypes.byref(z), ctypes.byref(st)))
+        return z.value, st.value
+
+    _SCRATCH_CAP = 256 << 20  # largest result staged in the reusable pinned scratch
+
+    def _out_buffer(self, nbytes: int) -> np.ndarray:
+        """Result buffer of encode_host / decode_host: a reusable pinned scratch (so a call on
+        pinned inputs stays zero-copy end to end; results are copied out before returning), or
+        plain memory past _SCRATCH_CAP."""
+        n = max(int(nbytes), 1)
+        if n > self._SCRATCH_CAP:
+            return np.empty(n, dtype=np.uint8)
+        cur = getattr(self, "_scratch", None)
+        if cur is None or cur.size < n:
+            cur = self._scratch = self.host_empty(max(n, 2 * (cur.size if cur is not None else 0), 1 << 20))
+        return cur[:n]
+
     # -- host batches ---------------------------------------------------------
     def sha1_host(self, datas) -> list[bytes]:
         """SHA-1 digests (20 bytes each) of host byte strings, hashed on the GPU."""
@@ -195,7 +238,7 @@ class Engine:
             descs[i] = (a, ln, total, max(B, 1), k, m)
             blocks.append((total, B, m - k))
             total += (m - k) * B
-        out = np.empty(max(total, 1), dtype=np.uint8)
+        out = self._out_buffer(total)
         if not digests:
             self.encode_batch(descs, 0, out, host=True)
             mv = memoryview(out)
@@ -237,7 +280,7 @@ class Engine:
             descs[i] = (total, B, padlen, slot, k, m)
             slot += k
             total += k * B - padlen
-        buf = np.empty(max(total, 1), dtype=np.uint8) if out is None else out
+        buf = self._out_buffer(total) if out is None else out
         self.decode_batch(descs, sn, bo, 0, buf, host=True)
         return bytes(memoryview(buf)[:total])
 

@@ -28,6 +28,14 @@ VARIANTS = {
     "tmp": {"SEC_NT_LOAD": 0, "SEC_NT_STORE": 0},  # temporal (cached) loads and stores
     "decpipe": {"SEC_DEC_BATCH": 0},  # decode: one-slot-ahead pipeline only (before batching)
     "decb8": {"SEC_DEC_BATCH": 8},  # default is 16: all slot loads up front for k * U <= 16
+    # store cache policy (kernels.hip SEC_ENC_ST / SEC_DEC_ST: 0 plain, 1 nt, 2 nt sc1, 3 sc0 sc1)
+    "dst2": {"SEC_DEC_ST": 2},
+    "dst0": {"SEC_DEC_ST": 0},
+    "est2": {"SEC_ENC_ST": 2},
+    "xcd": {"SEC_XCD_ORDER": 1},  # api.cpp: each XCD walks a contiguous eighth of the tiles
+    "noxcd": {"SEC_XCD_ORDER": 0},  # default (-1): XCD order for decode groups of full tiles only
+    "xcd_dst0": {"SEC_XCD_ORDER": 1, "SEC_DEC_ST": 0},
+    "xcd_dst2": {"SEC_XCD_ORDER": 1, "SEC_DEC_ST": 2},
 }
 
 
