@@ -126,7 +126,7 @@ size_t env_size(const char *name, size_t dflt)
 
 // ---- plan ---------------------------------------------------------------
 struct Group {
-    int rows, U, lanes;
+    int rows, U, lanes, wide;  // wide: k > kBatchVecs / U, blocks loaded in several batches
     uint32_t first, count;
 };
 
@@ -182,20 +182,25 @@ struct Image {
 
 // u-steps (4 KiB each) a lane covers per tile.  Larger U = more bytes in flight
 // per lane but more registers; SEC_TILE_U overrides (read per plan build).
-int pick_u(uint64_t B, int rows)
+// The kernels keep all k * U loads of a lane in one batch, so U > 1 only when
+// k * U <= kBatchVecs (wider k goes in U = 1 tiles, batched kBatchVecs blocks at a time).
+int pick_u(uint64_t B, int rows, int k)
 {
     const char *env = getenv("SEC_TILE_U");
     const int forced = env ? atoi(env) : 0;
+    int u = 1;
     if (forced == 1 || forced == 2 || forced == 4)
-        return forced;
-    if (B >= 4 * (uint64_t)sec::kStepBytes * 4 && rows <= 2)
-        return 4;
-    if (B >= 2 * (uint64_t)sec::kStepBytes * 4 && rows <= 4)
-        return 2;
-    return 1;
+        u = forced;
+    else if (B >= 4 * (uint64_t)sec::kStepBytes * 4 && rows <= 2)
+        u = 4;
+    else if (B >= 2 * (uint64_t)sec::kStepBytes * 4 && rows <= 4)
+        u = 2;
+    while (u > 1 && k * u > sec::kBatchVecs)
+        u /= 2;
+    return u;
 }
 
-using Bins = std::map<std::tuple<int, int, int>, std::vector<sec::Tile>>;  // (rows, U, lanes)
+using Bins = std::map<std::tuple<int, int, int, int>, std::vector<sec::Tile>>;  // (rows, U, lanes, wide)
 
 uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 
@@ -204,34 +209,45 @@ uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 // Tiles of 256 lanes x 4 KiB * U cover [0, valid); the ragged rest (and small chunks
 // entirely) get U = 1 tiles of up to 1024 lanes sized to what is left, so a 64 KiB
 // RS(10,4) chunk (6550 valid positions) is one 448-lane tile.  Lanes clamp to end at
-// `valid`.  Positions [valid, B) — or all of [0, B) when valid < 16 — become
-// one-thread tail items (at most padlen per normal chunk).
+// `valid`.  Positions [valid, B) (at most padlen for a normal chunk) are computed byte
+// by byte by the last tile of each row group (Tile::ntail): a separate one-thread-per-
+// byte launch cost C4 13-17 % on top of its main kernels (profiles/r01_c4_kernel_stats).
+// Chunks with valid < 16 get no tile: all of [0, B) becomes one-thread tail items.
 void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B, int64_t valid,
-              int rows_total)
+              int rows_total, int k)
 {
     if (B == 0)
         return;
     valid = std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)B));
     const uint64_t v = valid >= sec::kLaneBytes ? (uint64_t)valid : 0;
     const int ngroups = rows_total == 0 ? 1 : (rows_total + sec::kMaxRows - 1) / sec::kMaxRows;
-    if (v > 0)
-        for (int g = 0; g < ngroups; ++g) {
-            const int r0 = g * sec::kMaxRows;
-            const int rows = std::min(sec::kMaxRows, rows_total - r0);
-            const int U = pick_u(B, rows);
-            const uint64_t step = (uint64_t)sec::kStepBytes * U;
-            const uint64_t nfull = v > (uint64_t)sec::kLaneBytes * 1024 ? v / step : 0;
-            auto &full = bins[{rows, U, sec::kLanes}];
-            for (uint64_t i = 0; i < nfull; ++i)
-                full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
-            for (uint64_t t0 = nfull * step; t0 < v;) {
-                const uint64_t lanes = std::min<uint64_t>(1024, round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
-                bins[{rows, 1, (int)lanes}].push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
-                t0 += lanes * sec::kLaneBytes;
-            }
+    if (v == 0) {  // too small for a tile: every position is a tail item
+        for (uint64_t t = 0; t < B; ++t)
+            tail.push_back(sec::TailItem{chunk, (uint32_t)t});
+        return;
+    }
+    for (int g = 0; g < ngroups; ++g) {
+        const int r0 = g * sec::kMaxRows;
+        const int rows = std::min(sec::kMaxRows, rows_total - r0);
+        const int U = pick_u(B, rows, k);
+        const int wide = k * U > sec::kBatchVecs;  // U == 1 then (pick_u)
+        const uint64_t step = (uint64_t)sec::kStepBytes * U;
+        const uint64_t nfull = v > (uint64_t)sec::kLaneBytes * 1024 ? v / step : 0;
+        auto &full = bins[{rows, U, sec::kLanes, wide}];
+        sec::Tile *last = nullptr;
+        for (uint64_t i = 0; i < nfull; ++i) {
+            full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
+            last = &full.back();
         }
-    for (uint64_t t = v; t < B; ++t)
-        tail.push_back(sec::TailItem{chunk, (uint32_t)t});
+        for (uint64_t t0 = nfull * step; t0 < v;) {
+            const uint64_t lanes = std::min<uint64_t>(1024, round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
+            auto &bin = bins[{rows, 1, (int)lanes, k > sec::kBatchVecs}];
+            bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
+            last = &bin.back();
+            t0 += lanes * sec::kLaneBytes;
+        }
+        last->ntail = (uint32_t)(B - v);  // the ragged end [v, B) rides on the last tile
+    }
 }
 
 // XCD order.  Workgroup b of a launch is dispatched to XCD b % 8, so with the tiles in chunk
@@ -272,7 +288,7 @@ void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile
         if (kv.second.empty())
             continue;
         groups.push_back(Group{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first),
-                               (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
+                               std::get<3>(kv.first), (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
         const size_t first = tiles.size();
         tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
         if (use_xcd_order(decode, groups.back())) {
@@ -590,7 +606,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
             if (p > 0)
-                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p);
+                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k);
         }
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles, false);
@@ -617,7 +633,7 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
     for (const Group &g : sp.groups) {
-        int e = sec_launch_encode(g.rows, g.U, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
+        int e = sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
         if (e)
             return hip_fail((hipError_t)e, "sec_encode_kernel");
     }
@@ -761,7 +777,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             sp.in_bytes += (uint64_t)c.k * c.B;
             sp.out_bytes += nout;
             if (nout > 0)
-                add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i]);
+                add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k);
         }
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles, true);
@@ -788,7 +804,8 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const uint64_t *so = plan.meta.as<uint64_t>(sp.off_soff);
     const uint32_t *sr = plan.meta.as<uint32_t>(sp.off_srow), *mr = plan.meta.as<uint32_t>(sp.off_mrow);
     for (const Group &g : sp.groups) {
-        int e = sec_launch_decode(g.rows, g.U, g.lanes, blocks, out, dd, dt + g.first, g.count, tabs, so, sr, mr, s);
+        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, blocks, out, dd, dt + g.first, g.count, tabs, so, sr,
+                                  mr, s);
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_kernel");
     }

@@ -120,10 +120,10 @@ __device__ __forceinline__ void gf_mac(u32x4 (&acc)[R][U], const u32x4 (&x)[U], 
 //   SEC_NT_LOAD / SEC_NT_STORE  nontemporal (streaming) global loads / stores: every
 //                               byte is touched once, so keeping it out of the caches
 //                               measured +11% on encode, +4% on decode (r01 sweep)
-//   SEC_PREFETCH                issue block j+1's loads before block j's arithmetic
-//   SEC_DEC_BATCH               decode: when k * U <= this many 16-byte vectors per lane,
-//                               issue every slot's loads before any store or arithmetic
-//                               (C2 decode +4 %, RS(8,3) +6.6 %, C4 +2 %; r01 sweep_dec_batch)
+//   SEC_ENC_BATCH / SEC_DEC_BATCH  16-byte vectors per lane loaded as one batch (all
+//                               issued before any arithmetic): KB = this / U blocks (slots)
+//                               per batch.  Decode batching: C2 +4 %, RS(8,3) +6.6 %, C4 +2 %
+//                               (r01 sweep_dec_batch); encode: C2 +3.5 %, C4 +9 %
 //   SEC_ENC_ST / SEC_DEC_ST     store cache policy of the encode / decode kernels:
 //                               0 plain, 1 nt, 2 "nt sc1" (write-through, line dropped from
 //                               L2), 3 "sc0 sc1".  The asm forms end in s_nop 1: a store of
@@ -142,10 +142,10 @@ __device__ __forceinline__ void gf_mac(u32x4 (&acc)[R][U], const u32x4 (&x)[U], 
 #define SEC_DEC_ST SEC_NT_STORE
 #endif
 #ifndef SEC_DEC_BATCH
-#define SEC_DEC_BATCH 16
+#define SEC_DEC_BATCH sec::kBatchVecs
 #endif
-#ifndef SEC_PREFETCH
-#define SEC_PREFETCH 1
+#ifndef SEC_ENC_BATCH
+#define SEC_ENC_BATCH sec::kBatchVecs
 #endif
 
 __device__ __forceinline__ u32x4 load16(const u8 *p)
@@ -181,9 +181,16 @@ __device__ __forceinline__ u32 gf_mul_byte(const u32 *__restrict__ t, u32 x)
 // is < `valid` (all k blocks fully readable there, including the last, shorter data
 // block); a lane's 16 bytes are clamped to end at `valid`, so the last lane of a ragged
 // chunk overlaps its neighbour (identical bytes written twice) instead of taking a
-// byte-granular path.  Positions in [valid, B) — at most padlen of them — belong to
-// sec_encode_tail.
-template <int R, int U>
+// byte-granular path.  Positions in [valid, B) — at most padlen of them — are computed
+// byte by byte by the chunk's last tile (Tile::ntail, encode_ragged) after its main work.
+template <int R, int U, bool W>
+__device__ __forceinline__ void encode_main(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d,
+                                            const sec::Tile &tl, const u32 *__restrict__ tabs, u32 t);
+template <int R>
+__device__ __forceinline__ void encode_ragged(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d,
+                                           const sec::Tile &tl, const u32 *__restrict__ tabs);
+
+template <int R, int U, bool W>
 __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
                                                          const sec::EncDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
@@ -191,10 +198,18 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_encode_kernel(const u
 {
     const sec::Tile tl = tiles[blockIdx.x];
     const sec::EncDesc d = descs[tl.chunk];
-    const u32 B = d.B, k = d.k, valid = d.valid;
     const u32 t = tl.t0 + threadIdx.x * sec::kLaneBytes;
-    if (t >= valid)
-        return;
+    if (t < d.valid)
+        encode_main<R, U, W>(in, par, d, tl, tabs, t);
+    if (tl.ntail)
+        encode_ragged<R>(in, par, d, tl, tabs);
+}
+
+template <int R, int U, bool W>
+__device__ __forceinline__ void encode_main(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d,
+                                            const sec::Tile &tl, const u32 *__restrict__ tabs, u32 t)
+{
+    const u32 B = d.B, k = d.k, valid = d.valid;
     const u32 step = blockDim.x * sec::kLaneBytes;  // bytes one u-step of the workgroup covers
     u32 pos[U];
 #pragma unroll
@@ -212,33 +227,35 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_encode_kernel(const u
         for (int u = 0; u < U; ++u)
             acc[r][u] = u32x4{0u, 0u, 0u, 0u};
 
-#if SEC_PREFETCH
-    u32x4 x[U];
+    // Blocks go in batches of KB: every load of a batch is issued before any arithmetic and
+    // the batch is consumed in order (counted waits), so a lane keeps KB * U = SEC_ENC_BATCH
+    // loads in flight; C2 (k = 4) and C4 (k = 10) are one batch.  A one-block-ahead prefetch
+    // loop compiled to a full wait at its head (the next block's load included): one load in
+    // flight per lane and u-step, C2 -3.5 %, C4 -9 % (profiles/r01_sweep_enc_batch.jsonl).
+    constexpr int KB = SEC_ENC_BATCH / U > 0 ? SEC_ENC_BATCH / U : 1;
+    auto batch = [&](u32 j0) {
+        u32x4 xs[KB][U];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-        x[u] = load16(row + pos[u]);
-    for (u32 j = 0; j < k; ++j, tj += tstep) {
-        u32x4 xn[U];
-        row += B;
-        if (j + 1 < k) {
+        for (int c = 0; c < KB; ++c)
+            if (j0 + c < k) {
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                xn[u] = load16(row + pos[u]);
-        }
-        gf_mac<R, U>(acc, x, tj);
+                for (int u = 0; u < U; ++u)
+                    xs[c][u] = load16(row + (u64)(j0 + c) * B + pos[u]);
+            }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            x[u] = xn[u];
+        for (int c = 0; c < KB; ++c)
+            if (j0 + c < k)
+                gf_mac<R, U>(acc, xs[c], tj + (j0 + c) * tstep);
+    };
+    // W (wide k, U = 1 only): k > KB, several batches.  A separate instantiation: merely
+    // compiling this loop into the k <= KB kernel cost C4 15 % (registers; r01 sweep_wide).
+    if constexpr (W) {
+#pragma unroll 1
+        for (u32 j0 = 0; j0 < k; j0 += KB)
+            batch(j0);
+    } else {
+        batch(0);  // the plan guarantees k <= KB here
     }
-#else
-    for (u32 j = 0; j < k; ++j, tj += tstep, row += B) {
-        u32x4 x[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            x[u] = load16(row + pos[u]);
-        gf_mac<R, U>(acc, x, tj);
-    }
-#endif
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -246,7 +263,53 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_encode_kernel(const u
             store16<SEC_ENC_ST>(dst + (u64)r * d.par_stride + pos[u], acc[r][u]);
 }
 
-// One thread per (chunk, position) in [valid, B) — or [0, B) for chunks with valid < 16:
+// Lane of the workgroup that takes ragged position i first: the lanes past the tile's main
+// range (idle there) come first, then the wrap reaches the busy ones.
+__device__ __forceinline__ u32 ragged_lane0(u32 valid, u32 t0)
+{
+    const u32 used = min(blockDim.x, (valid - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes);
+    return (threadIdx.x + blockDim.x - used) % blockDim.x;
+}
+
+// The chunk's ragged end [valid, valid + ntail), byte by byte, for this tile's R parity rows:
+// blocks 0..k-2 are full there and block k-1 is zero padding, so it contributes nothing.
+// Each lane issues its bytes' loads kBatch at a time before using any (a loop of dependent
+// single-byte loads costs one memory latency per block).
+constexpr u32 kBatch = 16;
+
+template <int R>
+__device__ __forceinline__ void encode_ragged(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d,
+                                              const sec::Tile &tl, const u32 *__restrict__ tabs)
+{
+    const u8 *src = in + d.in_off;
+    const u32 nblk = d.k - 1;
+    for (u32 i = ragged_lane0(d.valid, tl.t0); i < tl.ntail; i += blockDim.x) {
+        const u32 tp = d.valid + i;
+        u32 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            acc[r] = 0;
+        for (u32 j0 = 0; j0 < nblk; j0 += kBatch) {
+            u32 x[kBatch];
+#pragma unroll
+            for (u32 q = 0; q < kBatch; ++q)
+                x[q] = j0 + q < nblk ? (u32)src[(u64)(j0 + q) * d.B + tp] : 0u;
+#pragma unroll
+            for (u32 q = 0; q < kBatch; ++q)
+                if (j0 + q < nblk) {
+                    const u32 *tj = tabs + d.tab + ((j0 + q) * d.p + tl.r0) * sec::kTabDwords;
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        acc[r] ^= gf_mul_byte(tj + r * sec::kTabDwords, x[q]);
+                }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            par[d.par_off + (u64)(tl.r0 + r) * d.par_stride + tp] = (u8)acc[r];
+    }
+}
+
+// One thread per (chunk, position) of the chunks too small for a tile (valid < 16):
 // all p parity bytes at that position, the last block's padding read as zero.
 __global__ __launch_bounds__(256) void sec_encode_tail(const u8 *__restrict__ in, u8 *__restrict__ par,
                                                        const sec::EncDesc *__restrict__ descs,
@@ -274,8 +337,19 @@ __global__ __launch_bounds__(256) void sec_encode_tail(const u8 *__restrict__ in
 // (zfec's normalisation).  Present primaries are copied to their output row;
 // the R missing rows of this tile's row group are XOR_c Minv[row][c] * slot_c.
 // Positions are < valid = the last output row's length, so every row is writable
-// and every slot (always B bytes) readable; the rest goes to sec_decode_tail.
-template <int R, int U>
+// and every slot (always B bytes) readable; the rest is decode_ragged's (Tile::ntail).
+template <int R, int U, bool W>
+__device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+                                            const sec::DecDesc &d, const sec::Tile &tl, u32 t,
+                                            const u32 *__restrict__ tabs, const u64 *__restrict__ slot_off,
+                                            const u32 *__restrict__ slot_row, const u32 *__restrict__ miss_row);
+template <int R>
+__device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::DecDesc &d,
+                                           const sec::Tile &tl, const u32 *__restrict__ tabs,
+                                           const u64 *__restrict__ slot_off, const u32 *__restrict__ slot_row,
+                                           const u32 *__restrict__ miss_row);
+
+template <int R, int U, bool W>
 __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                          const sec::DecDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
@@ -286,10 +360,64 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_decode_kernel(const u
 {
     const sec::Tile tl = tiles[blockIdx.x];
     const sec::DecDesc d = descs[tl.chunk];
-    const u32 B = d.B, k = d.k, valid = d.valid;
     const u32 t = tl.t0 + threadIdx.x * sec::kLaneBytes;
-    if (t >= valid)
-        return;
+    if (t < d.valid)
+        decode_main<R, U, W>(blocks, out, d, tl, t, tabs, slot_off, slot_row, miss_row);
+    if (tl.ntail)
+        decode_ragged<R>(blocks, out, d, tl, tabs, slot_off, slot_row, miss_row);
+}
+
+// The chunk's ragged end [valid, valid + ntail), byte by byte: the present primaries' bytes
+// (row group 0) and this tile's R recovered rows, wherever the output row still has bytes.
+// Every slot's byte is loaded once, kBatch slots at a time, and feeds the copy and all R rows.
+template <int R>
+__device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::DecDesc &d,
+                                              const sec::Tile &tl, const u32 *__restrict__ tabs,
+                                              const u64 *__restrict__ slot_off, const u32 *__restrict__ slot_row,
+                                              const u32 *__restrict__ miss_row)
+{
+    for (u32 i = ragged_lane0(d.valid, tl.t0); i < tl.ntail; i += blockDim.x) {
+        const u32 tp = d.valid + i;
+        u8 *dst = out + d.out_off + tp;
+        u32 acc[R > 0 ? R : 1];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            acc[r] = 0;
+        for (u32 c0 = 0; c0 < d.k; c0 += kBatch) {
+            u32 x[kBatch];
+#pragma unroll
+            for (u32 q = 0; q < kBatch; ++q)
+                x[q] = c0 + q < d.k ? (u32)blocks[slot_off[d.slot0 + c0 + q] + tp] : 0u;
+#pragma unroll
+            for (u32 q = 0; q < kBatch; ++q)
+                if (c0 + q < d.k) {
+                    const u32 c = c0 + q;
+                    const u32 orow = slot_row[d.slot0 + c];
+                    if (tl.r0 == 0 && orow != 0xFFFFFFFFu && (u64)orow * d.B + tp < d.n)
+                        dst[(u64)orow * d.B] = (u8)x[q];
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+                        acc[r] ^= gf_mul_byte(tabs + d.tab + (c * d.e + tl.r0 + r) * sec::kTabDwords, x[q]);
+                }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const u32 orow = miss_row[d.slot0 + tl.r0 + r];
+            if ((u64)orow * d.B + tp < d.n)
+                dst[(u64)orow * d.B] = (u8)acc[r];
+        }
+    }
+}
+
+template <int R, int U, bool W>
+__device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+                                            const sec::DecDesc &d, const sec::Tile &tl, u32 t,
+                                            const u32 *__restrict__ tabs,
+                                                         const u64 *__restrict__ slot_off,
+                                                         const u32 *__restrict__ slot_row,
+                                                         const u32 *__restrict__ miss_row)
+{
+    const u32 B = d.B, k = d.k, valid = d.valid;
     const u32 step = blockDim.x * sec::kLaneBytes;  // bytes one u-step of the workgroup covers
     u32 pos[U];
 #pragma unroll
@@ -307,24 +435,24 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_decode_kernel(const u
         for (int u = 0; u < U; ++u)
             acc[r][u] = u32x4{0u, 0u, 0u, 0u};
 
-#if SEC_DEC_BATCH
-    // k * U <= SEC_DEC_BATCH: issue every slot's loads before any store or arithmetic (more
-    // bytes in flight per lane than the one-slot-ahead pipeline below)
+    // Slots go in batches of KB, as in encode_main: every load of a batch before any store
+    // or arithmetic, then the batch in order — each present primary copied to its output
+    // row, every slot fed to the R accumulators.  C2 / C4 are one batch (all loads in flight).
     constexpr int KB = SEC_DEC_BATCH / U > 0 ? SEC_DEC_BATCH / U : 1;
-    if (k <= (u32)KB) {
+    auto batch = [&](u32 c0) {
         u32x4 xs[KB][U];
 #pragma unroll
         for (int c = 0; c < KB; ++c)
-            if (c < (int)k) {
-                const u8 *s = blocks + slot_off[d.slot0 + c];
+            if (c0 + c < k) {
+                const u8 *s = blocks + slot_off[d.slot0 + c0 + c];
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     xs[c][u] = load16(s + pos[u]);
             }
 #pragma unroll
         for (int c = 0; c < KB; ++c)
-            if (c < (int)k) {
-                const u32 orow = slot_row[d.slot0 + c];
+            if (c0 + c < k) {
+                const u32 orow = slot_row[d.slot0 + c0 + c];
                 if (copies && orow != 0xFFFFFFFFu) {
                     u8 *o = dst + (u64)orow * B;
 #pragma unroll
@@ -332,48 +460,15 @@ __global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_decode_kernel(const u
                         store16<SEC_DEC_ST>(o + pos[u], xs[c][u]);
                 }
                 if constexpr (R > 0)
-                    gf_mac<R, U>(acc, xs[c], tj + c * tstep);
+                    gf_mac<R, U>(acc, xs[c], tj + (c0 + c) * tstep);
             }
-        if constexpr (R > 0) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                u8 *o = dst + (u64)miss_row[d.slot0 + tl.r0 + r] * B;
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    store16<SEC_DEC_ST>(o + pos[u], acc[r][u]);
-            }
-        }
-        return;
-    }
-#endif
-    // every slot is read (R > 0) or copied (R == 0: all primaries present)
-    u32x4 x[U];
-    {
-        const u8 *s = blocks + slot_off[d.slot0];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            x[u] = load16(s + pos[u]);
-    }
-    for (u32 c = 0; c < k; ++c, tj += tstep) {
-        u32x4 xn[U];
-        if (c + 1 < k) {
-            const u8 *s = blocks + slot_off[d.slot0 + c + 1];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                xn[u] = load16(s + pos[u]);
-        }
-        const u32 orow = slot_row[d.slot0 + c];
-        if (copies && orow != 0xFFFFFFFFu) {
-            u8 *o = dst + (u64)orow * B;
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                store16<SEC_DEC_ST>(o + pos[u], x[u]);
-        }
-        if constexpr (R > 0)
-            gf_mac<R, U>(acc, x, tj);
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            x[u] = xn[u];
+    };
+    if constexpr (W) {  // wide k: several batches (see encode_main)
+#pragma unroll 1
+        for (u32 c0 = 0; c0 < k; c0 += KB)
+            batch(c0);
+    } else {
+        batch(0);  // the plan guarantees k <= KB here
     }
     if constexpr (R > 0) {
 #pragma unroll
@@ -534,54 +629,54 @@ __global__ __launch_bounds__(64) void sec_sha1_kernel(const u8 *__restrict__ bas
         out[q] = __builtin_bswap32(h[q]);
 }
 
-template <int R, int U>
+template <int R, int U, bool W>
 hipError_t launch_enc(const u8 *in, u8 *par, const sec::EncDesc *descs, const sec::Tile *tiles, u32 ntiles,
                       const u32 *tabs, u32 lanes, hipStream_t s)
 {
-    hipLaunchKernelGGL((sec_encode_kernel<R, U>), dim3(ntiles), dim3(lanes), 0, s, in, par, descs, tiles, tabs);
+    hipLaunchKernelGGL((sec_encode_kernel<R, U, W>), dim3(ntiles), dim3(lanes), 0, s, in, par, descs, tiles, tabs);
     return hipGetLastError();
 }
 
-template <int R, int U>
+template <int R, int U, bool W>
 hipError_t launch_dec(const u8 *blocks, u8 *out, const sec::DecDesc *descs, const sec::Tile *tiles, u32 ntiles,
                       const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, u32 lanes, hipStream_t s)
 {
-    hipLaunchKernelGGL((sec_decode_kernel<R, U>), dim3(ntiles), dim3(lanes), 0, s, blocks, out, descs, tiles, tabs,
+    hipLaunchKernelGGL((sec_decode_kernel<R, U, W>), dim3(ntiles), dim3(lanes), 0, s, blocks, out, descs, tiles, tabs,
                        so, sr, mr);
     return hipGetLastError();
 }
 
-template <int U>
+template <int U, bool W>
 hipError_t dispatch_enc(int rows, const u8 *in, u8 *par, const sec::EncDesc *d, const sec::Tile *t, u32 nt,
                         const u32 *tabs, u32 lanes, hipStream_t s)
 {
     switch (rows) {
-    case 1: return launch_enc<1, U>(in, par, d, t, nt, tabs, lanes, s);
-    case 2: return launch_enc<2, U>(in, par, d, t, nt, tabs, lanes, s);
-    case 3: return launch_enc<3, U>(in, par, d, t, nt, tabs, lanes, s);
-    case 4: return launch_enc<4, U>(in, par, d, t, nt, tabs, lanes, s);
-    case 5: return launch_enc<5, U>(in, par, d, t, nt, tabs, lanes, s);
-    case 6: return launch_enc<6, U>(in, par, d, t, nt, tabs, lanes, s);
-    case 7: return launch_enc<7, U>(in, par, d, t, nt, tabs, lanes, s);
-    case 8: return launch_enc<8, U>(in, par, d, t, nt, tabs, lanes, s);
+    case 1: return launch_enc<1, U, W>(in, par, d, t, nt, tabs, lanes, s);
+    case 2: return launch_enc<2, U, W>(in, par, d, t, nt, tabs, lanes, s);
+    case 3: return launch_enc<3, U, W>(in, par, d, t, nt, tabs, lanes, s);
+    case 4: return launch_enc<4, U, W>(in, par, d, t, nt, tabs, lanes, s);
+    case 5: return launch_enc<5, U, W>(in, par, d, t, nt, tabs, lanes, s);
+    case 6: return launch_enc<6, U, W>(in, par, d, t, nt, tabs, lanes, s);
+    case 7: return launch_enc<7, U, W>(in, par, d, t, nt, tabs, lanes, s);
+    case 8: return launch_enc<8, U, W>(in, par, d, t, nt, tabs, lanes, s);
     default: return hipErrorInvalidValue;
     }
 }
 
-template <int U>
+template <int U, bool W>
 hipError_t dispatch_dec(int rows, const u8 *b, u8 *o, const sec::DecDesc *d, const sec::Tile *t, u32 nt,
                         const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, u32 lanes, hipStream_t s)
 {
     switch (rows) {
-    case 0: return launch_dec<0, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 1: return launch_dec<1, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 2: return launch_dec<2, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 3: return launch_dec<3, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 4: return launch_dec<4, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 5: return launch_dec<5, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 6: return launch_dec<6, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 7: return launch_dec<7, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 8: return launch_dec<8, U>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 0: return launch_dec<0, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 1: return launch_dec<1, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 2: return launch_dec<2, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 3: return launch_dec<3, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 4: return launch_dec<4, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 5: return launch_dec<5, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 6: return launch_dec<6, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 7: return launch_dec<7, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 8: return launch_dec<8, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -597,18 +692,21 @@ int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void 
     return hipGetLastError();
 }
 
-int sec_launch_encode(int rows, int U, int lanes, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
-                      const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, void *stream)
+int sec_launch_encode(int rows, int U, int wide, int lanes, const uint8_t *in, uint8_t *par,
+                      const sec::EncDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
+                      void *stream)
 {
     if (ntiles == 0)
         return hipSuccess;
-    if (lanes < 64 || lanes % 64 || lanes > (U == 1 ? 1024 : sec::kLanes))
+    if (lanes < 64 || lanes % 64 || lanes > (U == 1 ? 1024 : sec::kLanes) || (wide && U != 1))
         return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
+    if (wide)
+        return dispatch_enc<1, true>(rows, in, par, descs, tiles, ntiles, tabs, (u32)lanes, s);
     switch (U) {
-    case 1: return dispatch_enc<1>(rows, in, par, descs, tiles, ntiles, tabs, (u32)lanes, s);
-    case 2: return dispatch_enc<2>(rows, in, par, descs, tiles, ntiles, tabs, (u32)lanes, s);
-    case 4: return dispatch_enc<4>(rows, in, par, descs, tiles, ntiles, tabs, (u32)lanes, s);
+    case 1: return dispatch_enc<1, false>(rows, in, par, descs, tiles, ntiles, tabs, (u32)lanes, s);
+    case 2: return dispatch_enc<2, false>(rows, in, par, descs, tiles, ntiles, tabs, (u32)lanes, s);
+    case 4: return dispatch_enc<4, false>(rows, in, par, descs, tiles, ntiles, tabs, (u32)lanes, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -623,20 +721,22 @@ int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *
     return hipGetLastError();
 }
 
-int sec_launch_decode(int rows, int U, int lanes, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
-                      const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, const uint64_t *slot_off,
-                      const uint32_t *slot_row, const uint32_t *miss_row, void *stream)
+int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,
+                      const sec::DecDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
+                      const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row, void *stream)
 {
     if (ntiles == 0)
         return hipSuccess;
-    if (lanes < 64 || lanes % 64 || lanes > (U == 1 ? 1024 : sec::kLanes))
+    if (lanes < 64 || lanes % 64 || lanes > (U == 1 ? 1024 : sec::kLanes) || (wide && U != 1))
         return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
     const u32 L = (u32)lanes;
+    if (wide)
+        return dispatch_dec<1, true>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
     switch (U) {
-    case 1: return dispatch_dec<1>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
-    case 2: return dispatch_dec<2>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
-    case 4: return dispatch_dec<4>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
+    case 1: return dispatch_dec<1, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
+    case 2: return dispatch_dec<2, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
+    case 4: return dispatch_dec<4, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -8,7 +8,9 @@
 // wave reads one coalesced 1 KiB run from each of the k input blocks and
 // writes one 1 KiB run per output row.  Tiles cover [0, valid) of a chunk
 // (valid = length of its last, possibly short, data block); the < padlen
-// positions in [valid, B) are "tail items", one thread each.
+// positions in [valid, B) are computed byte by byte by the chunk's last tile
+// (Tile::ntail).  Chunks too small for a tile (valid < 16) become "tail items",
+// one thread per position, in a separate launch.
 #pragma once
 #include <stdint.h>
 
@@ -19,6 +21,8 @@ constexpr int kLaneBytes = 16;      // bytes per lane per u-step (dwordx4)
 constexpr int kStepBytes = kLanes * kLaneBytes;  // 4 KiB per u-step
 constexpr int kMaxRows = 8;         // output rows per tile (accumulator groups)
 constexpr int kTabDwords = 5;       // v_perm tables per GF coefficient
+constexpr int kBatchVecs = 16;      // 16 B vectors a lane loads per batch (SEC_ENC/DEC_BATCH):
+                                    // a tile has U > 1 only if k * U <= kBatchVecs
 
 // One encode chunk, device copy (48 B).
 struct EncDesc {
@@ -49,7 +53,8 @@ struct Tile {
     uint32_t chunk;  // descriptor index
     uint32_t t0;     // first byte position within the block
     uint32_t r0;     // first output row of this tile's row group
-    uint32_t pad;
+    uint32_t ntail;  // on the chunk's last tile of the row group: B - valid, the ragged
+                     // positions [valid, B) it also computes byte by byte; else 0
 };
 
 // One byte position handled by the tail kernels.
@@ -74,12 +79,14 @@ struct MsgDesc {
 // launchers (kernels.hip); all enqueue on `stream` and return hipError_t as int
 extern "C++" {
 int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void *stream);
-int sec_launch_encode(int rows, int U, int lanes, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
-                      const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, void *stream);
+// wide: k > kBatchVecs / U (U must be 1): the kernels that load the blocks in several batches
+int sec_launch_encode(int rows, int U, int wide, int lanes, const uint8_t *in, uint8_t *par,
+                      const sec::EncDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
+                      void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
                            uint32_t nitems, const uint32_t *tabs, void *stream);
-int sec_launch_decode(int rows, int U, int lanes, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
-                      const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
+int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,
+                      const sec::DecDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
                       const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,
                       void *stream);
 int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDesc *msgs, uint32_t nmsgs,

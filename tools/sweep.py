@@ -23,17 +23,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 VARIANTS = {
-    "base": {},  # defaults: nontemporal loads + stores, prefetch
-    "nopf": {"SEC_PREFETCH": 0},
+    "base": {},  # defaults: nontemporal loads + stores, 16-vector load batches
     "tmp": {"SEC_NT_LOAD": 0, "SEC_NT_STORE": 0},  # temporal (cached) loads and stores
-    "decpipe": {"SEC_DEC_BATCH": 0},  # decode: one-slot-ahead pipeline only (before batching)
     "decb8": {"SEC_DEC_BATCH": 8},  # default is 16: all slot loads up front for k * U <= 16
     # store cache policy (kernels.hip SEC_ENC_ST / SEC_DEC_ST: 0 plain, 1 nt, 2 nt sc1, 3 sc0 sc1)
     "dst2": {"SEC_DEC_ST": 2},
     "dst0": {"SEC_DEC_ST": 0},
     "est2": {"SEC_ENC_ST": 2},
     "xcd": {"SEC_XCD_ORDER": 1},  # api.cpp: each XCD walks a contiguous eighth of the tiles
-    "noxcd": {"SEC_XCD_ORDER": 0},  # default (-1): XCD order for decode groups of full tiles only
+    "noxcd": {"SEC_XCD_ORDER": 0},
+    "eb4": {"SEC_ENC_BATCH": 4},
+    "nowide": {"SEC_WIDE_K": 0},  # A/B only: drops the k > 16 loop (register cost)  # encode: KB * U = 4 vectors per batch
+    "eb8": {"SEC_ENC_BATCH": 8},  # default (-1): XCD order for decode groups of full tiles only
     "xcd_dst0": {"SEC_XCD_ORDER": 1, "SEC_DEC_ST": 0},
     "xcd_dst2": {"SEC_XCD_ORDER": 1, "SEC_DEC_ST": 2},
 }
@@ -50,7 +51,7 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--variants", default="base,nopf,tmp")
+    ap.add_argument("--variants", default="base,tmp")
     ap.add_argument("--us", default="1,2,4")
     ap.add_argument("--workload", default="c2", help="c2 | c4 | nch,n,k,m (custom shape)")
     a = ap.parse_args()
