@@ -226,6 +226,10 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
             tail.push_back(sec::TailItem{chunk, (uint32_t)t});
         return;
     }
+    const bool ragged_kernel = env_size("SEC_RAGGED_KERNEL", 0) != 0;  // A/B: the old tail launch
+    if (ragged_kernel)
+        for (uint64_t t = v; t < B; ++t)
+            tail.push_back(sec::TailItem{chunk, (uint32_t)t});
     for (int g = 0; g < ngroups; ++g) {
         const int r0 = g * sec::kMaxRows;
         const int rows = std::min(sec::kMaxRows, rows_total - r0);
@@ -246,7 +250,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
             last = &bin.back();
             t0 += lanes * sec::kLaneBytes;
         }
-        last->ntail = (uint32_t)(B - v);  // the ragged end [v, B) rides on the last tile
+        last->ntail = ragged_kernel ? 0 : (uint32_t)(B - v);  // the ragged end [v, B) rides on the last tile
     }
 }
 

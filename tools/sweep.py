@@ -55,7 +55,9 @@ def main():
     ap.add_argument("--us", default="1,2,4")
     ap.add_argument("--workload", default="c2", help="c2 | c4 | nch,n,k,m (custom shape)")
     a = ap.parse_args()
-    tags = a.variants.split(",")
+    # a variant is TAG or TAG@ENV=VALUE: the TAG build, with ENV set while its plan is built
+    specs = a.variants.split(",")
+    tags = sorted({v.split("@")[0] for v in specs})
     libs = build(tags)
     if a.build:
         return
@@ -79,15 +81,20 @@ def main():
     enc_bytes = nch * (n + (m - k) * B)
     dec_bytes = nch * (k * B + n)
 
-    configs = [(t, int(u)) for t in tags for u in a.us.split(",")]
+    configs = [(v, int(u)) for v in specs for u in a.us.split(",")]
     engines = {}
-    for t, u in configs:
+    for v, u in configs:
+        t, _, env = v.partition("@")
         os.environ["SEC_TILE_U"] = str(u)
+        if env:
+            os.environ[env.split("=")[0]] = env.split("=")[1]
         e = Engine(0, lib_path=libs[t])
-        e.encode_batch(ed, src, par)  # builds + caches this engine's plan with U
+        e.encode_batch(ed, src, par)  # builds + caches this engine's plan with U (and env)
         e.decode_batch(dd, sn, offs, 0, out)
-        assert torch.equal(out, src), (t, u)
-        engines[(t, u)] = e
+        assert torch.equal(out, src), (v, u)
+        engines[(v, u)] = e
+        if env:
+            os.environ.pop(env.split("=")[0])
     os.environ.pop("SEC_TILE_U", None)
     samples = {c: ([], []) for c in configs}
     for _ in range(a.rounds):
