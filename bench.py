@@ -260,7 +260,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(enc_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(enc_gbs / PEAK_HBM_GBS, 4),
                          "traffic": traffic,
-                         "kernel": "sec_encode_kernel<2, 4>",
+                         "kernel": "sec_encode_kernel<2, 1, false>",
                          "algorithmic_bytes_per_launch": enc_alg,
                          "avg_launch_ms": round(enc_avg_s * 1e3, 4), "launches": enc_n},
             "decode_kernel": {"achieved": round(dec_alg / dec_avg_s / 1e9, 1), "unit": "GB/s",

@@ -180,21 +180,26 @@ struct Image {
     }
 };
 
+// lanes of a full tile (U = 1 only; U > 1 tiles are 256 lanes): SEC_FULL_LANES, for A/B
+int full_lanes() { return std::max(64, std::min(1024, (int)env_size("SEC_FULL_LANES", sec::kLanes))) / 64 * 64; }
+
 // u-steps (4 KiB each) a lane covers per tile.  Larger U = more bytes in flight
 // per lane but more registers; SEC_TILE_U overrides (read per plan build).
 // The kernels keep all k * U loads of a lane in one batch, so U > 1 only when
 // k * U <= kBatchVecs (wider k goes in U = 1 tiles, batched kBatchVecs blocks at a time).
+// (Full tiles are 256 lanes x 4 KiB x U; see add_work.)
 int pick_u(uint64_t B, int rows, int k)
 {
     const char *env = getenv("SEC_TILE_U");
     const int forced = env ? atoi(env) : 0;
+    // U = 1 by default: one 16 B vector per block per lane, 4 KiB per workgroup and block.
+    // Measured on C2 against U = 2 / 4: encode 6.48 vs 6.09 / 5.95 TB/s, decode 6.31 vs
+    // 5.79 / 5.62 (profiles/r01_sweep_u.jsonl); U > 1 only on request (SEC_TILE_U).
+    (void)B;
+    (void)rows;
     int u = 1;
     if (forced == 1 || forced == 2 || forced == 4)
         u = forced;
-    else if (B >= 4 * (uint64_t)sec::kStepBytes * 4 && rows <= 2)
-        u = 4;
-    else if (B >= 2 * (uint64_t)sec::kStepBytes * 4 && rows <= 4)
-        u = 2;
     while (u > 1 && k * u > sec::kBatchVecs)
         u /= 2;
     return u;
@@ -235,9 +240,10 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
         const int rows = std::min(sec::kMaxRows, rows_total - r0);
         const int U = pick_u(B, rows, k);
         const int wide = k * U > sec::kBatchVecs;  // U == 1 then (pick_u)
-        const uint64_t step = (uint64_t)sec::kStepBytes * U;
+        const int flanes = U == 1 ? full_lanes() : sec::kLanes;
+        const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * U;
         const uint64_t nfull = v > (uint64_t)sec::kLaneBytes * 1024 ? v / step : 0;
-        auto &full = bins[{rows, U, sec::kLanes, wide}];
+        auto &full = bins[{rows, U, flanes, wide}];
         sec::Tile *last = nullptr;
         for (uint64_t i = 0; i < nfull; ++i) {
             full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
@@ -258,8 +264,9 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
 // order the eight XCDs interleave over the same region.  In XCD order each XCD instead walks
 // one contiguous eighth of the group's tiles: tile(b) = start(b % 8) + b / 8 (bijective for
 // any count).  Measured (profiles/r01_sweep2_*.jsonl): decode with full 256-lane multi-step
-// tiles (C2/C3) +2.6 %; encode within noise; one-tile-per-chunk groups (C4) -4 to -6 %.
-// So decode uses it for groups of full tiles only.  SEC_XCD_ORDER (build knob, for A/B):
+// tiles (C2/C3, U = 4) +2.6 %; encode within noise; one-tile-per-chunk groups (C4) -4 to
+// -6 %; decode with the default U = 1 full tiles -3 % (profiles/r01_sweep_u1_knobs.jsonl).
+// So it applies to decode groups of full U > 1 tiles only (off by default).  SEC_XCD_ORDER (build knob, for A/B):
 // -1 = that rule, 0 = never, 1 = every group of both kernels.
 #ifndef SEC_XCD_ORDER
 #define SEC_XCD_ORDER -1
@@ -269,7 +276,7 @@ bool use_xcd_order(bool decode, const Group &g)
 {
     if (SEC_XCD_ORDER >= 0)
         return SEC_XCD_ORDER == 1;
-    return decode && g.lanes == sec::kLanes && g.U > 1;
+    return decode && g.U > 1 && g.lanes == sec::kLanes;
 }
 
 void xcd_order(std::vector<sec::Tile> &t)
@@ -887,7 +894,8 @@ int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint
     } else {
         key.assign((const uint8_t *)msgs, (const uint8_t *)(msgs + nmsgs));
     }
-    key.insert(key.end(), (const uint8_t *)&flags, (const uint8_t *)&flags + sizeof(unsigned));
+    const unsigned kflags = flags & ~SEC_F_ASYNC;  // ASYNC does not change the plan
+    key.insert(key.end(), (const uint8_t *)&kflags, (const uint8_t *)&kflags + sizeof(unsigned));
     key.insert(key.end(), (const uint8_t *)&slab, (const uint8_t *)&slab + sizeof(size_t));
     key.insert(key.end(), (const uint8_t *)&seg_bytes, (const uint8_t *)&seg_bytes + sizeof(uint64_t));
     if (!(plan.valid && plan.key == key)) {
@@ -1353,7 +1361,7 @@ int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, cons
         key.resize(sizeof(sec_enc_chunk) * (size_t)nchunks);
         memcpy(key.data(), chunks, sizeof(sec_enc_chunk) * (size_t)nchunks);
     }
-    const unsigned kflags = flags | (digest ? 0x10000u : 0u);
+    const unsigned kflags = (flags & ~SEC_F_ASYNC) | (digest ? 0x10000u : 0u);  // ASYNC does not change the plan
     key.insert(key.end(), (const uint8_t *)&kflags, (const uint8_t *)&kflags + sizeof(unsigned));
     if (!(plan.valid && plan.gen == ctx->enc_tabs.gen && plan.key == key)) {
         plan.valid = false;
@@ -1780,7 +1788,8 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         memcpy(key.data() + kc, sharenums, total_slots * 4);
         memcpy(key.data() + kc + total_slots * 4, block_offs, total_slots * 8);
     }
-    key.insert(key.end(), (const uint8_t *)&flags, (const uint8_t *)&flags + sizeof(unsigned));
+    const unsigned kflags = flags & ~SEC_F_ASYNC;  // ASYNC does not change the plan
+    key.insert(key.end(), (const uint8_t *)&kflags, (const uint8_t *)&kflags + sizeof(unsigned));
     const bool reuse = plan.valid && plan.gen == ctx->dec_tabs.gen && plan.key == key;
     DecLayout L;
     if (!reuse || host)

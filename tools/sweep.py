@@ -30,9 +30,12 @@ VARIANTS = {
     "dst2": {"SEC_DEC_ST": 2},
     "dst0": {"SEC_DEC_ST": 0},
     "est2": {"SEC_ENC_ST": 2},
-    "xcd": {"SEC_XCD_ORDER": 1},  # api.cpp: each XCD walks a contiguous eighth of the tiles
+    "xcd": {"SEC_XCD_ORDER": 1},  # api.cpp: XCD order for every group (default: decode full tiles)
     "noxcd": {"SEC_XCD_ORDER": 0},
     "eb4": {"SEC_ENC_BATCH": 4},
+    "db8": {"SEC_DEC_BATCH": 8},  # decode KB = 8 / U (valid only for k * U <= 8)
+    "db8eb8": {"SEC_DEC_BATCH": 8, "SEC_ENC_BATCH": 8},
+    "b4": {"SEC_DEC_BATCH": 4, "SEC_ENC_BATCH": 4},  # KB = 4 / U: valid for k * U <= 4 only
     "nowide": {"SEC_WIDE_K": 0},  # A/B only: drops the k > 16 loop (register cost)  # encode: KB * U = 4 vectors per batch
     "eb8": {"SEC_ENC_BATCH": 8},  # default (-1): XCD order for decode groups of full tiles only
     "xcd_dst0": {"SEC_XCD_ORDER": 1, "SEC_DEC_ST": 0},
@@ -89,8 +92,13 @@ def main():
         if env:
             os.environ[env.split("=")[0]] = env.split("=")[1]
         e = Engine(0, lib_path=libs[t])
-        e.encode_batch(ed, src, par)  # builds + caches this engine's plan with U (and env)
-        e.decode_batch(dd, sn, offs, 0, out)
+        # builds + caches this engine's plans with U (and env).  The flags are part of the
+        # plan key, so these calls must be asynchronous like the timed ones: a synchronous
+        # call here would leave the timed calls to rebuild their plan without the overrides.
+        out.zero_()
+        e.encode_batch(ed, src, par, asynchronous=True)
+        e.decode_batch(dd, sn, offs, 0, out, asynchronous=True)
+        e.sync()
         assert torch.equal(out, src), (v, u)
         engines[(v, u)] = e
         if env:
@@ -111,13 +119,27 @@ def main():
             samples[c][0].append(ms / nl)
             ms, nl = e.collect_timing("decode")
             samples[c][1].append(ms / nl)
+    # the timed calls must have produced the same bytes (a fast wrong kernel is not a result)
+    ref_par = par.clone()
+    engines[configs[0]].encode_batch(ed, src, ref_par, asynchronous=True)
+    engines[configs[0]].sync()
+    bad = set()
+    for c in configs:
+        out.zero_()
+        par.zero_()
+        engines[c].encode_batch(ed, src, par, asynchronous=True)
+        engines[c].decode_batch(dd, sn, offs, 0, out, asynchronous=True)
+        engines[c].sync()
+        if not (torch.equal(par, ref_par) and torch.equal(out, src)):
+            bad.add(c)
     for c in configs:
         enc, dec = np.array(samples[c][0]), np.array(samples[c][1])
         print(json.dumps({"variant": c[0], "U": c[1], "workload": a.workload,
                           "enc_ms_med": round(float(np.median(enc)), 4), "enc_GBs": round(enc_bytes / np.median(enc) / 1e6, 1),
                           "enc_GBs_best": round(enc_bytes / enc.min() / 1e6, 1),
                           "dec_ms_med": round(float(np.median(dec)), 4), "dec_GBs": round(dec_bytes / np.median(dec) / 1e6, 1),
-                          "dec_GBs_best": round(dec_bytes / dec.min() / 1e6, 1)}), flush=True)
+                          "dec_GBs_best": round(dec_bytes / dec.min() / 1e6, 1),
+                          "verified": c not in bad}), flush=True)
 
 
 if __name__ == "__main__":
