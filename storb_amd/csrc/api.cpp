@@ -180,7 +180,7 @@ struct Image {
     }
 };
 
-// lanes of a full tile (U = 1 only; U > 1 tiles are 256 lanes): SEC_FULL_LANES, for A/B
+// lanes of every U = 1 tile (U > 1 tiles are 256 lanes); SEC_FULL_LANES overrides, for A/B
 int full_lanes() { return std::max(64, std::min(1024, (int)env_size("SEC_FULL_LANES", sec::kLanes))) / 64 * 64; }
 
 // u-steps (4 KiB each) a lane covers per tile.  Larger U = more bytes in flight
@@ -232,6 +232,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
         return;
     }
     const bool ragged_kernel = env_size("SEC_RAGGED_KERNEL", 0) != 0;  // A/B: the old tail launch
+    const bool exact = env_size("SEC_EXACT_LANES", 0) != 0;              // A/B: chunk-sized tiles
     if (ragged_kernel)
         for (uint64_t t = v; t < B; ++t)
             tail.push_back(sec::TailItem{chunk, (uint32_t)t});
@@ -242,19 +243,38 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
         const int wide = k * U > sec::kBatchVecs;  // U == 1 then (pick_u)
         const int flanes = U == 1 ? full_lanes() : sec::kLanes;
         const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * U;
-        const uint64_t nfull = v > (uint64_t)sec::kLaneBytes * 1024 ? v / step : 0;
         auto &full = bins[{rows, U, flanes, wide}];
         sec::Tile *last = nullptr;
-        for (uint64_t i = 0; i < nfull; ++i) {
-            full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
-            last = &full.back();
-        }
-        for (uint64_t t0 = nfull * step; t0 < v;) {
-            const uint64_t lanes = std::min<uint64_t>(1024, round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
-            auto &bin = bins[{rows, 1, (int)lanes, k > sec::kBatchVecs}];
-            bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
-            last = &bin.back();
-            t0 += lanes * sec::kLaneBytes;
+        if (!exact) {
+            // every U = 1 tile is flanes wide, the chunk's last one with idle lanes past
+            // `valid`: one launch per (rows, wide) class however mixed the chunk sizes are
+            const uint64_t nfull = U == 1 ? (v + step - 1) / step : v / step;
+            for (uint64_t i = 0; i < nfull; ++i) {
+                full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
+                last = &full.back();
+            }
+            const int ul = full_lanes();
+            auto &ones = bins[{rows, 1, ul, k > sec::kBatchVecs}];
+            for (uint64_t t0 = nfull * step; t0 < v; t0 += (uint64_t)sec::kLaneBytes * ul) {  // U > 1 remainder
+                ones.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
+                last = &ones.back();
+            }
+        } else {
+            // A/B (SEC_EXACT_LANES): partial tiles sized to what is left of the chunk, up to
+            // 1024 lanes — a separate launch per distinct width
+            const uint64_t nfull = v > (uint64_t)sec::kLaneBytes * 1024 ? v / step : 0;
+            for (uint64_t i = 0; i < nfull; ++i) {
+                full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
+                last = &full.back();
+            }
+            for (uint64_t t0 = nfull * step; t0 < v;) {
+                const uint64_t lanes =
+                    std::min<uint64_t>(1024, round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
+                auto &bin = bins[{rows, 1, (int)lanes, k > sec::kBatchVecs}];
+                bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
+                last = &bin.back();
+                t0 += lanes * sec::kLaneBytes;
+            }
         }
         last->ntail = ragged_kernel ? 0 : (uint32_t)(B - v);  // the ragged end [v, B) rides on the last tile
     }

@@ -12,7 +12,8 @@ C2/C3  1024 x 1 MiB RS(4,2) encode / decode ({1,3} erased), device-resident.
 C4  8192 x 64 KiB RS(10,4) (one GPU's share of 65536), device-resident encode / decode with
     data blocks {9,0,5,2} erased.
 C5  mixed chunk sizes log-uniform in [4 KiB, 4 MiB] (seed 5) up to ~1 GiB, RS(8,3):
-    device-resident encode / decode (blocks {7,2,5} erased) and end-to-end from host memory.
+    device-resident encode / decode (blocks {7,2,5} erased) and end-to-end from host memory
+    (pageable buffers, staged; and pinned buffers, zero-copy).
 """
 
 from __future__ import annotations
@@ -121,6 +122,17 @@ def dec_descs_var(sizes, k, m, B, data_base, par_base, erased):
     return d, sn, offs
 
 
+def c5_sizes() -> list[int]:
+    """BASELINE configs[4] chunk sizes: log-uniform integers in [4 KiB, 4 MiB], seed 5, ~1 GiB."""
+    r5 = np.random.default_rng(5)
+    sizes, tot = [], 0
+    while tot < (1 << 30):
+        s = int(np.exp(r5.uniform(np.log(4096), np.log(4 << 20))))
+        sizes.append(s)
+        tot += s
+    return sizes
+
+
 def device_case(eng, sizes, k, m, erased, reps=20):
     import torch
 
@@ -185,13 +197,20 @@ def sha1_case(eng, nch=1024, n=1 << 20, k=4, m=6, reps=5):
             "note": "wall time per call incl. launch + sync; one lane per piece (SHA-1 is sequential per message)"}
 
 
-def host_case(eng, sizes, k, m, erased, reps=3):
+def host_case(eng, sizes, k, m, erased, reps=3, pinned=False):
+    """End to end from host memory: pageable numpy buffers (staged through the library's pinned
+    slabs) or, with pinned=True, Engine.host_empty buffers (the zero-copy path)."""
     total = int(np.sum(sizes))
     rng = np.random.default_rng(55)
-    host = rng.integers(0, 256, total, dtype=np.uint8)
     ed, B = enc_descs_var(sizes, k, m)
-    par = np.empty(int(np.sum(B)) * (m - k), dtype=np.uint8)
-    out = np.empty_like(host)
+    nb = int(np.sum(B)) * (m - k)
+    if pinned:
+        host, par, out = eng.host_empty(total), eng.host_empty(nb), eng.host_empty(total)
+        host[:] = rng.integers(0, 256, total, dtype=np.uint8)
+    else:
+        host = rng.integers(0, 256, total, dtype=np.uint8)
+        par = np.empty(nb, dtype=np.uint8)
+        out = np.empty_like(host)
     dd, sn, offs = dec_descs_var(sizes, k, m, B, host.ctypes.data, par.ctypes.data, erased)
     te = timed(lambda: eng.encode_batch(ed, host, par, host=True), reps)
     td = timed(lambda: eng.decode_batch(dd, sn, offs, 0, out, host=True), reps)
@@ -213,15 +232,12 @@ def main():
                               "reference path = piece.py policy + oracle/fec_oracle.c (zfec restated), 1 thread"}
     res["c2_c3_1024x1MiB_rs(4,2)"] = device_case(eng, [1 << 20] * 1024, 4, 6, (1, 3))
     res["c4_8192x64KiB_rs(10,4)_per_gpu"] = device_case(eng, [65536] * 8192, 10, 14, (9, 0, 5, 2))
-    r5 = np.random.default_rng(5)
-    sizes, tot = [], 0
-    while tot < (1 << 30):
-        s = int(np.exp(r5.uniform(np.log(4096), np.log(4 << 20))))
-        sizes.append(s)
-        tot += s
+    sizes = c5_sizes()
     res["c5_mixed_4KiB-4MiB_rs(8,3)_device"] = device_case(eng, sizes, 8, 11, (7, 2, 5))
     res["c5_mixed_4KiB-4MiB_rs(8,3)_e2e_host"] = host_case(eng, sizes, 8, 11, (7, 2, 5))
+    res["c5_mixed_4KiB-4MiB_rs(8,3)_e2e_host_pinned"] = host_case(eng, sizes, 8, 11, (7, 2, 5), pinned=True)
     res["c2_1024x1MiB_rs(4,2)_e2e_host"] = host_case(eng, [1 << 20] * 1024, 4, 6, (1, 3))
+    res["c2_1024x1MiB_rs(4,2)_e2e_host_pinned"] = host_case(eng, [1 << 20] * 1024, 4, 6, (1, 3), pinned=True)
     res["f1_sha1_pieces_c2_device"] = sha1_case(eng)
     import hashlib
     blob = np.random.default_rng(3).integers(0, 256, 1 << 28, dtype=np.uint8).tobytes()

@@ -69,20 +69,33 @@ def main():
     from bench import dec_descs, enc_descs
     from storb_amd.engine import Engine
 
-    if a.workload == "c2":
-        nch, n, k, m, erased = 1024, 1 << 20, 4, 6, (1, 3)
-    elif a.workload == "c4":  # per-GPU share: 8192 x 64 KiB RS(10,4)
-        nch, n, k, m, erased = 8192, 65536, 10, 14, (0, 2, 5, 9)
+    if a.workload == "c5":  # BASELINE configs[4]: mixed sizes, as tools/bench_configs.py
+        from tools.bench_configs import c5_sizes, dec_descs_var, enc_descs_var
+
+        sizes, k, m, erased = c5_sizes(), 8, 11, (7, 2, 5)
+        total = int(np.sum(sizes))
+        src = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda")
+        ed, Bs = enc_descs_var(sizes, k, m)
+        par = torch.empty(int(np.sum(Bs)) * (m - k), dtype=torch.uint8, device="cuda")
+        out = torch.empty_like(src)
+        dd, sn, offs = dec_descs_var(sizes, k, m, Bs, src.data_ptr(), par.data_ptr(), erased)
+        enc_bytes = total + int(np.sum(Bs)) * (m - k)
+        dec_bytes = int(np.sum(Bs)) * k + total
     else:
-        nch, n, k, m = map(int, a.workload.split(","))
-        erased = ((k - 1,) + tuple(range(0, k - 1, 2)))[: m - k]  # k-1 first: see bench.dec_descs
-    src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
-    ed, B = enc_descs(nch, n, k, m)
-    par = torch.empty(nch * (m - k) * B, dtype=torch.uint8, device="cuda")
-    out = torch.empty_like(src)
-    dd, sn, offs = dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), erased)
-    enc_bytes = nch * (n + (m - k) * B)
-    dec_bytes = nch * (k * B + n)
+        if a.workload == "c2":
+            nch, n, k, m, erased = 1024, 1 << 20, 4, 6, (1, 3)
+        elif a.workload == "c4":  # per-GPU share: 8192 x 64 KiB RS(10,4)
+            nch, n, k, m, erased = 8192, 65536, 10, 14, (0, 2, 5, 9)
+        else:
+            nch, n, k, m = map(int, a.workload.split(","))
+            erased = ((k - 1,) + tuple(range(0, k - 1, 2)))[: m - k]  # k-1 first: see bench.dec_descs
+        src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
+        ed, B = enc_descs(nch, n, k, m)
+        par = torch.empty(nch * (m - k) * B, dtype=torch.uint8, device="cuda")
+        out = torch.empty_like(src)
+        dd, sn, offs = dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), erased)
+        enc_bytes = nch * (n + (m - k) * B)
+        dec_bytes = nch * (k * B + n)
 
     configs = [(v, int(u)) for v in specs for u in a.us.split(",")]
     engines = {}
