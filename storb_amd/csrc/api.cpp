@@ -181,7 +181,11 @@ struct Image {
 };
 
 // lanes of every U = 1 tile (U > 1 tiles are 256 lanes); SEC_FULL_LANES overrides, for A/B
-int full_lanes() { return std::max(64, std::min(1024, (int)env_size("SEC_FULL_LANES", sec::kLanes))) / 64 * 64; }
+int full_lanes(bool decode)
+{
+    const int l = (int)env_size(decode ? "SEC_FULL_LANES" : "SEC_ENC_LANES", env_size("SEC_FULL_LANES", sec::kLanes));
+    return std::max(64, std::min(1024, l)) / 64 * 64;
+}
 
 // u-steps (4 KiB each) a lane covers per tile.  Larger U = more bytes in flight
 // per lane but more registers; SEC_TILE_U overrides (read per plan build).
@@ -219,7 +223,7 @@ uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 // byte launch cost C4 13-17 % on top of its main kernels (profiles/r01_c4_kernel_stats).
 // Chunks with valid < 16 get no tile: all of [0, B) becomes one-thread tail items.
 void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B, int64_t valid,
-              int rows_total, int k)
+              int rows_total, int k, bool decode)
 {
     if (B == 0)
         return;
@@ -241,7 +245,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
         const int rows = std::min(sec::kMaxRows, rows_total - r0);
         const int U = pick_u(B, rows, k);
         const int wide = k * U > sec::kBatchVecs;  // U == 1 then (pick_u)
-        const int flanes = U == 1 ? full_lanes() : sec::kLanes;
+        const int flanes = U == 1 ? full_lanes(decode) : sec::kLanes;
         const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * U;
         auto &full = bins[{rows, U, flanes, wide}];
         sec::Tile *last = nullptr;
@@ -253,7 +257,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
                 full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
                 last = &full.back();
             }
-            const int ul = full_lanes();
+            const int ul = full_lanes(decode);
             auto &ones = bins[{rows, 1, ul, k > sec::kBatchVecs}];
             for (uint64_t t0 = nfull * step; t0 < v; t0 += (uint64_t)sec::kLaneBytes * ul) {  // U > 1 remainder
                 ones.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
@@ -637,7 +641,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
             if (p > 0)
-                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k);
+                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false);
         }
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles, false);
@@ -808,7 +812,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             sp.in_bytes += (uint64_t)c.k * c.B;
             sp.out_bytes += nout;
             if (nout > 0)
-                add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k);
+                add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true);
         }
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles, true);

@@ -144,6 +144,12 @@ __device__ __forceinline__ void gf_mac(u32x4 (&acc)[R][U], const u32x4 (&x)[U], 
 #ifndef SEC_DEC_BATCH
 #define SEC_DEC_BATCH sec::kBatchVecs
 #endif
+//   SEC_DEC_LATE                decode: store a batch's present primaries after its GF work
+//                               (1) or as each slot arrives (0): C4 decode +5 %, C2 / C5
+//                               within noise (profiles/r01_sweep_declate.jsonl)
+#ifndef SEC_DEC_LATE
+#define SEC_DEC_LATE 1
+#endif
 #ifndef SEC_ENC_BATCH
 #define SEC_ENC_BATCH sec::kBatchVecs
 #endif
@@ -453,7 +459,7 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
         for (int c = 0; c < KB; ++c)
             if (c0 + c < k) {
                 const u32 orow = slot_row[d.slot0 + c0 + c];
-                if (copies && orow != 0xFFFFFFFFu) {
+                if (!SEC_DEC_LATE && copies && orow != 0xFFFFFFFFu) {
                     u8 *o = dst + (u64)orow * B;
 #pragma unroll
                     for (int u = 0; u < U; ++u)
@@ -462,6 +468,18 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
                 if constexpr (R > 0)
                     gf_mac<R, U>(acc, xs[c], tj + (c0 + c) * tstep);
             }
+        if (SEC_DEC_LATE)  // the batch's copies after its arithmetic
+#pragma unroll
+            for (int c = 0; c < KB; ++c)
+                if (c0 + c < k) {
+                    const u32 orow = slot_row[d.slot0 + c0 + c];
+                    if (copies && orow != 0xFFFFFFFFu) {
+                        u8 *o = dst + (u64)orow * B;
+#pragma unroll
+                        for (int u = 0; u < U; ++u)
+                            store16<SEC_DEC_ST>(o + pos[u], xs[c][u]);
+                    }
+                }
     };
     if constexpr (W) {  // wide k: several batches (see encode_main)
 #pragma unroll 1

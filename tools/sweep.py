@@ -36,6 +36,7 @@ VARIANTS = {
     "db8": {"SEC_DEC_BATCH": 8},  # decode KB = 8 / U (valid only for k * U <= 8)
     "db8eb8": {"SEC_DEC_BATCH": 8, "SEC_ENC_BATCH": 8},
     "b4": {"SEC_DEC_BATCH": 4, "SEC_ENC_BATCH": 4},  # KB = 4 / U: valid for k * U <= 4 only
+    "decearly": {"SEC_DEC_LATE": 0},  # decode: copies stored as each slot arrives
     "nowide": {"SEC_WIDE_K": 0},  # A/B only: drops the k > 16 loop (register cost)  # encode: KB * U = 4 vectors per batch
     "eb8": {"SEC_ENC_BATCH": 8},  # default (-1): XCD order for decode groups of full tiles only
     "xcd_dst0": {"SEC_XCD_ORDER": 1, "SEC_DEC_ST": 0},
