@@ -23,8 +23,8 @@ Also reported on the same line:
                 per task on min(16, usable cores) threads (`value`, `cores`), and 1 thread
                 (`single_thread_value`), --cpu-seconds each
   e2e           host-buffer encode+decode through the C ABI incl. PCIe: pageable buffers
-                (staged through pinned slabs) and pinned buffers (zero-copy) — reported
-                beside `value`, never as it
+                (page-locked per call, or staged through pinned slabs) and pinned buffers
+                (zero-copy) — reported beside `value`, never as it
 """
 
 from __future__ import annotations
@@ -303,25 +303,36 @@ def _e2e_pass(eng, host, par, out, nchunks, steps):
 
 
 def e2e_rate(eng, nchunks=1024, steps=3) -> dict:
-    """Encode + decode of host-resident 1 MiB chunks through SEC_F_HOST: from pageable numpy
-    buffers (staged through pinned slabs + DMA) and from pinned buffers (Engine.host_empty:
-    the kernels read / write host memory over PCIe directly)."""
+    """Encode + decode of host-resident 1 MiB chunks through SEC_F_HOST, three ways: pageable
+    numpy buffers (the library page-locks them for each call and the kernels read / write them
+    over PCIe), the same buffers staged through pinned slabs + DMA (SEC_REGISTER_MIN=0), and
+    pinned buffers (Engine.host_empty, zero-copy)."""
     rng = np.random.default_rng(7)
     host = rng.integers(0, 256, nchunks * CHUNK, dtype=np.uint8)
     nb = nchunks * (M - K) * (CHUNK // K)
-    z0, s0 = eng.host_paths()
-    enc, dec = _e2e_pass(eng, host, np.empty(nb, dtype=np.uint8), np.empty_like(host), nchunks, steps)
-    z1, s1 = eng.host_paths()
+    par, out = np.empty(nb, dtype=np.uint8), np.empty_like(host)
+    p0 = np.array(eng.host_paths())
+    enc, dec = _e2e_pass(eng, host, par, out, nchunks, steps)
+    p1 = np.array(eng.host_paths())
+    os.environ["SEC_REGISTER_MIN"] = "0"
+    try:
+        senc, sdec = _e2e_pass(eng, host, par, out, nchunks, steps)
+    finally:
+        os.environ.pop("SEC_REGISTER_MIN")
+    p2 = np.array(eng.host_paths())
     ph, pp, po = eng.host_empty(host.size), eng.host_empty(nb), eng.host_empty(host.size)
     ph[:] = host
     penc, pdec = _e2e_pass(eng, ph, pp, po, nchunks, steps)
-    z2, s2 = eng.host_paths()
-    if (z1 - z0, s1 - s0, z2 - z1, s2 - s1) != (0, 2 * (steps + 1), 2 * (steps + 1), 0):
-        raise SystemExit("bench: e2e calls did not take the expected host paths")
+    p3 = np.array(eng.host_paths())
+    calls = 2 * (steps + 1)
+    if (list(p1 - p0), list(p2 - p1), list(p3 - p2)) != ([0, calls, 0], [0, 0, calls], [calls, 0, 0]):
+        raise SystemExit(f"bench: e2e calls did not take the expected host paths {p0} {p1} {p2} {p3}")
     del ph, pp, po
-    return {"encode_gibs": enc, "decode_gibs": dec, "pinned_encode_gibs": penc, "pinned_decode_gibs": pdec,
-            "sample": f"{nchunks} x 1 MiB RS(4,2), {steps} calls each; *_gibs: pageable numpy buffers (staged); "
-                      f"pinned_*: Engine.host_empty buffers (zero-copy, kernels on host memory over PCIe)"}
+    return {"encode_gibs": enc, "decode_gibs": dec, "staged_encode_gibs": senc, "staged_decode_gibs": sdec,
+            "pinned_encode_gibs": penc, "pinned_decode_gibs": pdec,
+            "sample": f"{nchunks} x 1 MiB RS(4,2), {steps} calls each; *_gibs: pageable numpy buffers, page-locked "
+                      f"by the library per call; staged_*: the same, staged through pinned slabs; pinned_*: "
+                      f"Engine.host_empty buffers; the kernels read / write locked or pinned host memory over PCIe"}
 
 
 if __name__ == "__main__":

@@ -63,13 +63,15 @@ enum sec_status {
 
 /* flags for sec_encode_batch / sec_decode_batch */
 #define SEC_F_HOST 1u  /* in/out/blocks are HOST pointers; the call returns when the
-                          results are back in host memory.  Pageable buffers are staged
-                          through pinned slabs and device scratch.  When every buffer of
-                          an encode / decode lies in pinned memory mapped at the same
-                          address on the device (sec_host_alloc, sec_host_register,
-                          hipHostMalloc), the kernels read and write it directly over
-                          PCIe instead: no staging copy (sec_ctx_host_paths counts which
-                          path each call took)                                       */
+                          results are back in host memory.  When every buffer of an
+                          encode / decode lies in pinned memory mapped at the same address
+                          on the device (sec_host_alloc, sec_host_register, hipHostMalloc),
+                          the kernels read and write it directly over PCIe: no staging
+                          copy.  Pageable buffers of a large call (SEC_REGISTER_MIN bytes,
+                          default 4 MiB, in ranges of >= 1 MiB on average) are page-locked
+                          for the call and used the same way; otherwise (or if locking
+                          fails) they are staged through pinned slabs and device scratch.
+                          sec_ctx_host_paths counts which path each call took        */
 #define SEC_F_ASYNC 2u /* device pointers only: return once enqueued on the context
                           stream (sec_sync() waits)                                  */
 
@@ -236,9 +238,9 @@ int sec_host_free(sec_ctx *ctx, void *hptr);                 /* ctx may be NULL 
  * zero-copy path; unregister (ctx may be NULL) before freeing it. */
 int sec_host_register(sec_ctx *ctx, void *hptr, size_t bytes);
 int sec_host_unregister(sec_ctx *ctx, void *hptr);
-/* SEC_F_HOST encode / decode calls so far on this context: zero-copy (pinned buffers,
- * kernels on host memory) and staged (pageable buffers). */
-int sec_ctx_host_paths(sec_ctx *ctx, int64_t *zero_copy, int64_t *staged);
+/* SEC_F_HOST encode / decode calls so far on this context: zero-copy on the caller's pinned
+ * buffers, zero-copy on pages the call locked itself, and staged. */
+int sec_ctx_host_paths(sec_ctx *ctx, int64_t *zero_copy, int64_t *registered, int64_t *staged);
 /* kind: 0 host->device, 1 device->host, 2 device->device; synchronous on the ctx stream */
 int sec_memcpy(sec_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
 int sec_memset(sec_ctx *ctx, void *dptr, int value, size_t bytes);

@@ -383,7 +383,8 @@ struct sec_ctx {
     size_t bn_part_stride = 0;
     Slot slots[kSlots];
     std::unique_ptr<sec::CopyPool> pool;
-    int64_t zero_copy_calls = 0, staged_calls = 0;  // SEC_F_HOST calls by path (sec_ctx_host_paths)
+    // SEC_F_HOST encode / decode calls by path (sec_ctx_host_paths)
+    int64_t zero_copy_calls = 0, registered_calls = 0, staged_calls = 0;
 
     hipStream_t stream() const { return ext ? ext : own; }
     hipEvent_t ev()
@@ -1295,33 +1296,139 @@ bool pinned(uintptr_t a, uint64_t len, PinnedRange *cache)
     return true;
 }
 
-bool encode_pinned(const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in, const uint8_t *parity)
+// The caller byte ranges [a, a + len) a host call reads or writes.
+struct HostRange {
+    uintptr_t a;
+    uint64_t len;
+};
+
+std::vector<HostRange> encode_ranges(const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
+                                     const uint8_t *parity)
 {
-    PinnedRange ci, cp;
+    std::vector<HostRange> r;
     for (int64_t i = 0; i < nchunks; ++i) {
         const sec_enc_chunk &c = chunks[i];
         const uint64_t B = (c.n + (uint64_t)c.k - 1) / (uint64_t)c.k, p = (uint64_t)(c.m - c.k);
-        if (!pinned((uintptr_t)in + c.in_off, c.n, &ci))
-            return false;
-        if (p && B && !pinned((uintptr_t)parity + c.parity_off, (p - 1) * c.parity_stride + B, &cp))
-            return false;
+        r.push_back(HostRange{(uintptr_t)in + c.in_off, c.n});
+        if (p && B)
+            r.push_back(HostRange{(uintptr_t)parity + c.parity_off, (p - 1) * c.parity_stride + B});
     }
+    return r;
+}
+
+std::vector<HostRange> decode_ranges(const sec_dec_chunk *chunks, int64_t nchunks, const uint64_t *block_offs,
+                                     const uint8_t *blocks, const uint8_t *out)
+{
+    std::vector<HostRange> r;
+    for (int64_t i = 0; i < nchunks; ++i) {
+        const sec_dec_chunk &c = chunks[i];
+        r.push_back(HostRange{(uintptr_t)out + c.out_off, (uint64_t)c.k * c.B - c.padlen});
+        for (int j = 0; j < c.k; ++j)
+            r.push_back(HostRange{(uintptr_t)blocks + block_offs[c.slot0 + j], c.B});
+    }
+    return r;
+}
+
+bool all_pinned(const std::vector<HostRange> &rs)
+{
+    PinnedRange cache;
+    for (const HostRange &r : rs)
+        if (!pinned(r.a, r.len, &cache))
+            return false;
     return true;
 }
 
-bool decode_pinned(const sec_dec_chunk *chunks, int64_t nchunks, const uint64_t *block_offs, const uint8_t *blocks,
-                   const uint8_t *out)
-{
-    PinnedRange cb, co;
-    for (int64_t i = 0; i < nchunks; ++i) {
-        const sec_dec_chunk &c = chunks[i];
-        if (!pinned((uintptr_t)out + c.out_off, (uint64_t)c.k * c.B - c.padlen, &co))
-            return false;
-        for (int j = 0; j < c.k; ++j)
-            if (!pinned((uintptr_t)blocks + block_offs[c.slot0 + j], c.B, &cb))
+// Pages a host call locks for itself: pageable caller buffers are page-locked
+// (hipHostRegister) for the call's duration so the kernels can run on them directly.
+// Locking 1 GiB took 2.1 ms and unlocking 0.05 ms (tools/e2e_study.py), against tens of ms
+// for the two staging copies.  Used when the call moves at least SEC_REGISTER_MIN bytes
+// (default 4 MiB; 0 = never) in ranges of 1 MiB or more on average once ranges less than
+// 4 MiB apart are merged (one registration per small, separate buffer would cost more than
+// copying it).  Any failure
+// (memory already registered elsewhere, unregistrable mappings) releases what was locked and
+// the call is staged.  Released on every return path, after the stream has drained.
+class HostLock {
+public:
+    explicit HostLock(hipStream_t s) : s_(s) {}
+    ~HostLock() { release(); }
+    HostLock(const HostLock &) = delete;
+    HostLock &operator=(const HostLock &) = delete;
+
+    bool acquire(const std::vector<HostRange> &rs)
+    {
+        const uint64_t min_bytes = env_size("SEC_REGISTER_MIN", (size_t)4 << 20);
+        if (!getenv_zero("SEC_REGISTER_MIN") && min_bytes) {
+            uint64_t total = 0;
+            std::vector<std::pair<uintptr_t, uintptr_t>> pg;  // page-aligned [lo, hi)
+            for (const HostRange &r : rs)
+                if (r.len) {
+                    total += r.len;
+                    pg.emplace_back(r.a & ~kPageMask, (r.a + r.len + kPageMask) & ~kPageMask);
+                }
+            if (total < min_bytes)
                 return false;
+            std::sort(pg.begin(), pg.end());
+            std::vector<std::pair<uintptr_t, uintptr_t>> merged;
+            for (auto &q : pg)  // gaps up to kGap are locked too (e.g. the erased blocks of a decode)
+                if (!merged.empty() && q.first <= merged.back().second + kGap)
+                    merged.back().second = std::max(merged.back().second, q.second);
+                else
+                    merged.push_back(q);
+            if (merged.size() * ((uint64_t)1 << 20) > total)
+                return false;
+            for (auto &q : merged) {
+                if (hipHostRegister((void *)q.first, q.second - q.first, hipHostRegisterDefault) != hipSuccess) {
+                    (void)hipGetLastError();
+                    release();
+                    return false;
+                }
+                locked_.push_back((void *)q.first);
+            }
+            return true;
+        }
+        return false;
     }
-    return true;
+
+    void release()
+    {
+        if (locked_.empty())
+            return;
+        (void)hipStreamSynchronize(s_);  // nothing may still run on the pages
+        for (void *p : locked_)
+            (void)hipHostUnregister(p);
+        (void)hipGetLastError();
+        locked_.clear();
+    }
+
+private:
+    static constexpr uintptr_t kPageMask = 4095;
+    static constexpr uintptr_t kGap = (uintptr_t)4 << 20;
+    static bool getenv_zero(const char *name)
+    {
+        const char *v = getenv(name);
+        return v && v[0] == '0' && v[1] == 0;
+    }
+    hipStream_t s_;
+    std::vector<void *> locked_;
+};
+
+// Decides a host call's path: zero-copy on the caller's pinned buffers, zero-copy on pages
+// locked for the call (`lock`), or staged.  True = run the device path on host addresses.
+bool host_direct(sec_ctx *ctx, const std::vector<HostRange> &rs, HostLock &lock)
+{
+    if (all_pinned(rs)) {
+        ++ctx->zero_copy_calls;
+        return true;
+    }
+    if (lock.acquire(rs)) {
+        if (all_pinned(rs)) {
+            ++ctx->registered_calls;
+            return true;
+        }
+        lock.release();
+    }
+    ++ctx->staged_calls;
+    return false;
 }
 
 // sec_encode_batch (digests == nullptr, digest == false) and sec_encode_digest_batch.
@@ -1358,15 +1465,15 @@ int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, cons
         return SEC_OK;  // nothing to compute (m == k, or empty chunks)
     if ((!in && !host && total_in) || (!parity && total_par) || (digest && !digests))
         return SEC_EINVAL;
-    // pinned caller buffers: run the device path on them directly (synchronous, as every
-    // host call).  Digest mode keeps the staged path: SHA-1 is one latency-bound lane per
-    // piece, which would stall on every PCIe read.
-    if (host && !digest && encode_pinned(chunks, nchunks, in, parity)) {
+    // pinned (or lockable) caller buffers: run the device path on them directly (synchronous,
+    // as every host call).  Digest mode keeps the staged path: SHA-1 is one latency-bound lane
+    // per piece, which would stall on every PCIe read.
+    HostLock lock(ctx->stream());
+    if (host && !digest && host_direct(ctx, encode_ranges(chunks, nchunks, in, parity), lock)) {
         host = false;
         flags &= ~(SEC_F_HOST | SEC_F_ASYNC);
-        ++ctx->zero_copy_calls;
-    } else if (host) {
-        ++ctx->staged_calls;
+    } else if (host && digest) {
+        ++ctx->staged_calls;  // (host_direct counted the other staged calls)
     }
 
     // Plan key: the whole descriptor array for device mode; only the shapes for
@@ -1782,13 +1889,11 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         return SEC_OK;
     if (!out)  // blocks may be NULL: block_offs are then absolute addresses
         return SEC_EINVAL;
-    // pinned caller buffers: the device path on them directly (see encode_pinned)
-    if (host && decode_pinned(chunks, nchunks, block_offs, blocks, out)) {
+    // pinned (or lockable) caller buffers: the device path on them directly (see encode_impl)
+    HostLock lock(ctx->stream());
+    if (host && host_direct(ctx, decode_ranges(chunks, nchunks, block_offs, blocks, out), lock)) {
         host = false;
         flags &= ~(SEC_F_HOST | SEC_F_ASYNC);
-        ++ctx->zero_copy_calls;
-    } else if (host) {
-        ++ctx->staged_calls;
     }
 
     // Plan key (see sec_encode_batch): host mode keys on shapes + sharenums only.
@@ -1915,11 +2020,12 @@ int sec_host_unregister(sec_ctx *ctx, void *hptr)  // ctx unused: may be NULL
     return SEC_OK;
 }
 
-int sec_ctx_host_paths(sec_ctx *ctx, int64_t *zero_copy, int64_t *staged)
+int sec_ctx_host_paths(sec_ctx *ctx, int64_t *zero_copy, int64_t *registered, int64_t *staged)
 {
-    if (!ctx || !zero_copy || !staged)
+    if (!ctx || !zero_copy || !registered || !staged)
         return SEC_EINVAL;
     *zero_copy = ctx->zero_copy_calls;
+    *registered = ctx->registered_calls;
     *staged = ctx->staged_calls;
     return SEC_OK;
 }

@@ -184,11 +184,12 @@ class Engine:
         a, _ = addr(buf)
         self._check(self.lib.sec_host_unregister(None, a))
 
-    def host_paths(self) -> tuple[int, int]:
-        """(zero-copy, staged) counts of the ``host=True`` encode / decode calls so far."""
-        z, st = ctypes.c_int64(0), ctypes.c_int64(0)
-        self._check(self.lib.sec_ctx_host_paths(self._ctx, ctypes.byref(z), ctypes.byref(st)))
-        return z.value, st.value
+    def host_paths(self) -> tuple[int, int, int]:
+        """(zero-copy on pinned buffers, zero-copy on pages locked for the call, staged) counts
+        of the ``host=True`` encode / decode calls so far."""
+        z, r, st = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        self._check(self.lib.sec_ctx_host_paths(self._ctx, ctypes.byref(z), ctypes.byref(r), ctypes.byref(st)))
+        return z.value, r.value, st.value
 
     _SCRATCH_CAP = 256 << 20  # largest result staged in the reusable pinned scratch
 

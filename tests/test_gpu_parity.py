@@ -349,7 +349,7 @@ def test_zero_copy_pinned_buffers_and_host_rewrites():
         d = _enc_descs(nch, n, k, m)[0]
         hin, hpar, hout = eng.host_empty(nch * n), eng.host_empty(nch * (m - k) * B), eng.host_empty(nch * n)
         rng = np.random.default_rng(40)
-        z0, s0 = eng.host_paths()
+        z0, r0, s0 = eng.host_paths()
         for rep in range(3):
             hin[:] = rng.integers(0, 256, hin.size, dtype=np.uint8)
             eng.encode_batch(d, hin, hpar, host=True)
@@ -372,13 +372,15 @@ def test_zero_copy_pinned_buffers_and_host_rewrites():
             hout[:] = 0
             eng.decode_batch(dd, sn, offs, 0, hout, host=True)
             assert np.array_equal(hout, hin), rep
-        z1, s1 = eng.host_paths()
-        assert (z1 - z0, s1 - s0) == (6, 0)
-        # pinned input, pageable output: all-or-nothing -> the staged path, same bytes
+        z1, r1, s1 = eng.host_paths()
+        assert (z1 - z0, r1 - r0, s1 - s0) == (6, 0, 0)
+        # pinned input, pageable output: not zero-copy on the caller's pins alone (the call
+        # either locks the output pages itself or is staged); same bytes either way
         par2 = np.empty(hpar.size, dtype=np.uint8)
         eng.encode_batch(d, hin, par2, host=True)
         assert np.array_equal(par2, hpar)
-        assert eng.host_paths() == (z1, s1 + 1)
+        z2, r2, s2 = eng.host_paths()
+        assert z2 == z1 and (r2 - r1) + (s2 - s1) == 1
     finally:
         eng.close()
 
@@ -405,7 +407,56 @@ def test_registered_buffer_host_path():
         for ci in range(nch):
             want = oracle_parity(src[ci * n:(ci + 1) * n].tobytes(), k, m)
             assert par[ci * (m - k) * B:(ci + 1) * (m - k) * B].tobytes() == b"".join(want), ci
-        z, s = eng.host_paths()
+        z, r, s = eng.host_paths()
         print(f"registered buffers took the {'zero-copy' if z else 'staged'} path")
+    finally:
+        eng.close()
+
+
+def test_pageable_large_calls_lock_pages_per_call(monkeypatch):
+    """Large host calls on pageable memory page-lock the caller's ranges for the call, run the
+    kernels on them, and unlock them: results exact, the same buffers usable again (a second
+    call locks them again), and SEC_REGISTER_MIN=0 forces the staged path with equal bytes."""
+    from storb_amd.engine import Engine
+
+    eng = Engine(0)
+    try:
+        nch, n, k, m = 24, (1 << 20) + 7, 4, 6  # ragged, 24 MiB in
+        B = -(-n // k)
+        d = _enc_descs(nch, n, k, m)[0]
+        src = np.random.default_rng(43).integers(0, 256, nch * n, dtype=np.uint8)
+        pars = []
+        for rep in range(2):
+            par = np.zeros(nch * (m - k) * B, dtype=np.uint8)
+            eng.encode_batch(d, src, par, host=True)
+            pars.append(par)
+        z, r, s = eng.host_paths()
+        assert r == 2 and z == 0 and s == 0, (z, r, s)
+        for ci in (0, nch - 1):
+            want = oracle_parity(src[ci * n:(ci + 1) * n].tobytes(), k, m)
+            assert pars[0][ci * (m - k) * B:(ci + 1) * (m - k) * B].tobytes() == b"".join(want)
+        assert np.array_equal(pars[0], pars[1])
+        monkeypatch.setenv("SEC_REGISTER_MIN", "0")
+        par3 = np.zeros_like(pars[0])
+        eng.encode_batch(d, src, par3, host=True)
+        assert np.array_equal(par3, pars[0])
+        assert eng.host_paths() == (0, 2, 1)
+        monkeypatch.delenv("SEC_REGISTER_MIN")
+        # decode from the (pageable) data + parity arrays, blocks 3 (short) and 1 erased
+        keep = [0, 2, 4, 5]
+        dd = np.zeros(nch, dtype=DEC_DTYPE)
+        dd["out_off"] = np.arange(nch, dtype=np.uint64) * n
+        dd["B"], dd["padlen"], dd["k"], dd["m"] = B, B * k - n, k, m
+        dd["slot0"] = np.arange(nch, dtype=np.uint64) * k
+        sn = np.tile(np.array(keep, np.int32), nch)
+        offs = np.zeros(nch * k, np.uint64)
+        ci = np.arange(nch, dtype=np.uint64)
+        for j, sh in enumerate(keep):
+            offs[j::k] = (src.ctypes.data + ci * n + sh * B) if sh < k else \
+                (pars[0].ctypes.data + ci * (m - k) * B + (sh - k) * B)
+        out = np.zeros_like(src)
+        eng.decode_batch(dd, sn, offs, 0, out, host=True)
+        assert np.array_equal(out, src)
+        assert eng.host_paths() == (0, 3, 1)
     finally:
         eng.close()
