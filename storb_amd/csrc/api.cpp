@@ -1356,35 +1356,44 @@ public:
 
     bool acquire(const std::vector<HostRange> &rs)
     {
+        if (getenv_zero("SEC_REGISTER_MIN"))
+            return false;
         const uint64_t min_bytes = env_size("SEC_REGISTER_MIN", (size_t)4 << 20);
-        if (!getenv_zero("SEC_REGISTER_MIN") && min_bytes) {
-            uint64_t total = 0;
-            std::vector<std::pair<uintptr_t, uintptr_t>> pg;  // page-aligned [lo, hi)
-            for (const HostRange &r : rs)
-                if (r.len) {
-                    total += r.len;
+        uint64_t total = 0;
+        std::vector<std::pair<uintptr_t, uintptr_t>> pg;  // page-aligned [lo, hi) of unpinned ranges
+        PinnedRange cache;
+        for (const HostRange &r : rs)
+            if (r.len) {
+                total += r.len;
+                if (!pinned(r.a, r.len, &cache))  // already pinned (e.g. Engine's result scratch)
                     pg.emplace_back(r.a & ~kPageMask, (r.a + r.len + kPageMask) & ~kPageMask);
-                }
-            if (total < min_bytes)
-                return false;
-            std::sort(pg.begin(), pg.end());
+            }
+        if (total < min_bytes)
+            return false;
+        std::sort(pg.begin(), pg.end());
+        // ranges less than kGap apart are locked as one (e.g. around a decode's erased blocks);
+        // if that swallows memory that cannot be locked, retry with exact ranges once
+        for (const uintptr_t gap : {kGap, (uintptr_t)0}) {
             std::vector<std::pair<uintptr_t, uintptr_t>> merged;
-            for (auto &q : pg)  // gaps up to kGap are locked too (e.g. the erased blocks of a decode)
-                if (!merged.empty() && q.first <= merged.back().second + kGap)
+            for (auto &q : pg)
+                if (!merged.empty() && q.first <= merged.back().second + gap)
                     merged.back().second = std::max(merged.back().second, q.second);
                 else
                     merged.push_back(q);
             if (merged.size() * ((uint64_t)1 << 20) > total)
                 return false;
+            bool ok = true;
             for (auto &q : merged) {
                 if (hipHostRegister((void *)q.first, q.second - q.first, hipHostRegisterDefault) != hipSuccess) {
                     (void)hipGetLastError();
-                    release();
-                    return false;
+                    ok = false;
+                    break;
                 }
                 locked_.push_back((void *)q.first);
             }
-            return true;
+            if (ok)
+                return true;
+            release();
         }
         return false;
     }

@@ -458,5 +458,10 @@ def test_pageable_large_calls_lock_pages_per_call(monkeypatch):
         eng.decode_batch(dd, sn, offs, 0, out, host=True)
         assert np.array_equal(out, src)
         assert eng.host_paths() == (0, 3, 1)
+        # pageable input, pinned output (Engine.encode_host's result scratch): locks the input only
+        chunks = [src[ci * n:(ci + 1) * n] for ci in range(nch)]
+        par4 = eng.encode_host(chunks, [(k, m)] * nch)
+        assert b"".join(b"".join(p) for p in par4) == pars[0].tobytes()
+        assert eng.host_paths() == (0, 4, 1)
     finally:
         eng.close()
