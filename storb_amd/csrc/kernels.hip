@@ -153,6 +153,12 @@ __device__ __forceinline__ void gf_mac(u32x4 (&acc)[R][U], const u32x4 (&x)[U], 
 #ifndef SEC_ENC_BATCH
 #define SEC_ENC_BATCH sec::kBatchVecs
 #endif
+//   SEC_FIXED_K                 A/B only: the k <= KB kernels assume every chunk has this k
+//                               (compile-time block count: no per-block branches, counted
+//                               waits); valid only for workloads of that single k
+#ifndef SEC_FIXED_K
+#define SEC_FIXED_K 0
+#endif
 
 __device__ __forceinline__ u32x4 load16(const u8 *p)
 {
@@ -215,7 +221,7 @@ template <int R, int U, bool W>
 __device__ __forceinline__ void encode_main(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d,
                                             const sec::Tile &tl, const u32 *__restrict__ tabs, u32 t)
 {
-    const u32 B = d.B, k = d.k, valid = d.valid;
+    const u32 B = d.B, k = (!W && SEC_FIXED_K > 0) ? (u32)SEC_FIXED_K : d.k, valid = d.valid;
     const u32 step = blockDim.x * sec::kLaneBytes;  // bytes one u-step of the workgroup covers
     u32 pos[U];
 #pragma unroll
@@ -423,7 +429,7 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
                                                          const u32 *__restrict__ slot_row,
                                                          const u32 *__restrict__ miss_row)
 {
-    const u32 B = d.B, k = d.k, valid = d.valid;
+    const u32 B = d.B, k = (!W && SEC_FIXED_K > 0) ? (u32)SEC_FIXED_K : d.k, valid = d.valid;
     const u32 step = blockDim.x * sec::kLaneBytes;  // bytes one u-step of the workgroup covers
     u32 pos[U];
 #pragma unroll
@@ -539,6 +545,33 @@ __global__ __launch_bounds__(256) void sec_decode_tail(const u8 *__restrict__ bl
 // allowed) and byte-swapped to SHA-1's big-endian order.
 __device__ __forceinline__ u32 rotl(u32 x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
 
+// gfx950's three-input bitwise op (v_bitop3_b32, truth table as the immediate).  The
+// compiler does not form it from C: the message schedule's XOR of four words took 3
+// v_xor_b32 and Maj 2 ops.  Only symmetric tables are used (0x96 = XOR3, 0xE8 = Maj), so
+// the operand order of the table does not matter.
+__device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c)
+{
+    u32 r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// Ch(b, c, d) = (b & c) | (~b & d); written as C the compiler folded it into the round's
+// additions as 3 ops (sub, and, and_or)
+__device__ __forceinline__ u32 bfi(u32 b, u32 c, u32 d)
+{
+    u32 r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(c), "v"(d));
+    return r;
+}
+__device__ __forceinline__ u32 maj(u32 a, u32 b, u32 c)
+{
+    u32 r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// FIPS 180-4 SHA-1 compression: per round rotl(a, 5), f (v_bfi / XOR3 / Maj), two add3 and
+// rotl(b, 30); per scheduled word XOR3, XOR and a rotate.
 __device__ __forceinline__ void sha1_compress(u32 (&h)[5], u32 (&w)[16])
 {
     u32 a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
@@ -548,24 +581,24 @@ __device__ __forceinline__ void sha1_compress(u32 (&h)[5], u32 (&w)[16])
         if (t < 16) {
             wt = w[t];
         } else {
-            wt = rotl(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+            wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
             w[t & 15] = wt;
         }
         u32 f, k;
         if (t < 20) {
-            f = (b & c) | (~b & d);
+            f = bfi(b, c, d);
             k = 0x5A827999u;
         } else if (t < 40) {
-            f = b ^ c ^ d;
+            f = xor3(b, c, d);
             k = 0x6ED9EBA1u;
         } else if (t < 60) {
-            f = (b & c) | (b & d) | (c & d);
+            f = maj(b, c, d);
             k = 0x8F1BBCDCu;
         } else {
-            f = b ^ c ^ d;
+            f = xor3(b, c, d);
             k = 0xCA62C1D6u;
         }
-        const u32 tmp = rotl(a, 5) + f + e + k + wt;
+        const u32 tmp = rotl(a, 5) + f + (e + k + wt);
         e = d;
         d = c;
         c = rotl(b, 30);

@@ -41,6 +41,10 @@ VARIANTS = {
     "eb8": {"SEC_ENC_BATCH": 8},  # default (-1): XCD order for decode groups of full tiles only
     "xcd_dst0": {"SEC_XCD_ORDER": 1, "SEC_DEC_ST": 0},
     "xcd_dst2": {"SEC_XCD_ORDER": 1, "SEC_DEC_ST": 2},
+    # compile-time k (kernels.hip SEC_FIXED_K): valid only on a workload of that one k
+    "fk4": {"SEC_FIXED_K": 4},
+    "fk8": {"SEC_FIXED_K": 8},
+    "fk10": {"SEC_FIXED_K": 10},
 }
 
 
