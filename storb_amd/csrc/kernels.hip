@@ -88,31 +88,90 @@ __global__ __launch_bounds__(256) void sec_expand_tables(const u8 *__restrict__ 
     o[4] = pack(0 << 6, 1 << 6, 2 << 6, 3 << 6);  // c * (hi2<<6),   hi2 = 0..3
 }
 
+// gfx950's three-input bitwise op (v_bitop3_b32, truth table as the immediate).  The
+// compiler does not form it from C: a 4-term XOR took 3 v_xor_b32 (GF accumulation, SHA-1
+// message schedule) and SHA-1's Maj 2 ops.  Only symmetric tables are used (0x96 = XOR3,
+// 0xE8 = Maj), so the operand order of the table does not matter.
+__device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c)
+{
+    u32 r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// Ch(b, c, d) = (b & c) | (~b & d); written as C the compiler folded it into the round's
+// additions as 3 ops (sub, and, and_or)
+__device__ __forceinline__ u32 bfi(u32 b, u32 c, u32 d)
+{
+    u32 r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(c), "v"(d));
+    return r;
+}
+__device__ __forceinline__ u32 maj(u32 a, u32 b, u32 c)
+{
+    u32 r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // ---- the multiply-accumulate ------------------------------------------------
+template <int U>
+struct Sel {  // the 3 v_perm selectors of each dword of x: bits 0-2, 3-5, 6-7 of every byte
+    u32 s0[U][4], s1[U][4], s2[U][4];
+    __device__ __forceinline__ explicit Sel(const u32x4 (&x)[U])
+    {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const u32 v = x[u][w];
+                s0[u][w] = v & 0x07070707u;
+                s1[u][w] = (v >> 3) & 0x07070707u;
+                s2[u][w] = (v >> 6) & 0x03030303u;
+            }
+    }
+};
+__device__ __forceinline__ u32 perm(u32 hi, u32 lo, u32 sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
+
+// acc[r] ^= coefficient(r) * x for one block: 3 v_perm + 2 XOR per dword and row
 template <int R, int U>
 __device__ __forceinline__ void gf_mac(u32x4 (&acc)[R][U], const u32x4 (&x)[U], const u32 *__restrict__ t)
 {
-    u32 s0[U][4], s1[U][4], s2[U][4];
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const u32 v = x[u][w];
-            s0[u][w] = v & 0x07070707u;
-            s1[u][w] = (v >> 3) & 0x07070707u;
-            s2[u][w] = (v >> 6) & 0x03030303u;
-        }
+    const Sel<U> s(x);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const u32 a0 = t[r * 5 + 0], a1 = t[r * 5 + 1];
-        const u32 b0 = t[r * 5 + 2], b1 = t[r * 5 + 3];
-        const u32 c0 = t[r * 5 + 4];
+        const u32 *c = t + r * 5;
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int w = 0; w < 4; ++w)
-                acc[r][u][w] ^= __builtin_amdgcn_perm(a1, a0, s0[u][w]) ^ __builtin_amdgcn_perm(b1, b0, s1[u][w]) ^
-                                __builtin_amdgcn_perm(c0, c0, s2[u][w]);
+                acc[r][u][w] = xor3(acc[r][u][w], perm(c[1], c[0], s.s0[u][w]), perm(c[3], c[2], s.s1[u][w])) ^
+                               perm(c[4], c[4], s.s2[u][w]);
+    }
+}
+
+// Blocks go to gf_mac2 in pairs only for row groups of <= 4 rows: with 8 rows the second
+// block's selectors cost registers, and zfec(16,24) measured encode -14 %, decode -42 %
+// (C4 encode +12 %, C2 +1 %; profiles/r01_sweep_xor3.jsonl)
+__host__ __device__ constexpr bool kPairRows(int R) { return R <= 4; }
+
+// Two blocks at once: the 6 products of a dword and row go into acc by 3 XOR3s, so 3 v_perm
+// + 1.5 XOR per dword, row and block (a 4-term XOR chain in C took 3 v_xor_b32 per block)
+template <int R, int U>
+__device__ __forceinline__ void gf_mac2(u32x4 (&acc)[R][U], const u32x4 (&x)[U], const u32 *__restrict__ t,
+                                        const u32x4 (&y)[U], const u32 *__restrict__ q)
+{
+    const Sel<U> s(x), z(y);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const u32 *c = t + r * 5, *d = q + r * 5;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                u32 a = xor3(acc[r][u][w], perm(c[1], c[0], s.s0[u][w]), perm(c[3], c[2], s.s1[u][w]));
+                a = xor3(a, perm(c[4], c[4], s.s2[u][w]), perm(d[1], d[0], z.s0[u][w]));
+                acc[r][u][w] = xor3(a, perm(d[3], d[2], z.s1[u][w]), perm(d[4], d[4], z.s2[u][w]));
+            }
     }
 }
 
@@ -254,10 +313,20 @@ __device__ __forceinline__ void encode_main(const u8 *__restrict__ in, u8 *__res
                 for (int u = 0; u < U; ++u)
                     xs[c][u] = load16(row + (u64)(j0 + c) * B + pos[u]);
             }
+        if constexpr (kPairRows(R)) {
 #pragma unroll
-        for (int c = 0; c < KB; ++c)
-            if (j0 + c < k)
-                gf_mac<R, U>(acc, xs[c], tj + (j0 + c) * tstep);
+            for (int c = 0; c < KB; c += 2) {
+                if (c + 1 < KB && j0 + c + 1 < k)
+                    gf_mac2<R, U>(acc, xs[c], tj + (j0 + c) * tstep, xs[c + 1], tj + (j0 + c + 1) * tstep);
+                else if (j0 + c < k)
+                    gf_mac<R, U>(acc, xs[c], tj + (j0 + c) * tstep);
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < KB; ++c)
+                if (j0 + c < k)
+                    gf_mac<R, U>(acc, xs[c], tj + (j0 + c) * tstep);
+        }
     };
     // W (wide k, U = 1 only): k > KB, several batches.  A separate instantiation: merely
     // compiling this loop into the k <= KB kernel cost C4 15 % (registers; r01 sweep_wide).
@@ -461,19 +530,36 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
                 for (int u = 0; u < U; ++u)
                     xs[c][u] = load16(s + pos[u]);
             }
+        if constexpr (SEC_DEC_LATE) {  // slots in pairs (gf_mac2)
+            if constexpr (R > 0 && kPairRows(R)) {
 #pragma unroll
-        for (int c = 0; c < KB; ++c)
-            if (c0 + c < k) {
-                const u32 orow = slot_row[d.slot0 + c0 + c];
-                if (!SEC_DEC_LATE && copies && orow != 0xFFFFFFFFu) {
-                    u8 *o = dst + (u64)orow * B;
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        store16<SEC_DEC_ST>(o + pos[u], xs[c][u]);
+                for (int c = 0; c < KB; c += 2) {
+                    if (c + 1 < KB && c0 + c + 1 < k)
+                        gf_mac2<R, U>(acc, xs[c], tj + (c0 + c) * tstep, xs[c + 1], tj + (c0 + c + 1) * tstep);
+                    else if (c0 + c < k)
+                        gf_mac<R, U>(acc, xs[c], tj + (c0 + c) * tstep);
                 }
-                if constexpr (R > 0)
-                    gf_mac<R, U>(acc, xs[c], tj + (c0 + c) * tstep);
+            } else if constexpr (R > 0) {
+#pragma unroll
+                for (int c = 0; c < KB; ++c)
+                    if (c0 + c < k)
+                        gf_mac<R, U>(acc, xs[c], tj + (c0 + c) * tstep);
             }
+        } else {
+#pragma unroll
+            for (int c = 0; c < KB; ++c)
+                if (c0 + c < k) {
+                    const u32 orow = slot_row[d.slot0 + c0 + c];
+                    if (copies && orow != 0xFFFFFFFFu) {
+                        u8 *o = dst + (u64)orow * B;
+#pragma unroll
+                        for (int u = 0; u < U; ++u)
+                            store16<SEC_DEC_ST>(o + pos[u], xs[c][u]);
+                    }
+                    if constexpr (R > 0)
+                        gf_mac<R, U>(acc, xs[c], tj + (c0 + c) * tstep);
+                }
+        }
         if (SEC_DEC_LATE)  // the batch's copies after its arithmetic
 #pragma unroll
             for (int c = 0; c < KB; ++c)
@@ -544,31 +630,6 @@ __global__ __launch_bounds__(256) void sec_decode_tail(const u8 *__restrict__ bl
 // and wants many messages in flight.  Words are loaded 16 B at a time (unaligned
 // allowed) and byte-swapped to SHA-1's big-endian order.
 __device__ __forceinline__ u32 rotl(u32 x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
-
-// gfx950's three-input bitwise op (v_bitop3_b32, truth table as the immediate).  The
-// compiler does not form it from C: the message schedule's XOR of four words took 3
-// v_xor_b32 and Maj 2 ops.  Only symmetric tables are used (0x96 = XOR3, 0xE8 = Maj), so
-// the operand order of the table does not matter.
-__device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c)
-{
-    u32 r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-// Ch(b, c, d) = (b & c) | (~b & d); written as C the compiler folded it into the round's
-// additions as 3 ops (sub, and, and_or)
-__device__ __forceinline__ u32 bfi(u32 b, u32 c, u32 d)
-{
-    u32 r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(c), "v"(d));
-    return r;
-}
-__device__ __forceinline__ u32 maj(u32 a, u32 b, u32 c)
-{
-    u32 r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
 
 // FIPS 180-4 SHA-1 compression: per round rotl(a, 5), f (v_bfi / XOR3 / Maj), two add3 and
 // rotl(b, 30); per scheduled word XOR3, XOR and a rotate.
