@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-events", action="store_true",
+                    help="A/B only: no per-launch HIP events in the timed region (roofline fields then null)")
     return ap.parse_args()
 
 
@@ -213,7 +215,7 @@ def main():
     if not torch.equal(out, src):
         raise SystemExit("bench: decode round trip mismatch")
 
-    eng.set_timing(True)
+    eng.set_timing(not args.no_events)
     D.barrier(dmod, local)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -233,8 +235,8 @@ def main():
 
     enc_alg = N_CHUNKS * (n + (m - k) * B)  # bytes per encode launch
     dec_alg = N_CHUNKS * (k * B + n)  # reassemble: k blocks read + n written
-    enc_avg_s = enc_ms / 1e3 / max(enc_n, 1)
-    dec_avg_s = dec_ms / 1e3 / max(dec_n, 1)
+    enc_avg_s = enc_ms / 1e3 / max(enc_n, 1) or float("nan")
+    dec_avg_s = dec_ms / 1e3 / max(dec_n, 1) or float("nan")
     enc_gbs = enc_alg / enc_avg_s / 1e9
     traffic = load_traffic()
 

@@ -78,6 +78,9 @@ struct MsgDesc {
 
 // launchers (kernels.hip); all enqueue on `stream` and return hipError_t as int
 extern "C++" {
+// Timing: the next launch's dispatch records `start`, every launch records `stop` (both
+// hipEvent_t, or null), until the next call; returns the launches since the previous call.
+int sec_launch_events(void *start, void *stop);
 int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void *stream);
 // wide: k > kBatchVecs / U (U must be 1): the kernels that load the blocks in several batches
 int sec_launch_encode(int rows, int U, int wide, int lanes, const uint8_t *in, uint8_t *par,
