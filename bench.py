@@ -63,21 +63,23 @@ def parse():
     return ap.parse_args()
 
 
-def enc_descs(nchunks, n, k, m):
+def enc_descs(nchunks, n, k, m, pstride=None):
+    """pstride: distance between a chunk's parity blocks (default B, i.e. packed)."""
     from storb_amd._lib import ENC_DTYPE
 
     B = -(-n // k)
+    ps = pstride or B
     d = np.zeros(nchunks, dtype=ENC_DTYPE)
     d["in_off"] = np.arange(nchunks, dtype=np.uint64) * n
     d["n"] = n
-    d["parity_off"] = np.arange(nchunks, dtype=np.uint64) * (m - k) * B
-    d["parity_stride"] = B
+    d["parity_off"] = np.arange(nchunks, dtype=np.uint64) * (m - k) * ps
+    d["parity_stride"] = ps
     d["k"] = k
     d["m"] = m
     return d, B
 
 
-def dec_descs(nchunks, n, k, m, B, data_base, par_base, erased):
+def dec_descs(nchunks, n, k, m, B, data_base, par_base, erased, pstride=None):
     """Decode descriptors whose surviving blocks are read in place from the encode buffers.
 
     The C ABI needs B readable bytes per block; an in-place data block k-1 is short when
@@ -85,6 +87,7 @@ def dec_descs(nchunks, n, k, m, B, data_base, par_base, erased):
     """
     from storb_amd._lib import DEC_DTYPE
 
+    ps = pstride or B
     if B * k != n and (k - 1) not in erased:
         raise ValueError("padded last data block cannot be read in place: erase block k-1")
     keep = [s for s in range(m) if s not in erased][:k]
@@ -99,7 +102,7 @@ def dec_descs(nchunks, n, k, m, B, data_base, par_base, erased):
     offs = np.zeros(nchunks * k, np.uint64)
     ci = np.arange(nchunks, dtype=np.uint64)
     for j, s in enumerate(keep):
-        offs[j::k] = (data_base + ci * n + s * B) if s < k else (par_base + ci * (m - k) * B + (s - k) * B)
+        offs[j::k] = (data_base + ci * n + s * B) if s < k else (par_base + ci * (m - k) * ps + (s - k) * ps)
     return d, sn, offs
 
 

@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--variants", default="base,tmp")
     ap.add_argument("--us", default="1,2,4")
+    ap.add_argument("--palign", type=int, default=1, help="parity stride rounded up to this many bytes")
     ap.add_argument("--workload", default="c2", help="c2 | c4 | nch,n,k,m (custom shape)")
     a = ap.parse_args()
     # a variant is TAG or TAG@ENV=VALUE: the TAG build, with ENV set while its plan is built
@@ -100,10 +101,12 @@ def main():
             nch, n, k, m = map(int, a.workload.split(","))
             erased = ((k - 1,) + tuple(range(0, k - 1, 2)))[: m - k]  # k-1 first: see bench.dec_descs
         src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
-        ed, B = enc_descs(nch, n, k, m)
-        par = torch.empty(nch * (m - k) * B, dtype=torch.uint8, device="cuda")
+        B = -(-n // k)
+        ps = -(-B // a.palign) * a.palign
+        ed, B = enc_descs(nch, n, k, m, ps)
+        par = torch.zeros(nch * (m - k) * ps, dtype=torch.uint8, device="cuda")
         out = torch.empty_like(src)
-        dd, sn, offs = dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), erased)
+        dd, sn, offs = dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), erased, ps)
         enc_bytes = nch * (n + (m - k) * B)
         dec_bytes = nch * (k * B + n)
 
@@ -157,7 +160,7 @@ def main():
             bad.add(c)
     for c in configs:
         enc, dec = np.array(samples[c][0]), np.array(samples[c][1])
-        print(json.dumps({"variant": c[0], "U": c[1], "workload": a.workload,
+        print(json.dumps({"variant": c[0], "U": c[1], "workload": a.workload, "palign": a.palign,
                           "enc_ms_med": round(float(np.median(enc)), 4), "enc_GBs": round(enc_bytes / np.median(enc) / 1e6, 1),
                           "enc_GBs_best": round(enc_bytes / enc.min() / 1e6, 1),
                           "dec_ms_med": round(float(np.median(dec)), 4), "dec_GBs": round(dec_bytes / np.median(dec) / 1e6, 1),
