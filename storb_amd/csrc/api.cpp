@@ -209,6 +209,18 @@ int pick_u(uint64_t B, int rows, int k)
     return u;
 }
 
+// Whether a group of `rows` output rows over k blocks runs in the wide (W) kernels, which
+// load the blocks in several batches.  Needed when k * U > kBatchVecs; groups of more than 4
+// rows also go there from k > SEC_WIDE_K8 on (A/B knob), since the W kernels pair blocks for
+// 8-row groups with smaller batches (kernels.hip SEC_WIDE_BATCH).
+bool is_wide(int k, int U, int rows)
+{
+    if (k * U > sec::kBatchVecs)
+        return true;
+    const int k8 = (int)env_size("SEC_WIDE_K8", sec::kBatchVecs);  // read per plan build
+    return U == 1 && rows > 4 && k > k8;
+}
+
 using Bins = std::map<std::tuple<int, int, int, int>, std::vector<sec::Tile>>;  // (rows, U, lanes, wide)
 
 uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
@@ -244,7 +256,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
         const int r0 = g * sec::kMaxRows;
         const int rows = std::min(sec::kMaxRows, rows_total - r0);
         const int U = pick_u(B, rows, k);
-        const int wide = k * U > sec::kBatchVecs;  // U == 1 then (pick_u)
+        const int wide = is_wide(k, U, rows);  // U == 1 then (pick_u)
         const int flanes = U == 1 ? full_lanes(decode) : sec::kLanes;
         const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * U;
         auto &full = bins[{rows, U, flanes, wide}];
@@ -258,7 +270,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
                 last = &full.back();
             }
             const int ul = full_lanes(decode);
-            auto &ones = bins[{rows, 1, ul, k > sec::kBatchVecs}];
+            auto &ones = bins[{rows, 1, ul, is_wide(k, 1, rows)}];
             for (uint64_t t0 = nfull * step; t0 < v; t0 += (uint64_t)sec::kLaneBytes * ul) {  // U > 1 remainder
                 ones.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
                 last = &ones.back();
@@ -274,7 +286,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
             for (uint64_t t0 = nfull * step; t0 < v;) {
                 const uint64_t lanes =
                     std::min<uint64_t>(1024, round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
-                auto &bin = bins[{rows, 1, (int)lanes, k > sec::kBatchVecs}];
+                auto &bin = bins[{rows, 1, (int)lanes, is_wide(k, 1, rows)}];
                 bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
                 last = &bin.back();
                 t0 += lanes * sec::kLaneBytes;

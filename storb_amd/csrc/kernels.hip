@@ -150,10 +150,20 @@ __device__ __forceinline__ void gf_mac(u32x4 (&acc)[R][U], const u32x4 (&x)[U], 
     }
 }
 
-// Blocks go to gf_mac2 in pairs only for row groups of <= 4 rows: with 8 rows the second
+// In the k <= 16 kernels blocks go to gf_mac2 in pairs only for row groups of <= 4 rows: with 8 rows the second
 // block's selectors cost registers, and zfec(16,24) measured encode -14 %, decode -42 %
 // (C4 encode +12 %, C2 +1 %; profiles/r01_sweep_xor3.jsonl)
-__host__ __device__ constexpr bool kPairRows(int R) { return R <= 4; }
+// The wide-k (W) kernels load smaller batches (SEC_WIDE_BATCH), which leaves the registers
+// to pair blocks for 8-row groups too: zfec(32,48) / (64,96) encode +11 %, decode +7-10 %
+// (profiles/r01_sweep_wide_pair.jsonl).
+#ifndef SEC_PAIR_ROWS
+#define SEC_PAIR_ROWS 4
+#endif
+#ifndef SEC_WIDE_PAIR_ROWS
+#define SEC_WIDE_PAIR_ROWS 8
+#endif
+template <int R, bool W>
+__host__ __device__ constexpr bool kPairRows() { return R <= (W ? SEC_WIDE_PAIR_ROWS : SEC_PAIR_ROWS); }
 
 // Two blocks at once: the 6 products of a dword and row go into acc by 3 XOR3s, so 3 v_perm
 // + 1.5 XOR per dword, row and block (a 4-term XOR chain in C took 3 v_xor_b32 per block)
@@ -212,6 +222,11 @@ __device__ __forceinline__ void gf_mac2(u32x4 (&acc)[R][U], const u32x4 (&x)[U],
 #endif
 #ifndef SEC_ENC_BATCH
 #define SEC_ENC_BATCH sec::kBatchVecs
+#endif
+//   SEC_WIDE_BATCH              vectors per batch in the wide-k (W) kernels, which loop over
+//                               batches; default: the encode / decode batch
+#ifndef SEC_WIDE_BATCH
+#define SEC_WIDE_BATCH 8
 #endif
 //   SEC_FIXED_K                 A/B only: the k <= KB kernels assume every chunk has this k
 //                               (compile-time block count: no per-block branches, counted
@@ -304,7 +319,8 @@ __device__ __forceinline__ void encode_main(const u8 *__restrict__ in, u8 *__res
     // loads in flight; C2 (k = 4) and C4 (k = 10) are one batch.  A one-block-ahead prefetch
     // loop compiled to a full wait at its head (the next block's load included): one load in
     // flight per lane and u-step, C2 -3.5 %, C4 -9 % (profiles/r01_sweep_enc_batch.jsonl).
-    constexpr int KB = SEC_ENC_BATCH / U > 0 ? SEC_ENC_BATCH / U : 1;
+    constexpr int KBV = (W && SEC_WIDE_BATCH > 0) ? SEC_WIDE_BATCH : SEC_ENC_BATCH;
+    constexpr int KB = KBV / U > 0 ? KBV / U : 1;
     auto batch = [&](u32 j0) {
         u32x4 xs[KB][U];
 #pragma unroll
@@ -314,7 +330,7 @@ __device__ __forceinline__ void encode_main(const u8 *__restrict__ in, u8 *__res
                 for (int u = 0; u < U; ++u)
                     xs[c][u] = load16(row + (u64)(j0 + c) * B + pos[u]);
             }
-        if constexpr (kPairRows(R)) {
+        if constexpr (kPairRows<R, W>()) {
 #pragma unroll
             for (int c = 0; c < KB; c += 2) {
                 if (c + 1 < KB && j0 + c + 1 < k)
@@ -520,7 +536,8 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
     // Slots go in batches of KB, as in encode_main: every load of a batch before any store
     // or arithmetic, then the batch in order — each present primary copied to its output
     // row, every slot fed to the R accumulators.  C2 / C4 are one batch (all loads in flight).
-    constexpr int KB = SEC_DEC_BATCH / U > 0 ? SEC_DEC_BATCH / U : 1;
+    constexpr int KBV = (W && SEC_WIDE_BATCH > 0) ? SEC_WIDE_BATCH : SEC_DEC_BATCH;
+    constexpr int KB = KBV / U > 0 ? KBV / U : 1;
     auto batch = [&](u32 c0) {
         u32x4 xs[KB][U];
 #pragma unroll
@@ -532,7 +549,7 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
                     xs[c][u] = load16(s + pos[u]);
             }
         if constexpr (SEC_DEC_LATE) {  // slots in pairs (gf_mac2)
-            if constexpr (R > 0 && kPairRows(R)) {
+            if constexpr (R > 0 && kPairRows<R, W>()) {
 #pragma unroll
                 for (int c = 0; c < KB; c += 2) {
                     if (c + 1 < KB && c0 + c + 1 < k)

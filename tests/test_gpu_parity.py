@@ -55,7 +55,8 @@ def test_decode_golden(engine):
 
 
 @pytest.mark.parametrize("k,m", [(1, 2), (2, 3), (3, 4), (4, 6), (5, 8), (8, 11), (10, 14), (8, 16), (12, 20),
-                                 (16, 24), (20, 30), (32, 48), (64, 96), (4, 4), (7, 256)])
+                                 (16, 24), (20, 30), (32, 48), (64, 96), (4, 4), (7, 256),
+                                 (128, 256), (255, 256)])
 def test_encode_random_sizes_vs_oracle(engine, k, m):
     rng = random.Random(k * 1000 + m)
     sizes = [k, k * k, 4095, 4096 * k, 4096 * k + 1, 65536, 65536 + 7, 6554 * k - 3, 262144 + 13, 1 << 20]
@@ -81,7 +82,8 @@ def test_encode_mixed_shapes_one_batch(engine):
         assert p == oracle_parity(c, k, m)
 
 
-@pytest.mark.parametrize("k,m", [(2, 3), (4, 6), (8, 11), (10, 14), (16, 24), (16, 40), (32, 48)])
+@pytest.mark.parametrize("k,m", [(2, 3), (4, 6), (8, 11), (10, 14), (16, 24), (16, 40), (32, 48), (64, 96),
+                                 (3, 256), (128, 256)])
 def test_decode_erasures_vs_oracle(engine, k, m):
     rng = random.Random(k + 100 * m)
     items, expect = [], []

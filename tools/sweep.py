@@ -45,6 +45,11 @@ VARIANTS = {
     "fk4": {"SEC_FIXED_K": 4},
     "fk8": {"SEC_FIXED_K": 8},
     "fk10": {"SEC_FIXED_K": 10},
+    # wide k (W kernels): the earlier 16-vector batches without block pairs for 8-row groups;
+    # 4-vector batches; pairs for 8-row groups in the k <= 16 kernels too
+    "prevwide": {"SEC_WIDE_BATCH": 16, "SEC_WIDE_PAIR_ROWS": 4},
+    "wb4": {"SEC_WIDE_BATCH": 4},
+    "pair8": {"SEC_PAIR_ROWS": 8},
 }
 
 
