@@ -257,7 +257,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
         const int rows = std::min(sec::kMaxRows, rows_total - r0);
         const int U = pick_u(B, rows, k);
         const int wide = is_wide(k, U, rows);  // U == 1 then (pick_u)
-        const int flanes = U == 1 ? full_lanes(decode) : sec::kLanes;
+        const int flanes = U == 1 ? std::min(full_lanes(decode), sec::max_lanes(rows, 1)) : sec::kLanes;
         const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * U;
         auto &full = bins[{rows, U, flanes, wide}];
         sec::Tile *last = nullptr;
@@ -269,7 +269,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
                 full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
                 last = &full.back();
             }
-            const int ul = full_lanes(decode);
+            const int ul = std::min(full_lanes(decode), sec::max_lanes(rows, 1));
             auto &ones = bins[{rows, 1, ul, is_wide(k, 1, rows)}];
             for (uint64_t t0 = nfull * step; t0 < v; t0 += (uint64_t)sec::kLaneBytes * ul) {  // U > 1 remainder
                 ones.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
@@ -285,7 +285,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
             }
             for (uint64_t t0 = nfull * step; t0 < v;) {
                 const uint64_t lanes =
-                    std::min<uint64_t>(1024, round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
+                    std::min<uint64_t>(sec::max_lanes(rows, 1), round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
                 auto &bin = bins[{rows, 1, (int)lanes, is_wide(k, 1, rows)}];
                 bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
                 last = &bin.back();

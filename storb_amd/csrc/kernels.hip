@@ -278,7 +278,7 @@ __device__ __forceinline__ void encode_ragged(const u8 *__restrict__ in, u8 *__r
                                            const sec::Tile &tl, const u32 *__restrict__ tabs);
 
 template <int R, int U, bool W>
-__global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+__global__ __launch_bounds__(sec::max_lanes(R, U)) void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
                                                          const sec::EncDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
                                                          const u32 *__restrict__ tabs)
@@ -448,7 +448,7 @@ __device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 
                                            const u32 *__restrict__ miss_row);
 
 template <int R, int U, bool W>
-__global__ __launch_bounds__(U == 1 ? 1024 : 256) void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+__global__ __launch_bounds__(sec::max_lanes(R, U)) void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                          const sec::DecDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
                                                          const u32 *__restrict__ tabs,
@@ -851,7 +851,7 @@ int sec_launch_encode(int rows, int U, int wide, int lanes, const uint8_t *in, u
 {
     if (ntiles == 0)
         return hipSuccess;
-    if (lanes < 64 || lanes % 64 || lanes > (U == 1 ? 1024 : sec::kLanes) || (wide && U != 1))
+    if (lanes < 64 || lanes % 64 || lanes > sec::max_lanes(rows, U) || (wide && U != 1))
         return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
     if (wide)
@@ -879,7 +879,7 @@ int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *block
 {
     if (ntiles == 0)
         return hipSuccess;
-    if (lanes < 64 || lanes % 64 || lanes > (U == 1 ? 1024 : sec::kLanes) || (wide && U != 1))
+    if (lanes < 64 || lanes % 64 || lanes > sec::max_lanes(rows, U) || (wide && U != 1))
         return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
     const u32 L = (u32)lanes;

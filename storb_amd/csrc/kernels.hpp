@@ -23,6 +23,13 @@ constexpr int kMaxRows = 8;         // output rows per tile (accumulator groups)
 constexpr int kTabDwords = 5;       // v_perm tables per GF coefficient
 constexpr int kBatchVecs = 16;      // 16 B vectors a lane loads per batch (SEC_ENC/DEC_BATCH):
                                     // a tile has U > 1 only if k * U <= kBatchVecs
+// Largest workgroup of a tile kernel with `rows` output rows (its launch bound, which also
+// caps its VGPRs: 1024 lanes leave 128 per lane).  Groups of more than 4 rows are bound by
+// SEC_LB_WIDE_ROWS lanes (A/B knob); the plan clamps its tile widths to this.
+#ifndef SEC_LB_WIDE_ROWS
+#define SEC_LB_WIDE_ROWS 1024
+#endif
+constexpr int max_lanes(int rows, int U) { return U != 1 ? kLanes : (rows > 4 ? SEC_LB_WIDE_ROWS : 1024); }
 
 // One encode chunk, device copy (48 B).
 struct EncDesc {

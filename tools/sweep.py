@@ -50,6 +50,10 @@ VARIANTS = {
     "prevwide": {"SEC_WIDE_BATCH": 16, "SEC_WIDE_PAIR_ROWS": 4},
     "wb4": {"SEC_WIDE_BATCH": 4},
     "pair8": {"SEC_PAIR_ROWS": 8},
+    # launch bound of the > 4-row kernels (VGPR cap: 1024 lanes leave 128), with / without pairs
+    "lb256": {"SEC_LB_WIDE_ROWS": 256},
+    "lb256p8": {"SEC_LB_WIDE_ROWS": 256, "SEC_PAIR_ROWS": 8},
+    "lb512p8": {"SEC_LB_WIDE_ROWS": 512, "SEC_PAIR_ROWS": 8},
 }
 
 
