@@ -692,8 +692,19 @@ __device__ __forceinline__ void sha1_compress(u32 (&h)[5], u32 (&w)[16])
 }
 
 // byte i of the message: real below `avail`, zero from there to `len`
+// Batches of fewer than kSha1PrefetchMsgs messages (under one wave per SIMD) load each next
+// block before compressing the current one: with no other wave on the SIMD the loads'
+// latency was exposed per block.  C2's 6144 pieces of 256 KiB: 6.30-6.44 -> 5.07 ms; C4's
+// 114688 short pieces, which have waves to switch to, measured 6-22 % slower with it
+// (registers), so they keep the plain loop (profiles/r01_sha1_prefetch.jsonl).
+// SEC_SHA1_PF = 0 / 1 forces it off / on (A/B).
+#ifndef SEC_SHA1_PF
+#define SEC_SHA1_PF -1
+#endif
+constexpr uint32_t kSha1PrefetchMsgs = 65536;
 __device__ __forceinline__ u32 msg_byte(const u8 *p, uint64_t i, uint64_t avail) { return i < avail ? p[i] : 0u; }
 
+template <bool PF>
 __global__ __launch_bounds__(64) void sec_sha1_kernel(const u8 *__restrict__ base0, const u8 *__restrict__ base1,
                                                       const sec::MsgDesc *__restrict__ msgs, u32 nmsgs,
                                                       u8 *__restrict__ digests)
@@ -706,7 +717,31 @@ __global__ __launch_bounds__(64) void sec_sha1_kernel(const u8 *__restrict__ bas
     u32 h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
     u32 w[16];
     const uint64_t nfull = m.len / 64;
-    for (uint64_t blk = 0; blk < nfull; ++blk) {
+    // PF: the next block's four 16 B loads are issued before this block's compression, so
+    // with one wave per SIMD their latency overlaps the round chain
+    const uint64_t nfast = PF ? min(nfull, m.avail / 64) : 0;  // blocks wholly inside the real bytes
+    u32x4 nx[4];
+    if (nfast) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            nx[q] = *reinterpret_cast<const u32x4_u *>(p + 16 * q);
+    }
+    for (uint64_t blk = 0; blk < nfast; ++blk) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            w[4 * q + 0] = __builtin_bswap32(nx[q].x);
+            w[4 * q + 1] = __builtin_bswap32(nx[q].y);
+            w[4 * q + 2] = __builtin_bswap32(nx[q].z);
+            w[4 * q + 3] = __builtin_bswap32(nx[q].w);
+        }
+        if (blk + 1 < nfast) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                nx[q] = *reinterpret_cast<const u32x4_u *>(p + (blk + 1) * 64 + 16 * q);
+        }
+        sha1_compress(h, w);
+    }
+    for (uint64_t blk = nfast; blk < nfull; ++blk) {
         const uint64_t o = blk * 64;
         if (o + 64 <= m.avail) {
 #pragma unroll
@@ -898,8 +933,12 @@ int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDe
 {
     if (nmsgs == 0)
         return hipSuccess;
-    return launch(sec_sha1_kernel, dim3((nmsgs + 63) / 64), dim3(64), (hipStream_t)stream, base0, base1, msgs, nmsgs,
-                  digests);
+    const bool pf = SEC_SHA1_PF >= 0 ? SEC_SHA1_PF != 0 : nmsgs < kSha1PrefetchMsgs;
+    if (pf)
+        return launch(sec_sha1_kernel<true>, dim3((nmsgs + 63) / 64), dim3(64), (hipStream_t)stream, base0, base1, msgs,
+                      nmsgs, digests);
+    return launch(sec_sha1_kernel<false>, dim3((nmsgs + 63) / 64), dim3(64), (hipStream_t)stream, base0, base1, msgs,
+                  nmsgs, digests);
 }
 
 int sec_launch_decode_tail(const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,

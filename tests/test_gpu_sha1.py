@@ -42,6 +42,27 @@ def test_sha1_device_with_zero_tail(engine):
     assert [got[20 * i:20 * i + 20] for i in range(64)] == expect
 
 
+@pytest.mark.parametrize("nmsgs", [65535, 70001])
+def test_sha1_device_both_kernel_paths(engine, nmsgs):
+    """Below 65536 messages the kernel prefetches each next block, from there on it does not
+    (kernels.hip kSha1PrefetchMsgs): both paths, with zero tails, against hashlib on a sample."""
+    rng = np.random.default_rng(nmsgs)
+    buf = torch.from_numpy(rng.integers(0, 256, 1 << 20, dtype=np.uint8)).cuda()
+    host = buf.cpu().numpy().tobytes()
+    off = rng.integers(0, 1 << 19, nmsgs)
+    ln = rng.integers(0, 1000, nmsgs)
+    av = np.where(np.arange(nmsgs) % 3 == 0, rng.integers(0, 1000, nmsgs) % (ln + 1), ln)
+    msgs = np.zeros(nmsgs, dtype=MSG_DTYPE)
+    msgs["addr"] = buf.data_ptr() + off.astype(np.uint64)
+    msgs["len"], msgs["avail"] = ln, av
+    dig = torch.empty(nmsgs * 20, dtype=torch.uint8, device="cuda")
+    engine.sha1_batch(msgs, dig)
+    got = dig.cpu().numpy().reshape(-1, 20)
+    for i in list(range(0, nmsgs, 97)) + [nmsgs - 1]:
+        o, n, a = int(off[i]), int(ln[i]), int(av[i])
+        assert got[i].tobytes() == hashlib.sha1(host[o:o + a] + b"\0" * (n - a)).digest(), i
+
+
 @pytest.mark.parametrize("k,m", [(1, 2), (2, 3), (4, 6), (10, 14), (8, 11)])
 def test_encode_digest_host_matches_hashlib(engine, k, m):
     rng = random.Random(k * 31 + m)

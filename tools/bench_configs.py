@@ -186,6 +186,11 @@ def sha1_case(eng, nch=1024, n=1 << 20, k=4, m=6, reps=5):
     t_enc = timed(lambda: eng.encode_batch(ed, src, par), reps)
     t_both = timed(lambda: eng.encode_digest_batch(ed, src, par, dig), reps)
     hsrc = src.cpu().numpy()
+    hd, hp = dig.cpu().numpy().reshape(-1, 20), par.cpu().numpy()
+    for i in (0, 1, nch * m - 1):  # a fast wrong digest is not a result
+        c, j = divmod(i, m)
+        piece = hsrc[c * n + j * B:c * n + (j + 1) * B] if j < k else hp[(c * (m - k) + j - k) * B:(c * (m - k) + j - k + 1) * B]
+        assert hd[i].tobytes() == hashlib.sha1(piece.tobytes()).digest(), i
     hpar = np.empty(nch * (m - k) * B, dtype=np.uint8)
     hdig = np.empty(nch * m * 20, dtype=np.uint8)
     t_host = timed(lambda: eng.encode_digest_batch(ed, hsrc, hpar, hdig, host=True), 2)
