@@ -692,16 +692,19 @@ __device__ __forceinline__ void sha1_compress(u32 (&h)[5], u32 (&w)[16])
 }
 
 // byte i of the message: real below `avail`, zero from there to `len`
-// Batches of fewer than kSha1PrefetchMsgs messages (under one wave per SIMD) load each next
-// block before compressing the current one: with no other wave on the SIMD the loads'
-// latency was exposed per block.  C2's 6144 pieces of 256 KiB: 6.30-6.44 -> 5.07 ms; C4's
-// 114688 short pieces, which have waves to switch to, measured 6-22 % slower with it
-// (registers), so they keep the plain loop (profiles/r01_sha1_prefetch.jsonl).
-// SEC_SHA1_PF = 0 / 1 forces it off / on (A/B).
+// Batches of fewer than kSha1PrefetchMsgs messages (under one wave per SIMD) load blocks
+// SEC_SHA1_DEPTH ahead of their compression: with no other wave on the SIMD the loads'
+// latency was exposed per block.  C2's 6144 pieces of 256 KiB: 6.30 ms without, 5.07 one
+// block ahead, 4.71 two ahead (three 4.9, four 4.73).  C4's 114688 short pieces have waves
+// to switch to and keep the plain loop (profiles/r01_sha1_prefetch.jsonl).
+// SEC_SHA1_PF = 0 / 1 forces the prefetch off / on (A/B).
 #ifndef SEC_SHA1_PF
 #define SEC_SHA1_PF -1
 #endif
 constexpr uint32_t kSha1PrefetchMsgs = 65536;
+#ifndef SEC_SHA1_DEPTH
+#define SEC_SHA1_DEPTH 2
+#endif
 __device__ __forceinline__ u32 msg_byte(const u8 *p, uint64_t i, uint64_t avail) { return i < avail ? p[i] : 0u; }
 
 template <bool PF>
@@ -720,26 +723,36 @@ __global__ __launch_bounds__(64) void sec_sha1_kernel(const u8 *__restrict__ bas
     // PF: the next block's four 16 B loads are issued before this block's compression, so
     // with one wave per SIMD their latency overlaps the round chain
     const uint64_t nfast = PF ? min(nfull, m.avail / 64) : 0;  // blocks wholly inside the real bytes
-    u32x4 nx[4];
-    if (nfast) {
+    // SEC_SHA1_DEPTH blocks ahead (1 or 2), in a ring of registers walked by an unrolled loop
+    constexpr int D = SEC_SHA1_DEPTH;
+    u32x4 nx[D][4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-            nx[q] = *reinterpret_cast<const u32x4_u *>(p + 16 * q);
-    }
-    for (uint64_t blk = 0; blk < nfast; ++blk) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            w[4 * q + 0] = __builtin_bswap32(nx[q].x);
-            w[4 * q + 1] = __builtin_bswap32(nx[q].y);
-            w[4 * q + 2] = __builtin_bswap32(nx[q].z);
-            w[4 * q + 3] = __builtin_bswap32(nx[q].w);
-        }
-        if (blk + 1 < nfast) {
+    for (int d = 0; d < D; ++d)
+        if ((uint64_t)d < nfast) {
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                nx[q] = *reinterpret_cast<const u32x4_u *>(p + (blk + 1) * 64 + 16 * q);
+                nx[d][q] = *reinterpret_cast<const u32x4_u *>(p + d * 64 + 16 * q);
         }
-        sha1_compress(h, w);
+    for (uint64_t b0 = 0; b0 < nfast; b0 += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const uint64_t blk = b0 + d;
+            if (blk < nfast) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    w[4 * q + 0] = __builtin_bswap32(nx[d][q].x);
+                    w[4 * q + 1] = __builtin_bswap32(nx[d][q].y);
+                    w[4 * q + 2] = __builtin_bswap32(nx[d][q].z);
+                    w[4 * q + 3] = __builtin_bswap32(nx[d][q].w);
+                }
+                if (blk + D < nfast) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        nx[d][q] = *reinterpret_cast<const u32x4_u *>(p + (blk + D) * 64 + 16 * q);
+                }
+                sha1_compress(h, w);
+            }
+        }
     }
     for (uint64_t blk = nfast; blk < nfull; ++blk) {
         const uint64_t o = blk * 64;

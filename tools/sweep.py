@@ -54,6 +54,9 @@ VARIANTS = {
     "lb256": {"SEC_LB_WIDE_ROWS": 256},
     "sha1pf": {"SEC_SHA1_PF": 1},  # SHA-1 next-block prefetch forced on / off (default: < 65536 messages)
     "sha1nopf": {"SEC_SHA1_PF": 0},
+    "sha1d1": {"SEC_SHA1_DEPTH": 1},  # prefetch depth in blocks (default 2)
+    "sha1d3": {"SEC_SHA1_DEPTH": 3},
+    "sha1d4": {"SEC_SHA1_DEPTH": 4},
     "lb256p8": {"SEC_LB_WIDE_ROWS": 256, "SEC_PAIR_ROWS": 8},
     "lb512p8": {"SEC_LB_WIDE_ROWS": 512, "SEC_PAIR_ROWS": 8},
 }
