@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident RS encode + decode of 1 MiB chunks on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-seconds S]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-seconds S] [--workload c2c3|c4]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -12,16 +12,25 @@ one step = encode all 1024 chunks + decode/reassemble all 1024 chunks with data 
 HBM before the timed region.  value = (chunk bytes encoded + chunk bytes decoded) by all
 ranks / max-over-ranks wall time, in GiB/s (2^30 B).
 
-Also reported on the same line:
-  roofline      the encode kernel (the dominant, BASELINE-target kernel): algorithmic bytes
-                per launch (n read + (m-k)*B written = 1.5 MiB per chunk) / average launch
-                time from HIP events on the launch stream, vs 8 TB/s HBM peak; `traffic` =
-                rocprofv3 PMC bytes per launch from profiles/ (FETCH_SIZE x2 + WRITE_SIZE,
-                gfx950 correction) when a matching summary is committed, else null
+--workload c4 (BASELINE configs[3]; not the headline line): 65536 x 64 KiB chunks, RS(10,4), split
+over the ranks by storb_amd.dist.partition (8192 per GPU at N = 8; the whole job on one GPU at
+N = 1), strong scaling: value = job bytes encoded per step / max-over-ranks time.  Decode
+(blocks {0,2,5,7} erased, the padded block 9 read in place) is timed after the timed region.
+
+Also reported on the headline line:
+  roofline      the decode kernel, the dominant one by time: algorithmic bytes per launch
+                (k*B read + n written = 2 MiB per chunk) / average launch time from HIP events
+                on the launch stream, vs 8 TB/s HBM peak; `traffic` = rocprofv3 PMC bytes per
+                launch from profiles/ (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction) when a
+                matching summary is committed, else null
+  encode_kernel the same for the encode kernel, the north star's target (n read + (m-k)*B
+                written = 1.5 MiB per chunk)
   cpu_baseline  oracle/fec_oracle.c (C restatement of zfec's fec.c: 64 KiB LUT, 8 KiB
                 strides) on a bounded sample of the same workload, rank 0 at N=1: one chunk
                 per task on min(16, usable cores) threads (`value`, `cores`), and 1 thread
                 (`single_thread_value`), --cpu-seconds each
+  decode_recover_only_kernel  the same decode with SEC_F_RECOVER (only the 2 missing primaries
+                written: k*B read + e*B written per chunk), after the timed region
   e2e           host-buffer encode+decode through the C ABI incl. PCIe: pageable buffers
                 (page-locked per call, or staged through pinned slabs) and pinned buffers
                 (zero-copy) — reported beside `value`, never as it
@@ -58,6 +67,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--workload", choices=("c2c3", "c4"), default="c2c3",
+                    help="c2c3: the headline line (BASELINE configs[1]+[2], weak scaling); c4: configs[3], "
+                         "65536 x 64 KiB RS(10,4) encode split over the ranks (strong scaling)")
+    ap.add_argument("--c4-chunks", type=int, default=65536, help="c4: chunks in the whole job (default 65536)")
     ap.add_argument("--no-events", action="store_true",
                     help="A/B only: no per-launch HIP events in the timed region (roofline fields then null)")
     return ap.parse_args()
@@ -79,20 +92,20 @@ def enc_descs(nchunks, n, k, m, pstride=None):
     return d, B
 
 
-def dec_descs(nchunks, n, k, m, B, data_base, par_base, erased, pstride=None):
+def dec_descs(nchunks, n, k, m, B, data_base, par_base, erased, pstride=None, recover=False):
     """Decode descriptors whose surviving blocks are read in place from the encode buffers.
 
-    The C ABI needs B readable bytes per block; an in-place data block k-1 is short when
-    padlen > 0 (zfec's padded copy is not in the chunk buffer), so it must be erased then.
-    """
+    Returns (descs, sharenums, block_offs, block_avail): an in-place data block k-1 is short
+    when padlen > 0 (zfec's padded copy is not in the chunk buffer), so its avail is B - padlen
+    (sec_decode_batch_ex reads the rest as zero).  recover: out_off for SEC_F_RECOVER output
+    (e*B per chunk)."""
     from storb_amd._lib import DEC_DTYPE
 
     ps = pstride or B
-    if B * k != n and (k - 1) not in erased:
-        raise ValueError("padded last data block cannot be read in place: erase block k-1")
     keep = [s for s in range(m) if s not in erased][:k]
+    e = sum(1 for s in range(k) if s not in keep)
     d = np.zeros(nchunks, dtype=DEC_DTYPE)
-    d["out_off"] = np.arange(nchunks, dtype=np.uint64) * n
+    d["out_off"] = np.arange(nchunks, dtype=np.uint64) * (e * B if recover else n)
     d["B"] = B
     d["padlen"] = B * k - n
     d["slot0"] = np.arange(nchunks, dtype=np.uint64) * k
@@ -100,20 +113,24 @@ def dec_descs(nchunks, n, k, m, B, data_base, par_base, erased, pstride=None):
     d["m"] = m
     sn = np.tile(np.array(keep, np.int32), nchunks)
     offs = np.zeros(nchunks * k, np.uint64)
+    avail = np.full(nchunks * k, B, np.uint64)
     ci = np.arange(nchunks, dtype=np.uint64)
     for j, s in enumerate(keep):
         offs[j::k] = (data_base + ci * n + s * B) if s < k else (par_base + ci * (m - k) * ps + (s - k) * ps)
-    return d, sn, offs
+        if s == k - 1:
+            avail[j::k] = n - (k - 1) * B
+    return d, sn, offs, avail
 
 
-def load_traffic():
-    """Per-launch HBM bytes of the encode kernel from a committed rocprofv3 PMC summary."""
+def load_traffic(kind: str):
+    """Per-launch HBM bytes of the encode / decode kernel from the committed rocprofv3 PMC summary
+    (profiles/pmc_encode_c2.json: FETCH_SIZE x 2 + WRITE_SIZE on this workload)."""
     path = os.path.join(ROOT, "profiles", "pmc_encode_c2.json")
     try:
         with open(path) as f:
             j = json.load(f)
-        if j.get("workload") == "c2" and j.get("hbm_bytes_per_launch"):
-            return float(j["hbm_bytes_per_launch"])
+        if j.get("workload") == "c2" and j.get(kind, {}).get("hbm_bytes_per_launch"):
+            return float(j[kind]["hbm_bytes_per_launch"])
     except (OSError, ValueError):
         pass
     return None
@@ -185,8 +202,55 @@ def cpu_baseline(seconds: float) -> dict:
                       f"oracle/fec_oracle.c (zfec fec.c restatement: 64 KiB LUT, 8 KiB strides)"}
 
 
+def timed_region(dmod, local, sync, steps, body):
+    """The contract's timed region: barrier + device sync on both sides of exactly `steps`
+    calls of body(); returns the max over ranks of the elapsed seconds."""
+    from storb_amd import dist as D
+
+    D.barrier(dmod, local)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        body()
+    sync()
+    D.barrier(dmod, local)
+    return D.max_over_ranks(dmod, time.perf_counter() - t0, local)
+
+
+def kernel_avg_s(eng, kind):
+    ms, n = eng.collect_timing(kind)
+    return (ms / 1e3 / n) if n else float("nan"), n
+
+
+def recover_only_rate(eng, torch, src, par, nchunks, n, k, m, B, reps=10) -> dict:
+    """SEC_F_RECOVER on the same blocks as the bench decode: only the e = 2 missing primaries
+    are written (zfec fec_decode's own output).  Algorithmic bytes: k*B read + e*B written."""
+    e = sum(1 for s in range(k) if s in ERASED)
+    dd, sn, offs, av = dec_descs(nchunks, n, k, m, B, src.data_ptr(), par.data_ptr(), ERASED, recover=True)
+    rec = torch.empty(nchunks * e * B, dtype=torch.uint8, device=src.device)
+    eng.decode_batch(dd, sn, offs, 0, rec, block_avail=av, recover_only=True)
+    s3 = src.view(nchunks, k, B)
+    r3 = rec.view(nchunks, e, B)
+    for j, blk in enumerate(sorted(s for s in ERASED if s < k)):
+        if not torch.equal(r3[:, j], s3[:, blk]):
+            bad = (r3[:, j] != s3[:, blk]).any(dim=1).nonzero().flatten().tolist()
+            raise SystemExit(f"bench: recover-only mismatch in row {j}: {len(bad)} chunks, first {bad[:8]}; "
+                             f"{r3[bad[0], j, :8].tolist()} vs {s3[bad[0], blk, :8].tolist()}")
+    eng.set_timing(True)
+    for _ in range(reps):
+        eng.decode_batch(dd, sn, offs, 0, rec, block_avail=av, recover_only=True, asynchronous=True)
+    eng.sync()
+    eng.set_timing(False)
+    t, nl = kernel_avg_s(eng, "decode")
+    alg = nchunks * (k + e) * B
+    return {"achieved": round(alg / t / 1e9, 1), "unit": "GB/s", "algorithmic_bytes_per_launch": alg,
+            "avg_launch_ms": round(t * 1e3, 4), "launches": nl}
+
+
 def main():
     args = parse()
+    if args.workload == "c4":
+        return main_c4(args)
     import torch
 
     from storb_amd import dist as D
@@ -206,11 +270,11 @@ def main():
     ed, B = enc_descs(N_CHUNKS, n, k, m)
     par = torch.empty(N_CHUNKS * (m - k) * B, dtype=torch.uint8, device=f"cuda:{local}")
     out = torch.empty_like(src)
-    dd, sn, offs = dec_descs(N_CHUNKS, n, k, m, B, src.data_ptr(), par.data_ptr(), ERASED)
+    dd, sn, offs, av = dec_descs(N_CHUNKS, n, k, m, B, src.data_ptr(), par.data_ptr(), ERASED)
 
     def step():
         eng.encode_batch(ed, src, par, asynchronous=True)
-        eng.decode_batch(dd, sn, offs, 0, out, asynchronous=True)
+        eng.decode_batch(dd, sn, offs, 0, out, block_avail=av, asynchronous=True)
 
     for _ in range(args.warmup):
         step()
@@ -219,29 +283,18 @@ def main():
         raise SystemExit("bench: decode round trip mismatch")
 
     eng.set_timing(not args.no_events)
-    D.barrier(dmod, local)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    eng.sync()
-    torch.cuda.synchronize()
-    D.barrier(dmod, local)
-    el = time.perf_counter() - t0
+    el_max = timed_region(dmod, local, torch.cuda.synchronize, args.steps, step)
     eng.set_timing(False)
-    enc_ms, enc_n = eng.collect_timing("encode")
-    dec_ms, dec_n = eng.collect_timing("decode")
-    el_max = D.max_over_ranks(dmod, el, local)
+    enc_avg_s, enc_n = kernel_avg_s(eng, "encode")
+    dec_avg_s, dec_n = kernel_avg_s(eng, "decode")
 
     bytes_per_step = 2 * N_CHUNKS * n  # encoded + decoded chunk bytes
     value = world * args.steps * bytes_per_step / el_max / GIB
 
     enc_alg = N_CHUNKS * (n + (m - k) * B)  # bytes per encode launch
     dec_alg = N_CHUNKS * (k * B + n)  # reassemble: k blocks read + n written
-    enc_avg_s = enc_ms / 1e3 / max(enc_n, 1) or float("nan")
-    dec_avg_s = dec_ms / 1e3 / max(dec_n, 1) or float("nan")
     enc_gbs = enc_alg / enc_avg_s / 1e9
-    traffic = load_traffic()
+    dec_gbs = dec_alg / dec_avg_s / 1e9
 
     res = None
     if rank == 0:
@@ -262,18 +315,21 @@ def main():
                                    "decode/reassemble with data shards {1,3} erased",
                        "chunks_per_gpu": N_CHUNKS, "chunk_bytes": n, "k": k, "m_total": m,
                        "bytes_per_step_per_gpu": bytes_per_step, "parallelism": f"chunk-partition x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(enc_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(enc_gbs / PEAK_HBM_GBS, 4),
-                         "traffic": traffic,
-                         "kernel": "sec_encode_kernel<2, 1, false>",
-                         "algorithmic_bytes_per_launch": enc_alg,
-                         "avg_launch_ms": round(enc_avg_s * 1e3, 4), "launches": enc_n},
-            "decode_kernel": {"achieved": round(dec_alg / dec_avg_s / 1e9, 1), "unit": "GB/s",
-                              "algorithmic_bytes_per_launch": dec_alg, "avg_launch_ms": round(dec_avg_s * 1e3, 4),
-                              "launches": dec_n},
+            # the dominant kernel by time is the decode (it moves 2 MiB per chunk to encode's 1.5)
+            "roofline": {"bound": "hbm", "achieved": round(dec_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(dec_gbs / PEAK_HBM_GBS, 4), "traffic": load_traffic("decode"),
+                         "kernel": "sec_decode_kernel<2, 1, false>", "algorithmic_bytes_per_launch": dec_alg,
+                         "avg_launch_ms": round(dec_avg_s * 1e3, 4), "launches": dec_n},
+            # the north star's target kernel (>= 70 % of HBM roofline on C2 encode)
+            "encode_kernel": {"achieved": round(enc_gbs, 1), "unit": "GB/s", "frac": round(enc_gbs / PEAK_HBM_GBS, 4),
+                              "traffic": load_traffic("encode"), "kernel": "sec_encode_kernel<2, 1, false>",
+                              "algorithmic_bytes_per_launch": enc_alg, "avg_launch_ms": round(enc_avg_s * 1e3, 4),
+                              "launches": enc_n},
             "encode_gibs": round(N_CHUNKS * n / enc_avg_s / GIB, 2),
             "decode_gibs": round(N_CHUNKS * n / dec_avg_s / GIB, 2),
         }
+        if not args.no_events:  # after the timed region; not part of `value`
+            res["decode_recover_only_kernel"] = recover_only_rate(eng, torch, src, par, N_CHUNKS, n, k, m, B)
 
     # host-buffer (PCIe-inclusive) rate: reported, never `value`
     if rank == 0 and world == 1 and not args.no_e2e:
@@ -289,9 +345,122 @@ def main():
         dmod.destroy_process_group()
 
 
+# ---------------------------------------------------------------- BASELINE configs[3] (C4)
+C4_CHUNKS, C4_CHUNK, C4_K, C4_M = 65536, 65536, 10, 14
+C4_ERASED = (0, 2, 5, 7)  # block 9 (zfec's padded last data block) survives and is read in place
+
+
+def c4_share(rank: int, world: int, nchunks: int = C4_CHUNKS) -> tuple[int, int]:
+    """This rank's contiguous chunk range of the C4 job (storb_amd.dist.partition by bytes)."""
+    from storb_amd import dist as D
+
+    return D.partition([C4_CHUNK] * nchunks, world)[rank]
+
+
+def c4_run(eng, dmod, rank, world, local, device, sync, steps, warmup, nchunks=C4_CHUNKS, verify=True,
+           keep=False):
+    """C4 as BASELINE.json writes it: `nchunks` x 64 KiB RS(10,4) chunks split over the ranks
+    (contiguous ranges, no data-path collective); each rank encodes its share on its device.
+    Returns this rank's numbers plus the job's aggregate (max-over-ranks time, summed chunks).
+    `eng` needs encode_batch / decode_batch / sync / set_timing / collect_timing (the product
+    Engine; tests/test_dist.py drives it with a stand-in on CPU tensors)."""
+    import torch
+
+    from storb_amd import dist as D
+
+    lo, hi = c4_share(rank, world, nchunks)
+    nch, n, k, m = hi - lo, C4_CHUNK, C4_K, C4_M
+    g = torch.Generator(device=device)
+    g.manual_seed(4_000_003 + lo)  # seed 4, per share
+    src = torch.randint(0, 256, (max(nch * n, 1),), dtype=torch.uint8, device=device, generator=g)
+    ed, B = enc_descs(nch, n, k, m)
+    par = torch.empty(max(nch * (m - k) * B, 1), dtype=torch.uint8, device=device)
+    out = torch.empty_like(src)
+    dd, sn, offs, av = dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), C4_ERASED)
+
+    def step():
+        eng.encode_batch(ed, src, par, asynchronous=True)
+
+    for _ in range(warmup):
+        step()
+    eng.sync()
+    if verify:  # every chunk: 4 data blocks erased, recovered from parity, block 9 in place
+        eng.decode_batch(dd, sn, offs, 0, out, block_avail=av)
+        if not torch.equal(out, src):
+            raise SystemExit(f"bench c4: rank {rank} round trip mismatch")
+    eng.set_timing(True)
+    el_max = timed_region(dmod, local, sync, steps, step)
+    eng.set_timing(False)
+    enc_avg_s, enc_n = kernel_avg_s(eng, "encode")
+    # decode (reassemble) of the share, after the timed region: reported beside `value`
+    eng.set_timing(True)
+    for _ in range(max(steps // 2, 1)):
+        eng.decode_batch(dd, sn, offs, 0, out, block_avail=av, asynchronous=True)
+    eng.sync()
+    eng.set_timing(False)
+    dec_avg_s, dec_n = kernel_avg_s(eng, "decode")
+    total_chunks = int(D.sum_over_ranks(dmod, float(nch), local))
+    counts = [int(D.sum_over_ranks(dmod, float(nch if r == rank else 0), local)) for r in range(world)]
+    res = {"lo": lo, "hi": hi, "chunks": nch, "B": B, "el_max": el_max, "total_chunks": total_chunks,
+           "per_rank_chunks": counts, "enc_avg_s": enc_avg_s, "enc_launches": enc_n, "dec_avg_s": dec_avg_s,
+           "dec_launches": dec_n}
+    if keep:  # the buffers, for tests that compare samples against the oracle
+        res.update(src=src, par=par)
+    return res
+
+
+def main_c4(args):
+    import torch
+
+    from storb_amd import dist as D
+    from storb_amd.engine import Engine
+
+    rank, local, world = D.rank_env()
+    local = int(os.environ.get("STORB_BENCH_DEVICE", local))
+    torch.cuda.set_device(local)
+    dmod = D.init(os.environ.get("STORB_DIST_BACKEND") or None)
+    eng = Engine(local)
+    r = c4_run(eng, dmod, rank, world, local, f"cuda:{local}", torch.cuda.synchronize, args.steps, args.warmup,
+               nchunks=args.c4_chunks)
+    n, k, m, B = C4_CHUNK, C4_K, C4_M, r["B"]
+    job_bytes = r["total_chunks"] * n
+    value = args.steps * job_bytes / r["el_max"] / GIB
+    enc_alg = r["chunks"] * (n + (m - k) * B)
+    dec_alg = r["chunks"] * (k * B + n)
+    if rank == 0:
+        enc_gbs = enc_alg / r["enc_avg_s"] / 1e9
+        res = {
+            "metric": "GiB/s device-resident RS(10,4) encode, 65536 x 64 KiB chunks sharded across N MI355X",
+            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(r["el_max"] / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (torch.randint uniform bytes, seed 4 per share), HBM-resident",
+            "config": {"workload": f"BASELINE configs[3]: {r['total_chunks']} x 64 KiB chunks, RS(k=10,m=4)="
+                                   "zfec(10,14), B = 6554, padlen 4, encode; chunks split by "
+                                   "storb_amd.dist.partition over the ranks, no data-path collective",
+                       "chunks_total": r["total_chunks"], "per_rank_chunks": r["per_rank_chunks"],
+                       "world_size": world,
+                       "backend": dmod.get_backend() if dmod is not None else None,
+                       "parallelism": f"chunk-partition x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(enc_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(enc_gbs / PEAK_HBM_GBS, 4), "traffic": None,
+                         "kernel": "sec_encode_kernel<4, 1, false>", "algorithmic_bytes_per_launch": enc_alg,
+                         "avg_launch_ms": round(r["enc_avg_s"] * 1e3, 4), "launches": r["enc_launches"]},
+            "decode_kernel": {"achieved": round(dec_alg / r["dec_avg_s"] / 1e9, 1), "unit": "GB/s",
+                              "erased": list(C4_ERASED), "block_9": "read in place, avail = B - padlen",
+                              "algorithmic_bytes_per_launch": dec_alg,
+                              "avg_launch_ms": round(r["dec_avg_s"] * 1e3, 4), "launches": r["dec_launches"]},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(res), flush=True)
+    eng.close()
+    if dmod is not None:
+        dmod.destroy_process_group()
+
+
 def _e2e_pass(eng, host, par, out, nchunks, steps):
     ed, B = enc_descs(nchunks, CHUNK, K, M)
-    dd, sn, offs = dec_descs(nchunks, CHUNK, K, M, B, host.ctypes.data, par.ctypes.data, ERASED)
+    dd, sn, offs, _ = dec_descs(nchunks, CHUNK, K, M, B, host.ctypes.data, par.ctypes.data, ERASED)
     eng.encode_batch(ed, host, par, host=True)
     eng.decode_batch(dd, sn, offs, 0, out, host=True)
     if not np.array_equal(out, host):

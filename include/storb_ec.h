@@ -74,6 +74,12 @@ enum sec_status {
                           sec_ctx_host_paths counts which path each call took        */
 #define SEC_F_ASYNC 2u /* device pointers only: return once enqueued on the context
                           stream (sec_sync() waits)                                  */
+#define SEC_F_RECOVER 4u /* decode only, recover-only: write just the chunk's missing
+                          primaries, i.e. what zfec's fec_decode itself produces: the
+                          e = (primaries absent from the chunk's k blocks) recovered
+                          blocks, B bytes each (block k-1 with its zero padding), in
+                          increasing block number at out + out_off + r*B.  Present
+                          primaries are not copied; a chunk with e = 0 writes nothing  */
 
 typedef struct sec_ctx sec_ctx;
 
@@ -143,11 +149,21 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
  * sharenums[slot0 + i]; the chunk's k*B - padlen bytes are written at
  * out + out_off.  Present primaries are copied, missing ones recovered.
  * `blocks` may be NULL, in which case block_offs are absolute addresses.
- * Every block must have B readable bytes: data block k-1 is zfec's zero-padded
- * copy, so a chunk buffer read in place does not provide it when padlen > 0. */
+ * Every block must have B readable bytes here; sec_decode_batch_ex lifts that.
+ * SEC_F_RECOVER: recover-only output instead (see the flag). */
 int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
                      const int32_t *sharenums, const uint64_t *block_offs,
                      const uint8_t *blocks, uint8_t *out, unsigned flags);
+
+/* sec_decode_batch with a readable length per block: block_avail[slot0 + i] bytes
+ * of block i exist at its address and bytes [avail, B) read as zero (values
+ * above B count as B; block_avail NULL = every block has B).  This is zfec's
+ * padded last data block read in place from the chunk buffer: avail = B - padlen
+ * (the same mechanism as sec_msg.avail).  Nothing past a block's avail is read. */
+int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
+                        const int32_t *sharenums, const uint64_t *block_offs,
+                        const uint64_t *block_avail, const uint8_t *blocks, uint8_t *out,
+                        unsigned flags);
 
 /* ---- piece ids: SHA-1 (piece_hash, /root/reference/storb/util/piece.py:54-68) ----
  * A message is `len` bytes at `addr`, of which the first `avail` exist in

@@ -34,6 +34,7 @@ SEC_ENOCRT = -15
 
 SEC_F_HOST = 1
 SEC_F_ASYNC = 2
+SEC_F_RECOVER = 4
 
 # zfec precondition failures (raised by zfec as zfec.Error)
 PRECONDITION_CODES = {SEC_EKM, SEC_EBLOCKLEN, SEC_ENBLOCKS, SEC_ESHARENUM, SEC_EDUPSHARE, SEC_EPADLEN, SEC_ESIZE}
@@ -83,6 +84,7 @@ _SIGS = {
     "sec_decode_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
     "sec_encode_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint]),
     "sec_decode_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp, ctypes.c_uint]),
+    "sec_decode_batch_ex": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint]),
     "sec_sha1_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, ctypes.c_uint]),
     "sec_encode_digest_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_uint]),
     "sec_bn_key_create": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(_vp)]),

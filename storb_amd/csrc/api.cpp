@@ -134,7 +134,7 @@ struct Group {
 struct SubPlan {
     int64_t c0 = 0, c1 = 0;  // chunk range
     std::vector<Group> groups;
-    size_t off_desc = 0, off_tiles = 0, off_tail = 0, off_soff = 0, off_srow = 0, off_mrow = 0;
+    size_t off_desc = 0, off_tiles = 0, off_tail = 0, off_soff = 0, off_srow = 0, off_mrow = 0, off_savail = 0;
     uint32_t ntail = 0;
     uint64_t in_bytes = 0, out_bytes = 0;  // dense slab sizes (host mode)
     size_t off_msgs = 0;                   // messages of this unit (SHA-1, bignum)
@@ -744,8 +744,27 @@ DecLayout dec_layout(const sec_dec_chunk *chunks, int64_t nchunks, const int32_t
     return L;
 }
 
+// Readable bytes of caller slot `j` of chunk c (sec_decode_batch_ex's block_avail; B if none).
+uint64_t slot_avail(const sec_dec_chunk &c, const uint64_t *block_avail, int j)
+{
+    return block_avail ? std::min<uint64_t>(block_avail[c.slot0 + j], c.B) : c.B;
+}
+
+// Output bytes of a decode chunk: the reassembled chunk, or (recover-only) its e recovered
+// blocks.  e = primaries absent from its sharenums.
+uint64_t dec_nout(const sec_dec_chunk &c, const int32_t *sharenums, bool recover)
+{
+    if (!recover)
+        return (uint64_t)c.k * c.B - c.padlen;
+    uint64_t present = 0;
+    for (int j = 0; j < c.k; ++j)
+        present += sharenums[c.slot0 + j] < c.k;
+    return ((uint64_t)c.k - present) * c.B;
+}
+
+// block_avail: nullable (device / zero-copy mode only: staged slots are zero-filled to B)
 int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const uint64_t *block_offs,
-                      const DecLayout &L, bool host)
+                      const uint64_t *block_avail, const DecLayout &L, bool host, bool recover)
 {
     Plan &plan = ctx->dec_plan;
     TableCache &tc = ctx->dec_tabs;
@@ -815,7 +834,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         sp.c1 = c1;
         std::vector<sec::DecDesc> descs((size_t)(c1 - c0));
         std::vector<uint64_t> soff;
-        std::vector<uint32_t> srow, mrow;
+        std::vector<uint32_t> srow, mrow, savail;
         Bins bins;
         std::vector<sec::TailItem> tail;
         for (int64_t i = c0; i < c1; ++i) {
@@ -824,17 +843,25 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             const int *idx = &L.idx[base];
             const uint32_t slot0 = (uint32_t)soff.size();
             std::vector<uint32_t> mr;
+            uint64_t min_avail = c.B;
             for (int s = 0; s < c.k; ++s) {
                 const int from = L.perm[base + s];
                 soff.push_back(host ? sp.in_bytes + (uint64_t)s * c.B : block_offs[c.slot0 + from]);
-                srow.push_back(idx[s] < c.k ? (uint32_t)idx[s] : 0xFFFFFFFFu);
+                // recover-only: no copies, and recovered row r goes to output row r
+                srow.push_back(!recover && idx[s] < c.k ? (uint32_t)idx[s] : 0xFFFFFFFFu);
+                const uint64_t av = host ? c.B : slot_avail(c, block_avail, from);
+                savail.push_back((uint32_t)av);
+                min_avail = std::min(min_avail, av);
                 if (idx[s] >= c.k)
-                    mr.push_back((uint32_t)s);
+                    mr.push_back(recover ? (uint32_t)mr.size() : (uint32_t)s);
             }
             mr.resize((size_t)c.k, 0);
             mrow.insert(mrow.end(), mr.begin(), mr.end());
-            const uint64_t nout = (uint64_t)c.k * c.B - c.padlen;
-            const int64_t valid = (int64_t)nout - (int64_t)(c.k - 1) * (int64_t)c.B;
+            const uint64_t nout = recover ? (uint64_t)e_of[i] * c.B : (uint64_t)c.k * c.B - c.padlen;
+            // positions below `valid`: every output row writable (the last one is the shortest)
+            // and every slot readable; [valid, B) goes byte by byte, reading past avail as zero
+            const int64_t valid = std::min<int64_t>(
+                recover ? (int64_t)c.B : (int64_t)nout - (int64_t)(c.k - 1) * (int64_t)c.B, (int64_t)min_avail);
             sec::DecDesc &d = descs[i - c0];
             d.out_off = host ? sp.out_bytes : c.out_off;
             d.n = nout;
@@ -858,6 +885,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         sp.off_soff = img.put(soff.data(), soff.size() * 8);
         sp.off_srow = img.put(srow.data(), srow.size() * 4);
         sp.off_mrow = img.put(mrow.data(), mrow.size() * 4);
+        sp.off_savail = img.put(savail.data(), savail.size() * 4);
         plan.subs.push_back(std::move(sp));
     }
     RC(upload_plan(ctx, plan, img, tc, pending));
@@ -871,17 +899,16 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::DecDesc *dd = plan.meta.as<sec::DecDesc>(sp.off_desc);
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->dec_tabs.buf.as<uint32_t>();
-    const uint64_t *so = plan.meta.as<uint64_t>(sp.off_soff);
-    const uint32_t *sr = plan.meta.as<uint32_t>(sp.off_srow), *mr = plan.meta.as<uint32_t>(sp.off_mrow);
+    const sec::DecSlots sl{plan.meta.as<uint64_t>(sp.off_soff), plan.meta.as<uint32_t>(sp.off_srow),
+                           plan.meta.as<uint32_t>(sp.off_mrow), plan.meta.as<uint32_t>(sp.off_savail)};
     for (const Group &g : sp.groups) {
-        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, blocks, out, dd, dt + g.first, g.count, tabs, so, sr,
-                                  mr, s);
+        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, blocks, out, dd, dt + g.first, g.count, tabs, sl, s);
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_kernel");
     }
     if (sp.ntail) {
         int e = sec_launch_decode_tail(blocks, out, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs,
-                                       so, sr, mr, s);
+                                       sl, s);
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_tail");
     }
@@ -1350,15 +1377,16 @@ std::vector<HostRange> encode_ranges(const sec_enc_chunk *chunks, int64_t nchunk
     return r;
 }
 
-std::vector<HostRange> decode_ranges(const sec_dec_chunk *chunks, int64_t nchunks, const uint64_t *block_offs,
-                                     const uint8_t *blocks, const uint8_t *out)
+std::vector<HostRange> decode_ranges(const sec_dec_chunk *chunks, int64_t nchunks, const int32_t *sharenums,
+                                     const uint64_t *block_offs, const uint64_t *block_avail, const uint8_t *blocks,
+                                     const uint8_t *out, bool recover)
 {
     std::vector<HostRange> r;
     for (int64_t i = 0; i < nchunks; ++i) {
         const sec_dec_chunk &c = chunks[i];
-        r.push_back(HostRange{(uintptr_t)out + c.out_off, (uint64_t)c.k * c.B - c.padlen});
+        r.push_back(HostRange{(uintptr_t)out + c.out_off, dec_nout(c, sharenums, recover)});
         for (int j = 0; j < c.k; ++j)
-            r.push_back(HostRange{(uintptr_t)blocks + block_offs[c.slot0 + j], c.B});
+            r.push_back(HostRange{(uintptr_t)blocks + block_offs[c.slot0 + j], slot_avail(c, block_avail, j)});
     }
     return r;
 }
@@ -1904,14 +1932,22 @@ int sec_bn_mulmod_batch(sec_ctx *ctx, const sec_bn_key *key, const uint8_t *a, c
 int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const int32_t *sharenums,
                      const uint64_t *block_offs, const uint8_t *blocks, uint8_t *out, unsigned flags)
 {
+    return sec_decode_batch_ex(ctx, chunks, nchunks, sharenums, block_offs, nullptr, blocks, out, flags);
+}
+
+int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const int32_t *sharenums,
+                        const uint64_t *block_offs, const uint64_t *block_avail, const uint8_t *blocks, uint8_t *out,
+                        unsigned flags)
+{
     if (!ctx || nchunks < 0 || (nchunks > 0 && (!chunks || !sharenums || !block_offs)) ||
-        (flags & ~(SEC_F_HOST | SEC_F_ASYNC)))
+        (flags & ~(SEC_F_HOST | SEC_F_ASYNC | SEC_F_RECOVER)))
         return SEC_EINVAL;
     if (nchunks == 0)
         return SEC_OK;
     if (nchunks >= (int64_t)UINT32_MAX)
         return SEC_EINVAL;
     bool host = flags & SEC_F_HOST;
+    const bool recover = flags & SEC_F_RECOVER;
     RC(set_dev(ctx));
 
     // _fec.Decoder.decode / easyfec.Decoder.decode preconditions
@@ -1926,7 +1962,7 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
             return SEC_EPADLEN;
         RC(check_sharenums(c.k, c.m, sharenums + c.slot0));
         total_slots = std::max<uint64_t>(total_slots, c.slot0 + (uint64_t)c.k);
-        total_out += (uint64_t)c.k * c.B - c.padlen;
+        total_out += dec_nout(c, sharenums, recover);
     }
     if (total_out == 0)
         return SEC_OK;
@@ -1934,12 +1970,16 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         return SEC_EINVAL;
     // pinned (or lockable) caller buffers: the device path on them directly (see encode_impl)
     HostLock lock(ctx->stream());
-    if (host && host_direct(ctx, decode_ranges(chunks, nchunks, block_offs, blocks, out), lock)) {
+    if (host &&
+        host_direct(ctx, decode_ranges(chunks, nchunks, sharenums, block_offs, block_avail, blocks, out, recover),
+                    lock)) {
         host = false;
         flags &= ~(SEC_F_HOST | SEC_F_ASYNC);
     }
 
-    // Plan key (see sec_encode_batch): host mode keys on shapes + sharenums only.
+    // Plan key (see sec_encode_batch): host mode keys on shapes + sharenums only (its slots
+    // are staged densely, zero-filled past their avail); device mode on every descriptor,
+    // sharenum, block offset and avail.
     Plan &plan = ctx->dec_plan;
     std::vector<uint8_t> key;
     if (host) {
@@ -1955,12 +1995,16 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         }
     } else {
         const size_t kc = sizeof(sec_dec_chunk) * (size_t)nchunks;
-        key.resize(kc + total_slots * (4 + 8));
+        const size_t ka = block_avail ? total_slots * 8 : 0;
+        key.resize(kc + total_slots * (4 + 8) + ka);
         memcpy(key.data(), chunks, kc);
         memcpy(key.data() + kc, sharenums, total_slots * 4);
         memcpy(key.data() + kc + total_slots * 4, block_offs, total_slots * 8);
+        if (ka)
+            memcpy(key.data() + kc + total_slots * 12, block_avail, ka);
     }
-    const unsigned kflags = flags & ~SEC_F_ASYNC;  // ASYNC does not change the plan
+    // ASYNC does not change the plan; whether an avail array came does (0x10000)
+    const unsigned kflags = (flags & ~SEC_F_ASYNC) | (!host && block_avail ? 0x10000u : 0u);
     key.insert(key.end(), (const uint8_t *)&kflags, (const uint8_t *)&kflags + sizeof(unsigned));
     const bool reuse = plan.valid && plan.gen == ctx->dec_tabs.gen && plan.key == key;
     DecLayout L;
@@ -1968,7 +2012,7 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         L = dec_layout(chunks, nchunks, sharenums);
     if (!reuse) {
         plan.valid = false;
-        RC(build_decode_plan(ctx, chunks, nchunks, block_offs, L, host));
+        RC(build_decode_plan(ctx, chunks, nchunks, block_offs, block_avail, L, host, recover));
         plan.key.swap(key);
         plan.valid = true;
     }
@@ -1988,7 +2032,10 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
             const sec_dec_chunk &c = chunks[i];
             for (int s = 0; s < c.k; ++s) {
                 const int from = L.perm[L.first[i] + s];
-                jobs.push_back(sec::CopyJob{stage + o, blocks + block_offs[c.slot0 + from], c.B});
+                const uint64_t av = slot_avail(c, block_avail, from);
+                jobs.push_back(sec::CopyJob{stage + o, blocks + block_offs[c.slot0 + from], av});
+                if (av < c.B)  // the slot's bytes past its avail are zero
+                    jobs.push_back(sec::CopyJob{stage + o + av, nullptr, c.B - av});
                 o += c.B;
             }
         }
@@ -1997,7 +2044,7 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
         uint64_t o = 0;
         for (int64_t i = sp.c0; i < sp.c1; ++i) {
             const sec_dec_chunk &c = chunks[i];
-            const uint64_t nout = (uint64_t)c.k * c.B - c.padlen;
+            const uint64_t nout = dec_nout(c, sharenums, recover);
             jobs.push_back(sec::CopyJob{out + c.out_off, stage + o, nout});
             o += nout;
         }

@@ -18,9 +18,17 @@ namespace sec {
 
 struct CopyJob {
     void *dst;
-    const void *src;
+    const void *src;  // nullptr: zero-fill dst (a decode block's bytes past its avail)
     size_t len;
 };
+
+inline void copy_or_zero(void *dst, const void *src, size_t len)
+{
+    if (src)
+        memcpy(dst, src, len);
+    else
+        memset(dst, 0, len);
+}
 
 class CopyPool {
 public:
@@ -51,7 +59,7 @@ public:
         if (threads_.empty() || total < kInline) {
             for (const auto &j : jobs)
                 if (j.len)  // memcpy's pointers must be valid even for 0 bytes
-                    memcpy(j.dst, j.src, j.len);
+                    copy_or_zero(j.dst, j.src, j.len);
             return;
         }
         {
@@ -63,7 +71,7 @@ public:
             for (const auto &j : jobs)
                 for (size_t o = 0; o < j.len; o += kPiece) {
                     const size_t n = j.len - o < kPiece ? j.len - o : kPiece;
-                    pieces_.push_back(CopyJob{(char *)j.dst + o, (const char *)j.src + o, n});
+                    pieces_.push_back(CopyJob{(char *)j.dst + o, j.src ? (const char *)j.src + o : nullptr, n});
                 }
             next_.store(0);
             left_.store(pieces_.size());
@@ -85,7 +93,7 @@ private:
             const size_t i = next_.fetch_add(1);
             if (i >= pieces_.size())
                 return;
-            memcpy(pieces_[i].dst, pieces_[i].src, pieces_[i].len);
+            copy_or_zero(pieces_[i].dst, pieces_[i].src, pieces_[i].len);
             if (left_.fetch_sub(1) == 1) {
                 std::lock_guard<std::mutex> lk(mu_);
                 done_cv_.notify_all();

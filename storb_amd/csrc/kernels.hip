@@ -434,35 +434,34 @@ __global__ __launch_bounds__(256) void sec_encode_tail(const u8 *__restrict__ in
 // Slot c of a chunk holds block number idx[c]; primaries sit in their own slot
 // (zfec's normalisation).  Present primaries are copied to their output row;
 // the R missing rows of this tile's row group are XOR_c Minv[row][c] * slot_c.
-// Positions are < valid = the last output row's length, so every row is writable
-// and every slot (always B bytes) readable; the rest is decode_ragged's (Tile::ntail).
+// Positions are < valid = min(the last output row's length, every slot's avail), so every
+// row is writable and every slot readable there; the rest is decode_ragged's (Tile::ntail),
+// which reads a slot's bytes past its avail as zero (zfec's padded block k-1 read in place).
+// Recover-only decodes (SEC_F_RECOVER) use the same kernels: no copies (row = none) and the
+// recovered rows go to output rows 0..e-1.
 template <int R, int U, bool W>
 __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                             const sec::DecDesc &d, const sec::Tile &tl, u32 t,
-                                            const u32 *__restrict__ tabs, const u64 *__restrict__ slot_off,
-                                            const u32 *__restrict__ slot_row, const u32 *__restrict__ miss_row);
+                                            const u32 *__restrict__ tabs, const sec::DecSlots sl);
 template <int R>
 __device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::DecDesc &d,
                                            const sec::Tile &tl, const u32 *__restrict__ tabs,
-                                           const u64 *__restrict__ slot_off, const u32 *__restrict__ slot_row,
-                                           const u32 *__restrict__ miss_row);
+                                           const sec::DecSlots sl);
 
 template <int R, int U, bool W>
 __global__ __launch_bounds__(sec::max_lanes(R, U)) void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                          const sec::DecDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
                                                          const u32 *__restrict__ tabs,
-                                                         const u64 *__restrict__ slot_off,
-                                                         const u32 *__restrict__ slot_row,
-                                                         const u32 *__restrict__ miss_row)
+                                                         const sec::DecSlots sl)
 {
     const sec::Tile tl = tiles[blockIdx.x];
     const sec::DecDesc d = descs[tl.chunk];
     const u32 t = tl.t0 + threadIdx.x * sec::kLaneBytes;
     if (t < d.valid)
-        decode_main<R, U, W>(blocks, out, d, tl, t, tabs, slot_off, slot_row, miss_row);
+        decode_main<R, U, W>(blocks, out, d, tl, t, tabs, sl);
     if (tl.ntail)
-        decode_ragged<R>(blocks, out, d, tl, tabs, slot_off, slot_row, miss_row);
+        decode_ragged<R>(blocks, out, d, tl, tabs, sl);
 }
 
 // The chunk's ragged end [valid, valid + ntail), byte by byte: the present primaries' bytes
@@ -471,8 +470,7 @@ __global__ __launch_bounds__(sec::max_lanes(R, U)) void sec_decode_kernel(const 
 template <int R>
 __device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::DecDesc &d,
                                               const sec::Tile &tl, const u32 *__restrict__ tabs,
-                                              const u64 *__restrict__ slot_off, const u32 *__restrict__ slot_row,
-                                              const u32 *__restrict__ miss_row)
+                                              const sec::DecSlots sl)
 {
     for (u32 i = ragged_lane0(d.valid, tl.t0); i < tl.ntail; i += blockDim.x) {
         const u32 tp = d.valid + i;
@@ -485,12 +483,12 @@ __device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 
             u32 x[kBatch];
 #pragma unroll
             for (u32 q = 0; q < kBatch; ++q)
-                x[q] = c0 + q < d.k ? (u32)blocks[slot_off[d.slot0 + c0 + q] + tp] : 0u;
+                x[q] = (c0 + q < d.k && tp < sl.avail[d.slot0 + c0 + q]) ? (u32)blocks[sl.off[d.slot0 + c0 + q] + tp] : 0u;
 #pragma unroll
             for (u32 q = 0; q < kBatch; ++q)
                 if (c0 + q < d.k) {
                     const u32 c = c0 + q;
-                    const u32 orow = slot_row[d.slot0 + c];
+                    const u32 orow = sl.row[d.slot0 + c];
                     if (tl.r0 == 0 && orow != 0xFFFFFFFFu && (u64)orow * d.B + tp < d.n)
                         dst[(u64)orow * d.B] = (u8)x[q];
 #pragma unroll
@@ -500,7 +498,7 @@ __device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const u32 orow = miss_row[d.slot0 + tl.r0 + r];
+            const u32 orow = sl.miss[d.slot0 + tl.r0 + r];
             if ((u64)orow * d.B + tp < d.n)
                 dst[(u64)orow * d.B] = (u8)acc[r];
         }
@@ -511,9 +509,7 @@ template <int R, int U, bool W>
 __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                             const sec::DecDesc &d, const sec::Tile &tl, u32 t,
                                             const u32 *__restrict__ tabs,
-                                                         const u64 *__restrict__ slot_off,
-                                                         const u32 *__restrict__ slot_row,
-                                                         const u32 *__restrict__ miss_row)
+                                                         const sec::DecSlots sl)
 {
     const u32 B = d.B, k = (!W && SEC_FIXED_K > 0) ? (u32)SEC_FIXED_K : d.k, valid = d.valid;
     const u32 step = blockDim.x * sec::kLaneBytes;  // bytes one u-step of the workgroup covers
@@ -543,7 +539,7 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
 #pragma unroll
         for (int c = 0; c < KB; ++c)
             if (c0 + c < k) {
-                const u8 *s = blocks + slot_off[d.slot0 + c0 + c];
+                const u8 *s = blocks + sl.off[d.slot0 + c0 + c];
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     xs[c][u] = load16(s + pos[u]);
@@ -567,7 +563,7 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
 #pragma unroll
             for (int c = 0; c < KB; ++c)
                 if (c0 + c < k) {
-                    const u32 orow = slot_row[d.slot0 + c0 + c];
+                    const u32 orow = sl.row[d.slot0 + c0 + c];
                     if (copies && orow != 0xFFFFFFFFu) {
                         u8 *o = dst + (u64)orow * B;
 #pragma unroll
@@ -582,7 +578,7 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
 #pragma unroll
             for (int c = 0; c < KB; ++c)
                 if (c0 + c < k) {
-                    const u32 orow = slot_row[d.slot0 + c0 + c];
+                    const u32 orow = sl.row[d.slot0 + c0 + c];
                     if (copies && orow != 0xFFFFFFFFu) {
                         u8 *o = dst + (u64)orow * B;
 #pragma unroll
@@ -601,7 +597,7 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
     if constexpr (R > 0) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            u8 *o = dst + (u64)miss_row[d.slot0 + tl.r0 + r] * B;
+            u8 *o = dst + (u64)sl.miss[d.slot0 + tl.r0 + r] * B;
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 store16<SEC_DEC_ST>(o + pos[u], acc[r][u]);
@@ -615,9 +611,7 @@ __global__ __launch_bounds__(256) void sec_decode_tail(const u8 *__restrict__ bl
                                                        const sec::DecDesc *__restrict__ descs,
                                                        const sec::TailItem *__restrict__ items, u32 nitems,
                                                        const u32 *__restrict__ tabs,
-                                                       const u64 *__restrict__ slot_off,
-                                                       const u32 *__restrict__ slot_row,
-                                                       const u32 *__restrict__ miss_row)
+                                                       const sec::DecSlots sl)
 {
     const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nitems)
@@ -625,19 +619,21 @@ __global__ __launch_bounds__(256) void sec_decode_tail(const u8 *__restrict__ bl
     const sec::TailItem it = items[i];
     const sec::DecDesc d = descs[it.chunk];
     u8 *dst = out + d.out_off + it.t;
+    auto slot_byte = [&](u32 c) -> u32 {  // bytes past the slot's avail read as zero
+        return it.t < sl.avail[d.slot0 + c] ? (u32)blocks[sl.off[d.slot0 + c] + it.t] : 0u;
+    };
     for (u32 c = 0; c < d.k; ++c) {
-        const u32 orow = slot_row[d.slot0 + c];
+        const u32 orow = sl.row[d.slot0 + c];
         if (orow != 0xFFFFFFFFu && (u64)orow * d.B + it.t < d.n)
-            dst[(u64)orow * d.B] = blocks[slot_off[d.slot0 + c] + it.t];
+            dst[(u64)orow * d.B] = (u8)slot_byte(c);
     }
     for (u32 r = 0; r < d.e; ++r) {
-        const u32 orow = miss_row[d.slot0 + r];
+        const u32 orow = sl.miss[d.slot0 + r];
         if ((u64)orow * d.B + it.t >= d.n)
             continue;
         u32 acc = 0;
         for (u32 c = 0; c < d.k; ++c)
-            acc ^= gf_mul_byte(tabs + d.tab + (c * d.e + r) * sec::kTabDwords,
-                               (u32)blocks[slot_off[d.slot0 + c] + it.t]);
+            acc ^= gf_mul_byte(tabs + d.tab + (c * d.e + r) * sec::kTabDwords, slot_byte(c));
         dst[(u64)orow * d.B] = (u8)acc;
     }
 }
@@ -834,10 +830,9 @@ hipError_t launch_enc(const u8 *in, u8 *par, const sec::EncDesc *descs, const se
 
 template <int R, int U, bool W>
 hipError_t launch_dec(const u8 *blocks, u8 *out, const sec::DecDesc *descs, const sec::Tile *tiles, u32 ntiles,
-                      const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, u32 lanes, hipStream_t s)
+                      const u32 *tabs, sec::DecSlots sl, u32 lanes, hipStream_t s)
 {
-    return launch(sec_decode_kernel<R, U, W>, dim3(ntiles), dim3(lanes), s, blocks, out, descs, tiles, tabs, so, sr,
-                  mr);
+    return launch(sec_decode_kernel<R, U, W>, dim3(ntiles), dim3(lanes), s, blocks, out, descs, tiles, tabs, sl);
 }
 
 template <int U, bool W>
@@ -859,18 +854,18 @@ hipError_t dispatch_enc(int rows, const u8 *in, u8 *par, const sec::EncDesc *d, 
 
 template <int U, bool W>
 hipError_t dispatch_dec(int rows, const u8 *b, u8 *o, const sec::DecDesc *d, const sec::Tile *t, u32 nt,
-                        const u32 *tabs, const u64 *so, const u32 *sr, const u32 *mr, u32 lanes, hipStream_t s)
+                        const u32 *tabs, sec::DecSlots sl, u32 lanes, hipStream_t s)
 {
     switch (rows) {
-    case 0: return launch_dec<0, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 1: return launch_dec<1, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 2: return launch_dec<2, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 3: return launch_dec<3, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 4: return launch_dec<4, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 5: return launch_dec<5, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 6: return launch_dec<6, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 7: return launch_dec<7, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
-    case 8: return launch_dec<8, U, W>(b, o, d, t, nt, tabs, so, sr, mr, lanes, s);
+    case 0: return launch_dec<0, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 1: return launch_dec<1, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 2: return launch_dec<2, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 3: return launch_dec<3, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 4: return launch_dec<4, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 5: return launch_dec<5, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 6: return launch_dec<6, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 7: return launch_dec<7, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 8: return launch_dec<8, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -923,7 +918,7 @@ int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *
 
 int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,
                       const sec::DecDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
-                      const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row, void *stream)
+                      sec::DecSlots sl, void *stream)
 {
     if (ntiles == 0)
         return hipSuccess;
@@ -932,11 +927,11 @@ int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *block
     hipStream_t s = (hipStream_t)stream;
     const u32 L = (u32)lanes;
     if (wide)
-        return dispatch_dec<1, true>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
+        return dispatch_dec<1, true>(rows, blocks, out, descs, tiles, ntiles, tabs, sl, L, s);
     switch (U) {
-    case 1: return dispatch_dec<1, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
-    case 2: return dispatch_dec<2, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
-    case 4: return dispatch_dec<4, false>(rows, blocks, out, descs, tiles, ntiles, tabs, slot_off, slot_row, miss_row, L, s);
+    case 1: return dispatch_dec<1, false>(rows, blocks, out, descs, tiles, ntiles, tabs, sl, L, s);
+    case 2: return dispatch_dec<2, false>(rows, blocks, out, descs, tiles, ntiles, tabs, sl, L, s);
+    case 4: return dispatch_dec<4, false>(rows, blocks, out, descs, tiles, ntiles, tabs, sl, L, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -955,12 +950,11 @@ int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDe
 }
 
 int sec_launch_decode_tail(const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
-                           const sec::TailItem *items, uint32_t nitems, const uint32_t *tabs,
-                           const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,
+                           const sec::TailItem *items, uint32_t nitems, const uint32_t *tabs, sec::DecSlots sl,
                            void *stream)
 {
     if (nitems == 0)
         return hipSuccess;
     return launch(sec_decode_tail, dim3((nitems + 255) / 256), dim3(256), (hipStream_t)stream, blocks, out, descs,
-                  items, nitems, tabs, slot_off, slot_row, miss_row);
+                  items, nitems, tabs, sl);
 }

@@ -53,7 +53,17 @@ struct DecDesc {
     uint32_t e;        // missing primaries (rows recovered)
     uint32_t tab;      // dword offset of tables, layout [slot][missing][5]
     uint32_t slot0;    // first entry in slot_off / slot_row / miss_row
-    uint32_t valid;    // clamp(n - (k-1)*B, 0, B): positions where every row is writable
+    uint32_t valid;    // positions [0, valid) where every output row is writable and every slot
+                       // readable: min(last output row's length, every slot's avail), clamped to [0, B)
+};
+
+// Per-slot metadata of a decode launch (device arrays).  Slot c of a chunk is entry
+// slot0 + c; a chunk's recovered rows are miss[slot0 .. slot0 + e).
+struct DecSlots {
+    const uint64_t *off;    // block address: blocks + off[slot]
+    const uint32_t *row;    // output row a present primary is copied to, or 0xFFFFFFFF
+    const uint32_t *miss;   // output row of each recovered (missing) primary
+    const uint32_t *avail;  // bytes of the block that exist in memory; the rest read as zero
 };
 
 struct Tile {
@@ -97,12 +107,10 @@ int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *
                            uint32_t nitems, const uint32_t *tabs, void *stream);
 int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,
                       const sec::DecDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
-                      const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,
-                      void *stream);
+                      sec::DecSlots slots, void *stream);
 int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDesc *msgs, uint32_t nmsgs,
                     uint8_t *digests, void *stream);
 int sec_launch_decode_tail(const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
-                           const sec::TailItem *items, uint32_t nitems, const uint32_t *tabs,
-                           const uint64_t *slot_off, const uint32_t *slot_row, const uint32_t *miss_row,
+                           const sec::TailItem *items, uint32_t nitems, const uint32_t *tabs, sec::DecSlots slots,
                            void *stream);
 }

@@ -22,7 +22,7 @@ import weakref
 import numpy as np
 
 from . import _lib
-from ._lib import DEC_DTYPE, ENC_DTYPE, MSG_DTYPE, SEC_F_ASYNC, SEC_F_HOST
+from ._lib import DEC_DTYPE, ENC_DTYPE, MSG_DTYPE, SEC_F_ASYNC, SEC_F_HOST, SEC_F_RECOVER
 
 
 class Error(Exception):
@@ -134,15 +134,23 @@ class Engine:
         self._check(self.lib.sec_encode_batch(self._ctx, _ptr(descs), len(descs), s or None, p or None, flags))
 
     def decode_batch(self, descs: np.ndarray, sharenums: np.ndarray, block_offs: np.ndarray, blocks, out, *,
-                     host: bool = False, asynchronous: bool = False) -> None:
+                     block_avail: np.ndarray | None = None, recover_only: bool = False, host: bool = False,
+                     asynchronous: bool = False) -> None:
+        """sec_decode_batch_ex.  block_avail (per slot, optional): bytes of the block that exist,
+        the rest read as zero (zfec's padded last data block read in place: B - padlen).
+        recover_only: write just the missing primaries (SEC_F_RECOVER), e*B bytes per chunk."""
         descs = np.ascontiguousarray(descs, dtype=DEC_DTYPE)
         sn = np.ascontiguousarray(sharenums, dtype=np.int32)
         bo = np.ascontiguousarray(block_offs, dtype=np.uint64)
+        av = None if block_avail is None else np.ascontiguousarray(block_avail, dtype=np.uint64)
+        if av is not None and av.size < bo.size:
+            raise ValueError("block_avail needs one entry per slot")
         b, _kb = addr(blocks)
         o, _ko = addr(out)
-        flags = (SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0)
-        self._check(self.lib.sec_decode_batch(self._ctx, _ptr(descs), len(descs), _ptr(sn), _ptr(bo), b or None,
-                                        o or None, flags))
+        flags = ((SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0) |
+                 (SEC_F_RECOVER if recover_only else 0))
+        self._check(self.lib.sec_decode_batch_ex(self._ctx, _ptr(descs), len(descs), _ptr(sn), _ptr(bo),
+                                                 None if av is None else _ptr(av), b or None, o or None, flags))
 
     def encode_digest_batch(self, descs: np.ndarray, src, parity, digests, *, host: bool = False,
                             asynchronous: bool = False) -> None:

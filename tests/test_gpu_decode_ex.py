@@ -1,0 +1,228 @@
+"""GPU parity for sec_decode_batch_ex: per-block readable lengths and recover-only decodes.
+
+* zfec's zero-padded last data block read IN PLACE from the chunk buffer (avail = B - padlen,
+  bytes past it read as zero): C4's shape (64 KiB RS(10,4), B = 6554, padlen 4) and C5's
+  mixed RS(8,3) sizes decoded with block k-1 present, against the source bytes (every chunk)
+  and the oracle (oracle/fec_oracle.c, a sample);
+* SEC_F_RECOVER (recover-only): the e missing primaries zfec's fec_decode itself produces
+  (/root/reference/storb/util/piece.py:196-197 reaches it through easyfec), B bytes each with
+  block k-1's zero padding, against the oracle's padded blocks; e = 0 chunks write nothing;
+* the same through the staged host path (pageable buffers, zero-filled staging) and the
+  zero-copy pinned path.
+"""
+
+import random
+
+import numpy as np
+import pytest
+
+from oracle import cfec
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from storb_amd._lib import DEC_DTYPE, ENC_DTYPE  # noqa: E402
+
+
+def _dev(nbytes, seed):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    return torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
+
+
+def _layout(sizes, k, m):
+    sizes = np.asarray(sizes, dtype=np.uint64)
+    B = (sizes + k - 1) // k
+    in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    par_off = np.concatenate([[0], np.cumsum(B * (m - k))[:-1]]).astype(np.uint64)
+    return sizes, B, in_off, par_off
+
+
+def _encode(engine, sizes, k, m, src):
+    sizes, B, in_off, par_off = _layout(sizes, k, m)
+    d = np.zeros(len(sizes), dtype=ENC_DTYPE)
+    d["in_off"], d["n"], d["parity_off"], d["parity_stride"] = in_off, sizes, par_off, B
+    d["k"], d["m"] = k, m
+    par = torch.empty(int(np.sum(B)) * (m - k), dtype=torch.uint8, device="cuda")
+    engine.encode_batch(d, src, par)
+    return par
+
+
+def _dec_inputs(sizes, k, m, keeps, data_base, par_base, recover=False):
+    """Descriptors + per-slot avail reading the kept blocks in place; keeps[i] = chunk i's
+    k block numbers.  An in-place block k-1 has B - padlen readable bytes."""
+    sizes, B, in_off, par_off = _layout(sizes, k, m)
+    n = len(sizes)
+    d = np.zeros(n, dtype=DEC_DTYPE)
+    d["B"], d["padlen"], d["k"], d["m"] = B, B * k - sizes, k, m
+    d["slot0"] = np.arange(n, dtype=np.uint64) * k
+    sn = np.zeros(n * k, np.int32)
+    offs = np.zeros(n * k, np.uint64)
+    avail = np.zeros(n * k, np.uint64)
+    out_off, o = np.zeros(n, np.uint64), 0
+    for i in range(n):
+        out_off[i] = o
+        keep = keeps[i]
+        e = sum(1 for s in range(k) if s not in keep)
+        o += (e * int(B[i])) if recover else int(sizes[i])
+        for j, s in enumerate(keep):
+            sn[i * k + j] = s
+            if s < k:
+                offs[i * k + j] = data_base + int(in_off[i]) + s * int(B[i])
+                avail[i * k + j] = int(sizes[i]) - s * int(B[i]) if s == k - 1 else int(B[i])
+            else:
+                offs[i * k + j] = par_base + int(par_off[i]) + (s - k) * int(B[i])
+                avail[i * k + j] = int(B[i])
+    d["out_off"] = out_off
+    return d, sn, offs, avail, o
+
+
+def _check_sample(src_h, par_h, sizes, k, m, sample):
+    sizes, B, in_off, par_off = _layout(sizes, k, m)
+    for ci in sample:
+        n, b = int(sizes[ci]), int(B[ci])
+        want = cfec.easy_encode(src_h[int(in_off[ci]):int(in_off[ci]) + n].tobytes(), k, m)[k:]
+        got = par_h[int(par_off[ci]):int(par_off[ci]) + (m - k) * b].tobytes()
+        assert got == b"".join(want), ci
+
+
+def test_c4_shape_decode_with_padded_block_in_place(engine):
+    # BASELINE configs[3] shape: 64 KiB chunks, RS(10,4), B = 6554, padlen 4; block 9 (the
+    # short, padded one) is PRESENT and read in place; four other data blocks erased
+    nch, n, k, m = 2048, 65536, 10, 14
+    src = _dev(nch * n, seed=77)
+    sizes = [n] * nch
+    par = _encode(engine, sizes, k, m, src)
+    _check_sample(src.cpu().numpy(), par.cpu().numpy(), sizes, k, m, [0, 1, 1000, nch - 1])
+    keep = [1, 3, 4, 6, 8, 9, 10, 11, 12, 13]  # erased 0, 2, 5, 7
+    d, sn, offs, avail, total = _dec_inputs(sizes, k, m, [keep] * nch, src.data_ptr(), par.data_ptr())
+    out = torch.empty(total, dtype=torch.uint8, device="cuda")
+    engine.decode_batch(d, sn, offs, 0, out, block_avail=avail)
+    assert torch.equal(out, src)
+
+
+def test_c5_mixed_decode_with_padded_block_in_place(engine):
+    # BASELINE configs[4] shape at reduced total: log-uniform 4 KiB..4 MiB, RS(8,3); every chunk
+    # keeps block 7 in place and loses a random set of the others
+    rng = np.random.default_rng(5)
+    sizes = np.exp(rng.uniform(np.log(4096), np.log(4 << 20), 96)).astype(int).tolist()
+    k, m = 8, 11
+    src = _dev(int(np.sum(sizes)), seed=55)
+    par = _encode(engine, sizes, k, m, src)
+    _check_sample(src.cpu().numpy(), par.cpu().numpy(), sizes, k, m, [0, 7, 95])
+    r = random.Random(5)
+    keeps = [sorted([7] + r.sample([s for s in range(m) if s != 7], k - 1)) for _ in sizes]
+    d, sn, offs, avail, total = _dec_inputs(sizes, k, m, keeps, src.data_ptr(), par.data_ptr())
+    out = torch.empty(total, dtype=torch.uint8, device="cuda")
+    engine.decode_batch(d, sn, offs, 0, out, block_avail=avail)
+    assert torch.equal(out, src)
+
+
+def _oracle_recovered(data, k, m, keep):
+    blocks = cfec.easy_encode(data, k, m)
+    return b"".join(blocks[s] for s in range(k) if s not in keep)
+
+
+@pytest.mark.parametrize("k,m", [(2, 3), (4, 6), (8, 11), (10, 14), (16, 24), (16, 40), (32, 48)])
+def test_recover_only_vs_oracle_device(engine, k, m):
+    rng = random.Random(1000 + k * m)
+    sizes = [n for n in (k * k, 4096 * k - 3, 65536, 65536 + 9, 6554 * k - 1, 300007)
+             if -(-n // k) * (k - 1) <= n]
+    keeps = []
+    for i, _ in enumerate(sizes):
+        if i == 0:
+            keeps.append(list(range(k)))  # e = 0: writes nothing
+        elif i == 1:
+            keeps.append(sorted(rng.sample(range(m), k)))
+        else:  # block k-1 (padded) kept in place on odd chunks, lost on even ones
+            others = [s for s in range(m) if s != k - 1]
+            keeps.append(sorted(rng.sample(others, k - 1) + [k - 1]) if i % 2 else sorted(rng.sample(others, k)))
+    host = [rng.randbytes(n) for n in sizes]
+    src = torch.frombuffer(bytearray(b"".join(host)), dtype=torch.uint8).to("cuda")
+    par = _encode(engine, sizes, k, m, src)
+    d, sn, offs, avail, total = _dec_inputs(sizes, k, m, keeps, src.data_ptr(), par.data_ptr(), recover=True)
+    out = torch.full((max(total, 1),), 0xA5, dtype=torch.uint8, device="cuda")
+    engine.decode_batch(d, sn, offs, 0, out, block_avail=avail, recover_only=True)
+    want = b"".join(_oracle_recovered(h, k, m, kp) for h, kp in zip(host, keeps))
+    assert len(want) == total
+    assert out.cpu().numpy()[:total].tobytes() == want
+
+
+def test_recover_only_c3_full_size(engine):
+    # 1024 x 1 MiB RS(4,2), data shards {1,3} erased: recover-only writes e*B = 512 KiB per chunk
+    nch, n, k, m = 1024, 1 << 20, 4, 6
+    src = _dev(nch * n, seed=8)
+    sizes = [n] * nch
+    par = _encode(engine, sizes, k, m, src)
+    d, sn, offs, avail, total = _dec_inputs(sizes, k, m, [[0, 2, 4, 5]] * nch, src.data_ptr(), par.data_ptr(),
+                                            recover=True)
+    out = torch.empty(total, dtype=torch.uint8, device="cuda")
+    engine.decode_batch(d, sn, offs, 0, out, recover_only=True)
+    B = n // k
+    got = out.view(nch, 2, B)
+    s = src.view(nch, k, B)
+    assert torch.equal(got[:, 0], s[:, 1]) and torch.equal(got[:, 1], s[:, 3])
+
+
+def test_host_paths_with_avail_and_recover():
+    """Pageable small buffers (staged: zero-filled past avail) and pinned buffers (zero-copy),
+    reassemble and recover-only, with block k-1 read in place."""
+    from storb_amd.engine import Engine
+
+    eng = Engine(0)
+    try:
+        rng = np.random.default_rng(9)
+        k, m = 10, 14
+        sizes = [65536, 65536 + 3, 40000, 6554 * 10 - 9]
+        total = sum(sizes)
+        for pinned in (False, True):
+            hin = eng.host_empty(total) if pinned else np.empty(total, np.uint8)
+            hin[:] = rng.integers(0, 256, total, dtype=np.uint8)
+            szs, B, in_off, par_off = _layout(sizes, k, m)
+            d = np.zeros(len(sizes), dtype=ENC_DTYPE)
+            d["in_off"], d["n"], d["parity_off"], d["parity_stride"] = in_off, szs, par_off, B
+            d["k"], d["m"] = k, m
+            npar = int(np.sum(B)) * (m - k)
+            hpar = eng.host_empty(npar) if pinned else np.empty(npar, np.uint8)
+            eng.encode_batch(d, hin, hpar, host=True)
+            keeps = [[1, 2, 3, 5, 6, 8, 9, 11, 12, 13]] * len(sizes)  # 9 in place; 0, 4, 7 lost
+            for recover in (False, True):
+                dd, sn, offs, avail, tot = _dec_inputs(sizes, k, m, keeps, hin.ctypes.data, hpar.ctypes.data,
+                                                       recover=recover)
+                out = eng.host_empty(tot) if pinned else np.empty(tot, np.uint8)
+                out[:] = 0x5A
+                eng.decode_batch(dd, sn, offs, 0, out, block_avail=avail, recover_only=recover, host=True)
+                if recover:
+                    want = b"".join(_oracle_recovered(hin[int(o):int(o) + int(n)].tobytes(), k, m, kp)
+                                    for o, n, kp in zip(in_off, szs, keeps))
+                    assert out.tobytes() == want, (pinned, recover)
+                else:
+                    assert np.array_equal(out, hin), (pinned, recover)
+        z, r, s = eng.host_paths()
+        assert z >= 3 and s >= 3, (z, r, s)  # pinned calls zero-copy, small pageable ones staged
+    finally:
+        eng.close()
+
+
+def test_avail_is_honoured_not_read_past():
+    """Bytes past a block's avail read as zero: a block whose tail holds garbage decodes as if
+    that tail were zero (the contract that lets a short in-place block be used)."""
+    from storb_amd.engine import get_engine
+
+    eng = get_engine(0)
+    k, m, n = 4, 6, 4 * 1000 - 3  # B = 1000, padlen 3: block 3 has 997 real bytes
+    data = random.Random(3).randbytes(n)
+    blocks = cfec.easy_encode(data, k, m)
+    B = len(blocks[0])
+    keep = [0, 3, 4, 5]  # blocks 1, 2 recovered; block 3 given with garbage in its pad
+    dirty3 = blocks[3][:B - 3] + b"\xff\xfe\xfd"
+    buf = np.frombuffer(b"".join([blocks[0], dirty3, blocks[4], blocks[5]]), np.uint8).copy()
+    dev = torch.from_numpy(buf).to("cuda")
+    dd = np.zeros(1, dtype=DEC_DTYPE)
+    dd["B"], dd["padlen"], dd["k"], dd["m"], dd["slot0"], dd["out_off"] = B, 3, k, m, 0, 0
+    sn = np.array(keep, np.int32)
+    offs = np.array([0, B, 2 * B, 3 * B], np.uint64) + dev.data_ptr()
+    out = torch.empty(n, dtype=torch.uint8, device="cuda")
+    eng.decode_batch(dd, sn, offs, 0, out, block_avail=np.array([B, B - 3, B, B], np.uint64))
+    assert out.cpu().numpy().tobytes() == data

@@ -10,9 +10,9 @@ C1  4 MiB object (reference policy: 8 x 512 KiB chunks, zfec(4,6)) and the 1 MiB
     (oracle/fec_oracle.c through the same piece logic, 1 thread) and storb_amd.piece on the GPU.
 C2/C3  1024 x 1 MiB RS(4,2) encode / decode ({1,3} erased), device-resident.
 C4  8192 x 64 KiB RS(10,4) (one GPU's share of 65536), device-resident encode / decode with
-    data blocks {9,0,5,2} erased.
+    data blocks {0,2,5,7} erased (block 9, zfec's padded one, read in place: avail = B - padlen).
 C5  mixed chunk sizes log-uniform in [4 KiB, 4 MiB] (seed 5) up to ~1 GiB, RS(8,3):
-    device-resident encode / decode (blocks {7,2,5} erased) and end-to-end from host memory
+    device-resident encode / decode (blocks {1,3,5} erased, block 7 read in place) and end-to-end from host memory
     (pageable buffers, staged; and pinned buffers, zero-copy).
 """
 
@@ -102,6 +102,7 @@ def enc_descs_var(sizes, k, m):
 
 
 def dec_descs_var(sizes, k, m, B, data_base, par_base, erased):
+    """Decode descriptors + per-slot avail (an in-place block k-1 has B - padlen bytes)."""
     from storb_amd._lib import DEC_DTYPE
 
     keep = [s for s in range(m) if s not in erased][:k]
@@ -117,9 +118,11 @@ def dec_descs_var(sizes, k, m, B, data_base, par_base, erased):
     d["k"], d["m"] = k, m
     sn = np.tile(np.array(keep, np.int32), n)
     offs = np.zeros(n * k, np.uint64)
+    avail = np.zeros(n * k, np.uint64)
     for j, s in enumerate(keep):
         offs[j::k] = (data_base + in_off + s * B) if s < k else (par_base + par_off + (s - k) * B)
-    return d, sn, offs
+        avail[j::k] = (sizes - (k - 1) * B) if s == k - 1 else B
+    return d, sn, offs, avail
 
 
 def c5_sizes() -> list[int]:
@@ -136,21 +139,20 @@ def c5_sizes() -> list[int]:
 def device_case(eng, sizes, k, m, erased, reps=20):
     import torch
 
-    assert (k - 1) in erased or all(int(s) % k == 0 for s in sizes)
     total = int(np.sum(sizes))
     ed, B = enc_descs_var(sizes, k, m)
     src = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda")
     par = torch.empty(int(np.sum(B)) * (m - k), dtype=torch.uint8, device="cuda")
     out = torch.empty_like(src)
-    dd, sn, offs = dec_descs_var(sizes, k, m, B, src.data_ptr(), par.data_ptr(), erased)
+    dd, sn, offs, av = dec_descs_var(sizes, k, m, B, src.data_ptr(), par.data_ptr(), erased)
     eng.encode_batch(ed, src, par)
-    eng.decode_batch(dd, sn, offs, 0, out)
+    eng.decode_batch(dd, sn, offs, 0, out, block_avail=av)
     assert torch.equal(out, src)
     eng.set_timing(True)
     for _ in range(reps):
         eng.encode_batch(ed, src, par, asynchronous=True)
     for _ in range(reps):
-        eng.decode_batch(dd, sn, offs, 0, out, asynchronous=True)
+        eng.decode_batch(dd, sn, offs, 0, out, block_avail=av, asynchronous=True)
     eng.sync()
     eng.set_timing(False)
     ems, en = eng.collect_timing("encode")
@@ -216,9 +218,9 @@ def host_case(eng, sizes, k, m, erased, reps=3, pinned=False):
         host = rng.integers(0, 256, total, dtype=np.uint8)
         par = np.empty(nb, dtype=np.uint8)
         out = np.empty_like(host)
-    dd, sn, offs = dec_descs_var(sizes, k, m, B, host.ctypes.data, par.ctypes.data, erased)
+    dd, sn, offs, av = dec_descs_var(sizes, k, m, B, host.ctypes.data, par.ctypes.data, erased)
     te = timed(lambda: eng.encode_batch(ed, host, par, host=True), reps)
-    td = timed(lambda: eng.decode_batch(dd, sn, offs, 0, out, host=True), reps)
+    td = timed(lambda: eng.decode_batch(dd, sn, offs, 0, out, block_avail=av, host=True), reps)
     assert np.array_equal(out, host)
     return {"encode_gibs": round(total / te / GIB, 2), "decode_gibs": round(total / td / GIB, 2)}
 
@@ -236,11 +238,11 @@ def main():
                       "note": "loopback: encode_chunk -> sha1 -> dict store -> reconstruct_data; "
                               "reference path = piece.py policy + oracle/fec_oracle.c (zfec restated), 1 thread"}
     res["c2_c3_1024x1MiB_rs(4,2)"] = device_case(eng, [1 << 20] * 1024, 4, 6, (1, 3))
-    res["c4_8192x64KiB_rs(10,4)_per_gpu"] = device_case(eng, [65536] * 8192, 10, 14, (9, 0, 5, 2))
+    res["c4_8192x64KiB_rs(10,4)_per_gpu"] = device_case(eng, [65536] * 8192, 10, 14, (0, 2, 5, 7))
     sizes = c5_sizes()
-    res["c5_mixed_4KiB-4MiB_rs(8,3)_device"] = device_case(eng, sizes, 8, 11, (7, 2, 5))
-    res["c5_mixed_4KiB-4MiB_rs(8,3)_e2e_host"] = host_case(eng, sizes, 8, 11, (7, 2, 5))
-    res["c5_mixed_4KiB-4MiB_rs(8,3)_e2e_host_pinned"] = host_case(eng, sizes, 8, 11, (7, 2, 5), pinned=True)
+    res["c5_mixed_4KiB-4MiB_rs(8,3)_device"] = device_case(eng, sizes, 8, 11, (1, 3, 5))
+    res["c5_mixed_4KiB-4MiB_rs(8,3)_e2e_host"] = host_case(eng, sizes, 8, 11, (1, 3, 5))
+    res["c5_mixed_4KiB-4MiB_rs(8,3)_e2e_host_pinned"] = host_case(eng, sizes, 8, 11, (1, 3, 5), pinned=True)
     res["c2_1024x1MiB_rs(4,2)_e2e_host"] = host_case(eng, [1 << 20] * 1024, 4, 6, (1, 3))
     res["c2_1024x1MiB_rs(4,2)_e2e_host_pinned"] = host_case(eng, [1 << 20] * 1024, 4, 6, (1, 3), pinned=True)
     res["f1_sha1_pieces_c2_device"] = sha1_case(eng)

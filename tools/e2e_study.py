@@ -89,7 +89,7 @@ def main():
     host = rng.integers(0, 256, n, dtype=np.uint8)
     par = np.empty(N_CHUNKS * (M - K) * B, dtype=np.uint8)
     out = np.empty_like(host)
-    dd, sn, offs = dec_descs(N_CHUNKS, CHUNK, K, M, B, host.ctypes.data, par.ctypes.data, ERASED)
+    dd, sn, offs, _av = dec_descs(N_CHUNKS, CHUNK, K, M, B, host.ctypes.data, par.ctypes.data, ERASED)
     te = timed(lambda: eng.encode_batch(ed, host, par, host=True))
     td = timed(lambda: eng.decode_batch(dd, sn, offs, 0, out, host=True))
     assert np.array_equal(out, host)
@@ -102,7 +102,7 @@ def main():
     hpar, pin_par = host_buf(eng, par.size)
     hout, pin_out = host_buf(eng, n)
     hin[:] = host
-    dd2, sn2, offs2 = dec_descs(N_CHUNKS, CHUNK, K, M, B, pin_in.value, pin_par.value, ERASED)
+    dd2, sn2, offs2, _av2 = dec_descs(N_CHUNKS, CHUNK, K, M, B, pin_in.value, pin_par.value, ERASED)
     te = timed(lambda: eng.encode_batch(ed, pin_in.value, pin_par.value))
     res["zerocopy_encode_gibs"] = round(n / te / GIB, 2)
     res["zerocopy_encode_ok"] = bool(np.array_equal(hpar, ref_par))

@@ -9,7 +9,8 @@ Per workload and EC kernel (encode / decode main kernels, one name each):
   * issue: SQ_INSTS_VALU per wave; the shares of SQ_WAVE_CYCLES spent waiting (SQ_WAIT_ANY),
     issue-stalled (SQ_WAIT_INST_ANY) and issuing (SQ_ACTIVE_INST_ANY / _VALU); raw counters kept;
   * effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration (MI355X_MICROARCH.md DVFS note);
-  * kernel duration from the --stats pass.
+  * kernel duration from the --stats pass, and the VALU issue floor: SQ_INSTS_VALU x 4 cycles
+    over 1024 SIMDs at that clock.
 Shapes follow tools/prof_shape.py.
 """
 
@@ -49,7 +50,7 @@ def counters(d: str) -> dict:
                 kind = kind_of(row.get("Kernel_Name", ""))
                 if not kind:
                     continue
-                names[kind] = row["Kernel_Name"].split("(")[0].replace("void (anonymous namespace)::", "")
+                names[kind] = row["Kernel_Name"].replace("void (anonymous namespace)::", "").split("(")[0]
                 vals[(kind, row["Counter_Name"], row["Dispatch_Id"])] += float(row["Counter_Value"])
     per = defaultdict(list)
     for (kind, cn, _), v in vals.items():
@@ -107,7 +108,14 @@ def main():
                     "issuing": round((c["SQ_ACTIVE_INST_ANY"] or 0) / wc, 3),
                     "issuing VALU": round((c["SQ_ACTIVE_INST_VALU"] or 0) / wc, 3)}
             if c["GRBM_GUI_ACTIVE"] and kind in st:
-                r["effective_clock_GHz"] = round(c["GRBM_GUI_ACTIVE"] / 8 / st[kind]["avg_ns"], 3)
+                clk = c["GRBM_GUI_ACTIVE"] / 8 / st[kind]["avg_ns"]  # GHz
+                r["effective_clock_GHz"] = round(clk, 3)
+                if c["SQ_INSTS_VALU"]:
+                    # wave64 VALU issue: one instruction per SIMD every 4 cycles (SQ_ACTIVE_INST_VALU
+                    # counts it as one quad-cycle); 256 CUs x 4 SIMDs
+                    floor_ns = c["SQ_INSTS_VALU"] * 4 / 1024 / clk
+                    r["valu_issue_floor_ms"] = round(floor_ns / 1e6, 4)
+                    r["valu_issue_floor_over_duration"] = round(floor_ns / st[kind]["avg_ns"], 3)
             wres[kind] = r
         res[w] = wres
     print(json.dumps(res, indent=1))
