@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <utility>
@@ -915,31 +916,99 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     return SEC_OK;
 }
 
+// ---- pinned caller memory: the zero-copy host path ----------------------------
+// A SEC_F_HOST encode / decode whose caller buffers all lie in page-locked host memory the
+// HIP runtime maps at the same address on the device (hipHostMalloc / sec_host_alloc,
+// hipHostRegister / sec_host_register) skips the staging pipeline: the device-mode kernels
+// run straight on the host buffers and read / write them over PCIe, with no staging copy
+// and no DMA.  Measured on C2 (tools/e2e_study.py): encode 50.9 GiB/s and decode 41.2 GiB/s
+// against 33.4 / 17.5 staged, with the link's own H2D 53.6 and both-ways 45.2 GiB/s.
+// Pageable memory keeps the staged path.
+struct PinnedRange {
+    uintptr_t lo = 0, hi = 0;  // last allocation found: [lo, hi)
+};
+
+// True when [p, p + len) lies inside ONE pinned allocation whose device address equals its
+// host address.  `cache` remembers the last allocation so runs of blocks inside one buffer
+// cost one lookup.  A failed lookup's error is cleared so later launches do not report it.
+// (addresses arrive as base + offset integers: a NULL base with absolute offsets is legal in
+// this ABI, and pointer arithmetic on NULL would let the compiler fold the NULL test away)
+bool pinned(uintptr_t a, uint64_t len, PinnedRange *cache)
+{
+    const void *p = (const void *)a;
+    if (len == 0)
+        return true;
+    if (!a)
+        return false;
+    if (cache->hi && a >= cache->lo && a + len <= cache->hi)
+        return true;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (at.type != hipMemoryTypeHost || at.devicePointer != at.hostPointer || !at.devicePointer)
+        return false;
+    void *start = nullptr;
+    size_t size = 0;
+    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
+        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const uintptr_t lo = (uintptr_t)start, hi = lo + size;
+    if (!size || a < lo || a + len > hi)
+        return false;
+    cache->lo = lo;
+    cache->hi = hi;
+    return true;
+}
+
 // ---- host pipeline ----------------------------------------------------------
-// For each slab: (CPU) gather caller bytes into the slot's pinned `in`;
-// (slot stream) H2D, kernels, D2H into pinned `out`; the scatter of `out` into
-// caller memory runs when the slot is next needed or at the end.  Two slots, so
-// the CPU gathers slab i+1 and scatters slab i-1 while the GPU works on slab i.
+// For each slab: (CPU) gather caller bytes into the slot's pinned `in`; (slot stream) the
+// kernels, then the scatter of pinned `out` into caller memory when the slot is next needed
+// or at the end.  Two slots, so the CPU gathers slab i+1 and scatters slab i-1 while the GPU
+// works on slab i.
+// `direct`: the EC kernels run on the pinned slabs themselves (mapped at the same address on
+// the device), reading and writing them over PCIe as the zero-copy path does, with no DMA
+// copies.  A small call then costs its two host copies and one kernel, not two DMA
+// round trips as well.  SHA-1 and the bignum kernels (one latency-bound lane or wave per
+// message) keep the DMA into device scratch: every PCIe read would stall their chains.
+// SEC_STAGE_DMA=1 forces the DMA form for the EC kernels too (A/B).
+bool pinned_mapped(const PinBuf &b)
+{
+    PinnedRange cache;
+    return b.p && pinned((uintptr_t)b.p, b.cap, &cache);
+}
+
 template <class Gather, class Scatter, class Launch>
-int run_pipeline(sec_ctx *ctx, Plan &plan, Gather gather, Scatter scatter, Launch launch)
+int run_pipeline(sec_ctx *ctx, Plan &plan, Gather gather, Scatter scatter, Launch launch, bool direct = false)
 {
     RC(slots_init(ctx));
     CK(hipEventRecord(ctx->meta_ev, ctx->stream()));  // behind the plan upload / table expansion
+    direct = direct && env_size("SEC_STAGE_DMA", 0) == 0;
     size_t i = 0;
     for (const SubPlan &sp : plan.subs) {
         Slot &sl = ctx->slots[i++ % kSlots];
         RC(slot_retire(ctx, sl));
         RC(sl.in.ensure(sp.in_bytes));
         RC(sl.out.ensure(sp.out_bytes));
-        RC(sl.din.ensure(sp.in_bytes));
-        RC(sl.dout.ensure(sp.out_bytes));
+        const bool on_pins = direct && pinned_mapped(sl.in) && pinned_mapped(sl.out);
+        if (!on_pins) {
+            RC(sl.din.ensure(sp.in_bytes));
+            RC(sl.dout.ensure(sp.out_bytes));
+        }
         std::vector<sec::CopyJob> jobs;
         gather(sp, sl.in.c(), jobs);
         pool(ctx).run(jobs);
         CK(hipStreamWaitEvent(sl.s, ctx->meta_ev, 0));
-        CK(hipMemcpyAsync(sl.din.p, sl.in.p, sp.in_bytes, hipMemcpyHostToDevice, sl.s));
-        RC(launch(sp, sl.din.as<uint8_t>(), sl.dout.as<uint8_t>(), sl.s));
-        CK(hipMemcpyAsync(sl.out.p, sl.dout.p, sp.out_bytes, hipMemcpyDeviceToHost, sl.s));
+        if (on_pins) {
+            RC(launch(sp, (uint8_t *)sl.in.p, (uint8_t *)sl.out.p, sl.s));
+        } else {
+            CK(hipMemcpyAsync(sl.din.p, sl.in.p, sp.in_bytes, hipMemcpyHostToDevice, sl.s));
+            RC(launch(sp, sl.din.as<uint8_t>(), sl.dout.as<uint8_t>(), sl.s));
+            CK(hipMemcpyAsync(sl.out.p, sl.dout.p, sp.out_bytes, hipMemcpyDeviceToHost, sl.s));
+        }
         CK(hipEventRecord(sl.done, sl.s));
         scatter(sp, sl.out.c(), sl.scatter);
         sl.busy = true;
@@ -1309,54 +1378,6 @@ int sec_decode_matrix(int k, int m, const int32_t *sharenums, uint8_t *out, int3
 
 namespace {
 
-// ---- pinned caller memory: the zero-copy host path ----------------------------
-// A SEC_F_HOST encode / decode whose caller buffers all lie in page-locked host memory the
-// HIP runtime maps at the same address on the device (hipHostMalloc / sec_host_alloc,
-// hipHostRegister / sec_host_register) skips the staging pipeline: the device-mode kernels
-// run straight on the host buffers and read / write them over PCIe, with no staging copy
-// and no DMA.  Measured on C2 (tools/e2e_study.py): encode 50.9 GiB/s and decode 41.2 GiB/s
-// against 33.4 / 17.5 staged, with the link's own H2D 53.6 and both-ways 45.2 GiB/s.
-// Pageable memory keeps the staged path.
-struct PinnedRange {
-    uintptr_t lo = 0, hi = 0;  // last allocation found: [lo, hi)
-};
-
-// True when [p, p + len) lies inside ONE pinned allocation whose device address equals its
-// host address.  `cache` remembers the last allocation so runs of blocks inside one buffer
-// cost one lookup.  A failed lookup's error is cleared so later launches do not report it.
-// (addresses arrive as base + offset integers: a NULL base with absolute offsets is legal in
-// this ABI, and pointer arithmetic on NULL would let the compiler fold the NULL test away)
-bool pinned(uintptr_t a, uint64_t len, PinnedRange *cache)
-{
-    const void *p = (const void *)a;
-    if (len == 0)
-        return true;
-    if (!a)
-        return false;
-    if (cache->hi && a >= cache->lo && a + len <= cache->hi)
-        return true;
-    hipPointerAttribute_t at;
-    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    if (at.type != hipMemoryTypeHost || at.devicePointer != at.hostPointer || !at.devicePointer)
-        return false;
-    void *start = nullptr;
-    size_t size = 0;
-    if (hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)p) != hipSuccess ||
-        hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    const uintptr_t lo = (uintptr_t)start, hi = lo + size;
-    if (!size || a < lo || a + len > hi)
-        return false;
-    cache->lo = lo;
-    cache->hi = hi;
-    return true;
-}
-
 // The caller byte ranges [a, a + len) a host call reads or writes.
 struct HostRange {
     uintptr_t a;
@@ -1391,24 +1412,42 @@ std::vector<HostRange> decode_ranges(const sec_dec_chunk *chunks, int64_t nchunk
     return r;
 }
 
-bool all_pinned(const std::vector<HostRange> &rs)
+// Pages host calls lock for themselves (transient registrations), process-wide.  A call's
+// HostLock page-locks pageable caller buffers (hipHostRegister) for the call's duration so the
+// kernels can run on them directly; ranges less than 4 MiB apart are locked as one, so a
+// registration can cover memory of other callers too.  Such pages must never count as pinned
+// for any other call: its owner unlocks them when its own stream has drained, whatever the
+// other call's kernels are doing, and memory freed and reused inside a registration would map
+// to the old pages on the device.  So every transient registration is recorded here, and a
+// range that touches one is never zero-copy for a call that does not hold it (that call is
+// staged).  Classification and locking happen under one mutex.
+struct TransientLocks {
+    std::mutex mu;
+    std::map<uintptr_t, uintptr_t> regs;  // page-aligned [lo, hi) of every transient registration
+
+    // true when [a, a + len) overlaps a registration
+    bool touches(uintptr_t a, uint64_t len) const
+    {
+        auto it = regs.upper_bound(a);  // first registration starting after a
+        if (it != regs.begin() && std::prev(it)->second > a)
+            return true;
+        return it != regs.end() && it->first < a + len;
+    }
+};
+
+TransientLocks &transient_locks()
 {
-    PinnedRange cache;
-    for (const HostRange &r : rs)
-        if (!pinned(r.a, r.len, &cache))
-            return false;
-    return true;
+    static TransientLocks t;
+    return t;
 }
 
-// Pages a host call locks for itself: pageable caller buffers are page-locked
-// (hipHostRegister) for the call's duration so the kernels can run on them directly.
-// Locking 1 GiB took 2.1 ms and unlocking 0.05 ms (tools/e2e_study.py), against tens of ms
-// for the two staging copies.  Used when the call moves at least SEC_REGISTER_MIN bytes
-// (default 4 MiB; 0 = never) in ranges of 1 MiB or more on average once ranges less than
-// 4 MiB apart are merged (one registration per small, separate buffer would cost more than
-// copying it).  Any failure
-// (memory already registered elsewhere, unregistrable mappings) releases what was locked and
-// the call is staged.  Released on every return path, after the stream has drained.
+// Locking is used when the call moves at least SEC_REGISTER_MIN bytes (default 4 MiB; 0 =
+// never) in ranges of 1 MiB or more on average once ranges less than 4 MiB apart are merged
+// (one registration per small, separate buffer would cost more than copying it).  Locking
+// 1 GiB took 2.1 ms and unlocking 0.05 ms (tools/e2e_study.py), against tens of ms for the
+// two staging copies.  Any failure (memory registered elsewhere, unregistrable mappings)
+// releases what was locked and the call is staged.  Released on every return path, after
+// the call's stream has drained.
 class HostLock {
 public:
     explicit HostLock(hipStream_t s) : s_(s) {}
@@ -1416,22 +1455,28 @@ public:
     HostLock(const HostLock &) = delete;
     HostLock &operator=(const HostLock &) = delete;
 
-    bool acquire(const std::vector<HostRange> &rs)
+    // 0: staged; 1: every range in persistently pinned memory (zero-copy, nothing locked);
+    // 2: zero-copy on pages this call locked (plus persistently pinned ones)
+    int acquire(const std::vector<HostRange> &rs)
     {
-        if (getenv_zero("SEC_REGISTER_MIN"))
-            return false;
-        const uint64_t min_bytes = env_size("SEC_REGISTER_MIN", (size_t)4 << 20);
+        TransientLocks &tl = transient_locks();
+        std::lock_guard<std::mutex> g(tl.mu);
         uint64_t total = 0;
-        std::vector<std::pair<uintptr_t, uintptr_t>> pg;  // page-aligned [lo, hi) of unpinned ranges
+        std::vector<std::pair<uintptr_t, uintptr_t>> pg;  // page-aligned [lo, hi) of pageable ranges
         PinnedRange cache;
-        for (const HostRange &r : rs)
-            if (r.len) {
-                total += r.len;
-                if (!pinned(r.a, r.len, &cache))  // already pinned (e.g. Engine's result scratch)
-                    pg.emplace_back(r.a & ~kPageMask, (r.a + r.len + kPageMask) & ~kPageMask);
-            }
-        if (total < min_bytes)
-            return false;
+        for (const HostRange &r : rs) {
+            if (!r.len)
+                continue;
+            total += r.len;
+            if (tl.touches(r.a, r.len))
+                return 0;  // another call's transient pages: neither pinned nor lockable for us
+            if (!pinned(r.a, r.len, &cache))  // persistently pinned (sec_host_alloc / _register)
+                pg.emplace_back(r.a & ~kPageMask, (r.a + r.len + kPageMask) & ~kPageMask);
+        }
+        if (pg.empty())
+            return 1;
+        if (getenv_zero("SEC_REGISTER_MIN") || total < env_size("SEC_REGISTER_MIN", (size_t)4 << 20))
+            return 0;
         std::sort(pg.begin(), pg.end());
         // ranges less than kGap apart are locked as one (e.g. around a decode's erased blocks);
         // if that swallows memory that cannot be locked, retry with exact ranges once
@@ -1443,32 +1488,40 @@ public:
                 else
                     merged.push_back(q);
             if (merged.size() * ((uint64_t)1 << 20) > total)
-                return false;
+                return 0;
             bool ok = true;
             for (auto &q : merged) {
-                if (hipHostRegister((void *)q.first, q.second - q.first, hipHostRegisterDefault) != hipSuccess) {
+                if (tl.touches(q.first, q.second - q.first) ||
+                    hipHostRegister((void *)q.first, q.second - q.first, hipHostRegisterDefault) != hipSuccess) {
                     (void)hipGetLastError();
                     ok = false;
                     break;
                 }
-                locked_.push_back((void *)q.first);
+                locked_.push_back(q);
+                tl.regs.emplace(q.first, q.second);
             }
-            if (ok)
-                return true;
-            release();
+            if (ok) {
+                // the runtime must map what it locked at the same address on the device
+                PinnedRange c2;
+                for (const HostRange &r : rs)
+                    if (r.len && !pinned(r.a, r.len, &c2))
+                        ok = false;
+                if (ok)
+                    return 2;
+            }
+            unlock_all(tl);
         }
-        return false;
+        return 0;
     }
 
     void release()
     {
         if (locked_.empty())
             return;
-        (void)hipStreamSynchronize(s_);  // nothing may still run on the pages
-        for (void *p : locked_)
-            (void)hipHostUnregister(p);
-        (void)hipGetLastError();
-        locked_.clear();
+        (void)hipStreamSynchronize(s_);  // nothing of this call may still run on the pages
+        TransientLocks &tl = transient_locks();
+        std::lock_guard<std::mutex> g(tl.mu);
+        unlock_all(tl);
     }
 
 private:
@@ -1479,27 +1532,28 @@ private:
         const char *v = getenv(name);
         return v && v[0] == '0' && v[1] == 0;
     }
+    void unlock_all(TransientLocks &tl)  // tl.mu held
+    {
+        for (auto &q : locked_) {
+            (void)hipHostUnregister((void *)q.first);
+            tl.regs.erase(q.first);
+        }
+        (void)hipGetLastError();
+        locked_.clear();
+    }
     hipStream_t s_;
-    std::vector<void *> locked_;
+    std::vector<std::pair<uintptr_t, uintptr_t>> locked_;
 };
 
 // Decides a host call's path: zero-copy on the caller's pinned buffers, zero-copy on pages
 // locked for the call (`lock`), or staged.  True = run the device path on host addresses.
 bool host_direct(sec_ctx *ctx, const std::vector<HostRange> &rs, HostLock &lock)
 {
-    if (all_pinned(rs)) {
-        ++ctx->zero_copy_calls;
-        return true;
+    switch (lock.acquire(rs)) {
+    case 1: ++ctx->zero_copy_calls; return true;
+    case 2: ++ctx->registered_calls; return true;
+    default: ++ctx->staged_calls; return false;
     }
-    if (lock.acquire(rs)) {
-        if (all_pinned(rs)) {
-            ++ctx->registered_calls;
-            return true;
-        }
-        lock.release();
-    }
-    ++ctx->staged_calls;
-    return false;
 }
 
 // sec_encode_batch (digests == nullptr, digest == false) and sec_encode_digest_batch.
@@ -1607,7 +1661,7 @@ int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, cons
     auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
         return launch_encode_sub(ctx, plan, sp, din, dout, dout + sp.dig_off, s);
     };
-    return run_pipeline(ctx, plan, gather, scatter, launch);
+    return run_pipeline(ctx, plan, gather, scatter, launch, !digest);
 }
 
 }  // namespace
@@ -2052,7 +2106,7 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
     auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
         return launch_decode_sub(ctx, plan, sp, din, dout, s);
     };
-    return run_pipeline(ctx, plan, gather, scatter, launch);
+    return run_pipeline(ctx, plan, gather, scatter, launch, true);
 }
 
 // ---------------------------------------------------------------------------

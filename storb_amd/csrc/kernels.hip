@@ -688,16 +688,17 @@ __device__ __forceinline__ void sha1_compress(u32 (&h)[5], u32 (&w)[16])
 }
 
 // byte i of the message: real below `avail`, zero from there to `len`
-// Batches of fewer than kSha1PrefetchMsgs messages (under one wave per SIMD) load blocks
-// SEC_SHA1_DEPTH ahead of their compression: with no other wave on the SIMD the loads'
-// latency was exposed per block.  C2's 6144 pieces of 256 KiB: 6.30 ms without, 5.07 one
-// block ahead, 4.71 two ahead (three 4.9, four 4.73).  C4's 114688 short pieces have waves
-// to switch to and keep the plain loop (profiles/r01_sha1_prefetch.jsonl).
-// SEC_SHA1_PF = 0 / 1 forces the prefetch off / on (A/B).
+// Blocks are loaded SEC_SHA1_DEPTH ahead of their compression (a ring of registers), so a
+// block's load latency overlaps earlier blocks' round chains.  Interleaved in-process A/B
+// against the plain loop (tools/sha1_ab.py, profiles/r02_sha1_prefetch_ab.jsonl; HIP-event
+// kernel times, median of 7 rounds, spread under 2 %): 1.14x on C4's 114688 pieces of
+// 6554 B (1.75 waves per SIMD) and 1.26-1.37x on every other shape measured (C2's 6144
+// pieces of 256 KiB, 4096 x 1 MiB, 16384 x 64 KiB, 65536 x 16 KiB, 32768 x 6554 B), so it
+// is used for every launch.  (Round 1 kept the plain loop for >= 65536 messages on wall-time
+// numbers that were dominated by launch and sync time.)  SEC_SHA1_PF = 0 forces it off (A/B).
 #ifndef SEC_SHA1_PF
-#define SEC_SHA1_PF -1
+#define SEC_SHA1_PF 1
 #endif
-constexpr uint32_t kSha1PrefetchMsgs = 65536;
 #ifndef SEC_SHA1_DEPTH
 #define SEC_SHA1_DEPTH 2
 #endif
@@ -941,8 +942,7 @@ int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDe
 {
     if (nmsgs == 0)
         return hipSuccess;
-    const bool pf = SEC_SHA1_PF >= 0 ? SEC_SHA1_PF != 0 : nmsgs < kSha1PrefetchMsgs;
-    if (pf)
+    if (SEC_SHA1_PF)
         return launch(sec_sha1_kernel<true>, dim3((nmsgs + 63) / 64), dim3(64), (hipStream_t)stream, base0, base1, msgs,
                       nmsgs, digests);
     return launch(sec_sha1_kernel<false>, dim3((nmsgs + 63) / 64), dim3(64), (hipStream_t)stream, base0, base1, msgs,

@@ -44,8 +44,18 @@ class Encoder:
             primaries[-1] = primaries[-1] + b"\x00" * (B - len(primaries[-1]))
         if m == k or B == 0:
             return primaries + [b""] * (m - k) if B == 0 else primaries
-        parity = get_engine().encode_host([mv], [(k, m)])[0]
-        return primaries + parity
+        return primaries + self.encode_parity(mv)
+
+    def encode_parity(self, data) -> list[bytes]:
+        """The m - k secondary blocks of ``encode(data)`` alone (no primary copies)."""
+        k, m = self.k, self.m
+        n = len(data)
+        B = -(-n // k)
+        if k > 1 and (k - 1) * B > n:
+            raise Error(_lib.strerror(_lib.SEC_EBLOCKLEN))
+        if m == k or B == 0:
+            return [b""] * (m - k)
+        return get_engine().encode_host([memoryview(data).cast("B")], [(k, m)])[0]
 
 
 class Decoder:

@@ -261,37 +261,90 @@ class Engine:
         digs = [[bytes(dv[20 * (f + j):20 * (f + j + 1)]) for j in range(m)] for f, m in zip(first, ms)]
         return par, digs
 
-    def decode_host(self, items, out=None) -> bytes:
+    def decode_host(self, items) -> bytes:
         """Reassemble chunks from host blocks, concatenated in order.
 
         items: [(k, m, blocks, sharenums, padlen)] with exactly k equal-length blocks each.
         Returns the concatenation of every chunk's k*B - padlen bytes.
         """
+        return b"".join(self._decode_parts(items, per_chunk=False))
+
+    def decode_host_chunks(self, items) -> list[bytes]:
+        """``decode_host``, one bytes object per chunk."""
+        return self._decode_parts(items, per_chunk=True)
+
+    def _decode_parts(self, items, per_chunk: bool) -> list:
+        """Chunks with a missing primary go to the GPU in ONE sec_decode_batch call; a chunk whose
+        k blocks are its k primaries needs no field arithmetic at all (zfec's fec_decode writes
+        nothing for present primaries and easyfec joins them, /root/reference/storb/util/
+        piece.py:196-197), so it is the join of its blocks, taken as views with no staging or
+        PCIe round trip.  Returns per chunk either that chunk's bytes (per_chunk) or a list of
+        buffers whose concatenation is the output."""
         n = len(items)
-        descs = np.zeros(n, dtype=DEC_DTYPE)
-        nslots = sum(it[0] for it in items)
-        sn = np.zeros(nslots, dtype=np.int32)
-        bo = np.zeros(nslots, dtype=np.uint64)
-        keep = []
-        slot = 0
-        total = 0
+        gpu = []  # indices of chunks with a missing primary
         for i, (k, m, blocks, sharenums, padlen) in enumerate(items):
             if len(blocks) != k or len(sharenums) != k:
                 raise Error(_lib.strerror(_lib.SEC_ENBLOCKS))
             B = len(blocks[0])
-            for j, b in enumerate(blocks):
+            for b in blocks:
                 if len(b) != B:
                     raise Error(_lib.strerror(_lib.SEC_EBLOCKLEN))
-                a, kp = addr(b)
-                keep.append(kp)
-                bo[slot + j] = a
-                sn[slot + j] = int(sharenums[j])
-            descs[i] = (total, B, padlen, slot, k, m)
-            slot += k
-            total += k * B - padlen
-        buf = self._out_buffer(total) if out is None else out
-        self.decode_batch(descs, sn, bo, 0, buf, host=True)
-        return bytes(memoryview(buf)[:total])
+            sn = [int(x) for x in sharenums]
+            if not (1 <= k <= m <= 256):
+                raise Error(_lib.strerror(_lib.SEC_EKM))
+            if any(x < 0 or x >= m for x in sn):
+                raise Error(_lib.strerror(_lib.SEC_ESHARENUM))
+            if len(set(sn)) != k:
+                raise Error(_lib.strerror(_lib.SEC_EDUPSHARE))
+            if not (0 <= padlen <= k * B):
+                raise Error(_lib.strerror(_lib.SEC_EPADLEN))
+            if any(x >= k for x in sn):
+                gpu.append(i)
+        dev = {}
+        if gpu:
+            descs = np.zeros(len(gpu), dtype=DEC_DTYPE)
+            nslots = sum(items[i][0] for i in gpu)
+            sn_arr = np.zeros(nslots, dtype=np.int32)
+            bo = np.zeros(nslots, dtype=np.uint64)
+            keep = []
+            slot = total = 0
+            for j, i in enumerate(gpu):
+                k, m, blocks, sharenums, padlen = items[i]
+                B = len(blocks[0])
+                for q, b in enumerate(blocks):
+                    a, kp = addr(b)
+                    keep.append(kp)
+                    bo[slot + q] = a
+                    sn_arr[slot + q] = int(sharenums[q])
+                descs[j] = (total, B, padlen, slot, k, m)
+                dev[i] = (total, k * B - padlen)
+                slot += k
+                total += k * B - padlen
+            buf = self._out_buffer(total)
+            self.decode_batch(descs, sn_arr, bo, 0, buf, host=True)
+            mv = memoryview(buf)
+        parts = []
+        for i in range(n):
+            if i in dev:
+                o, ln = dev[i]
+                parts.append(bytes(mv[o:o + ln]) if per_chunk else mv[o:o + ln])
+                continue
+            k, m, blocks, sharenums, padlen = items[i]
+            B = len(blocks[0])
+            order = sorted(range(k), key=lambda q: int(sharenums[q]))  # primary j's block
+            left = k * B - padlen
+            views = []
+            for q in order:
+                if left <= 0:
+                    break
+                v = memoryview(blocks[q]).cast("B")
+                views.append(v[:left] if left < B else v)
+                left -= B
+            if per_chunk:
+                parts.append(b"".join(views))
+            else:
+                parts.extend(views)
+        return parts
 
 
 # -- matrices (host arithmetic; no device needed) ------------------------------

@@ -16,6 +16,14 @@ Deliberate differences (documented in DESIGN.md §Boundary):
   logs here.
 * extra batch entry points ``encode_chunks`` / ``decode_chunks`` for callers that can hand
   over many chunks at once (the validator's upload loop, validator.py:1352-1431).
+* ``reconstruct_data_stream`` decodes window w+1 on a worker thread (its own HIP context)
+  while the caller consumes window w's chunks; ``encode_chunks_stream`` does the same for the
+  upload loop's produce/consume pattern (validator.py:1338-1446, 1630-1638).
+* ``encode_chunk`` starts the SHA-1 of its pieces on a small thread pool (hashlib, as
+  ``piece_hash``), data pieces while the parity is on the GPU; ``piece_hash(data)`` returns
+  that digest when ``data`` is one of those very piece objects (identity, not equality), so
+  the validator's ``piece_hash`` right after ``encode_chunk`` (validator.py:1081) does not
+  hash serially.  Same digests either way; ``PREFETCH_PIECE_IDS = False`` turns it off.
 """
 
 from __future__ import annotations
@@ -23,8 +31,12 @@ from __future__ import annotations
 import hashlib
 import logging
 import math
+import os
+import threading
 import typing
-from collections.abc import Iterator
+from collections import OrderedDict
+from collections.abc import Iterable, Iterator
+from concurrent.futures import Future, ThreadPoolExecutor
 from enum import IntEnum
 
 from pydantic import BaseModel, ConfigDict, Field
@@ -38,8 +50,17 @@ logger = logging.getLogger(__name__)
 __all__ = [
     "PieceType", "Piece", "EncodedChunk", "ProcessedPieceInfo", "EncodedPieces", "piece_hash", "piece_length",
     "encode_chunk", "decode_chunk", "reconstruct_data", "reconstruct_data_stream", "encode_chunks",
-    "decode_chunks", "chunk_shape", "piece_hashes", "encode_chunks_with_ids", "Encoder", "Decoder", "Error",
+    "decode_chunks", "chunk_shape", "piece_hashes", "encode_chunks_with_ids", "encode_chunks_stream", "Encoder",
+    "Decoder", "Error",
 ]
+
+PREFETCH_PIECE_IDS = True  # encode_chunk hashes its pieces on a thread pool (see module doc)
+# ... for chunks of at least this many bytes.  The validator's pattern (encode_chunk, then
+# piece_hash of every piece; tools/prefetch_study.py, profiles/r02_prefetch_study.json), us per
+# chunk without / with: 256 KiB 217 / 217, 512 KiB 395 / 303, 1 MiB 744 / 411, 4 MiB 2754 / 918.
+# Below 512 KiB each hand-off to a hashing thread (GIL + wake-up) costs what the hash saves.
+PREFETCH_MIN_CHUNK = 512 << 10
+STREAM_WINDOW_BYTES = 64 << 20  # chunk bytes per GPU call in the *_stream pipelines
 
 
 class PieceType(IntEnum):  # piece.py:21-23
@@ -74,9 +95,61 @@ class EncodedPieces(BaseModel):  # piece.py:50-51
     pieces: list[Piece]
 
 
+_pools: dict = {}
+_pools_lock = threading.Lock()
+
+
+def _pool(name: str) -> ThreadPoolExecutor:
+    """Module thread pools: "hash" (hashlib SHA-1, which releases the GIL) and "stream" (one
+    worker that runs the *_stream pipelines' GPU calls on its own engine)."""
+    with _pools_lock:
+        p = _pools.get(name)
+        if p is None:
+            n = 1 if name == "stream" else max(1, min(8, (os.cpu_count() or 2) - 1))
+            p = _pools[name] = ThreadPoolExecutor(n, thread_name_prefix=f"storb_amd_{name}")
+        return p
+
+
+def _sha1_hex(b) -> str:
+    return hashlib.sha1(b).hexdigest()
+
+
+class _PieceIdMemo:
+    """Digests encode_chunk started for its pieces, keyed by the piece's bytes object.  A hit
+    requires the very object (``is``), which the memo keeps alive while it holds it, so an id
+    cannot be reused under it; entries leave on first use or oldest-first past `max_bytes`."""
+
+    def __init__(self, max_bytes: int = 1 << 30):
+        self.max_bytes = max_bytes
+        self._d: OrderedDict = OrderedDict()
+        self._bytes = 0
+        self._lock = threading.Lock()
+
+    def put(self, obj: bytes, fut: Future) -> None:
+        with self._lock:
+            self._d[id(obj)] = (obj, fut)
+            self._bytes += len(obj)
+            while self._bytes > self.max_bytes and self._d:
+                _, (o, _f) = self._d.popitem(last=False)
+                self._bytes -= len(o)
+
+    def take(self, obj):
+        with self._lock:
+            e = self._d.get(id(obj))
+            if e is None or e[0] is not obj:
+                return None
+            del self._d[id(obj)]
+            self._bytes -= len(obj)
+        return e[1].result()
+
+
+_memo = _PieceIdMemo()
+
+
 def piece_hash(data: bytes) -> str:
     """SHA-1 hex digest of a piece (piece.py:54-68)."""
-    return hashlib.sha1(data).hexdigest()
+    d = _memo.take(data) if type(data) is bytes else None
+    return d if d is not None else hashlib.sha1(data).hexdigest()
 
 
 def piece_hashes(datas: typing.Sequence[bytes]) -> list[str]:
@@ -133,7 +206,18 @@ def encode_chunk(chunk: bytes, chunk_idx: int) -> EncodedChunk:
     piece_size = piece_length(chunk_size)  # ValueError for an empty chunk, as the reference
     logger.debug("[encode_chunk] chunk %d: %d bytes, piece_size = %d", chunk_idx, chunk_size, piece_size)
     k, m, B, padlen = chunk_shape(chunk_size)
-    encoded_pieces = Encoder(k, m).encode(chunk)
+    enc_ = Encoder(k, m)
+    if not PREFETCH_PIECE_IDS or chunk_size < PREFETCH_MIN_CHUNK:
+        encoded_pieces = enc_.encode(chunk)
+    else:  # data pieces hash while the GPU computes the parity, parity pieces right after
+        prim = _split(chunk, k, B)
+        hp = _pool("hash")
+        futs = [hp.submit(_sha1_hex, b) for b in prim]
+        parity = enc_.encode_parity(chunk) if m > k and B else [b""] * (m - k)
+        futs += [hp.submit(_sha1_hex, b) for b in parity]
+        encoded_pieces = prim + parity
+        for b, f in zip(encoded_pieces, futs):
+            _memo.put(b, f)
     enc = _build(chunk_idx, k, m, B, padlen, chunk_size, encoded_pieces)
     logger.debug("[encode_chunk] chunk %d: k=%d, m=%d, encoded %d blocks", chunk_idx, k, m, len(enc.pieces))
     return enc
@@ -226,8 +310,125 @@ def reconstruct_data(pieces: list[Piece], chunks: list[EncodedChunk]) -> bytes:
     return decode_chunks(chunks)
 
 
-def reconstruct_data_stream(pieces: list[Piece], chunks: list[EncodedChunk]) -> Iterator[bytes]:
-    """Yield the reconstructed bytes chunk by chunk (piece.py:239-263)."""
-    for chunk in chunks:
-        chunk.pieces = _relevant(pieces, chunk)
-        yield decode_chunk(chunk)
+def _windows(chunks, nbytes, size_of) -> Iterator[list]:
+    """Consecutive groups of chunks totalling at most `nbytes` (at least one chunk each)."""
+    win, acc = [], 0
+    for c in chunks:
+        sz = size_of(c)
+        if win and acc + sz > nbytes:
+            yield win
+            win, acc = [], 0
+        win.append(c)
+        acc += sz
+    if win:
+        yield win
+
+
+def _decode_window(window: list, by_chunk: dict):
+    """Worker side of reconstruct_data_stream: (per-chunk bytes, error) for one window.  The
+    window's chunks up to the first one that cannot be decoded are decoded (one GPU call for
+    those with a missing primary); that chunk's error is returned, to be raised in order."""
+    items, err = [], None
+    for chunk in window:
+        relevant = sorted(by_chunk.get(chunk.chunk_idx, []), key=lambda p: p.piece_idx)
+        if len(relevant) < chunk.k:
+            err = ValueError(f"Not enough pieces to reconstruct chunk {chunk.chunk_idx}")
+            break
+        chunk.pieces = relevant
+        blocks, sharenums = _sharenums(chunk, False)
+        B = len(blocks[0]) if blocks else 0
+        if not (1 <= chunk.k <= chunk.m <= 256) or not (0 <= chunk.padlen <= chunk.k * B):
+            items.append(None)  # easyfec's own slicing semantics: the per-chunk path
+            continue
+        items.append((chunk.k, chunk.m, blocks, sharenums, chunk.padlen))
+    try:
+        batch = [it for it in items if it is not None]
+        outs = iter(get_engine().decode_host_chunks(batch) if batch else [])
+        res = [next(outs) if it is not None else decode_chunk(ch) for it, ch in zip(items, window)]
+    except Exception as e:  # noqa: BLE001 - re-raised on the caller's thread, in order
+        return [], e
+    return res, err
+
+
+def reconstruct_data_stream(pieces: list[Piece], chunks: list[EncodedChunk], *,
+                            window_bytes: int | None = None) -> Iterator[bytes]:
+    """Yield the reconstructed bytes chunk by chunk (piece.py:239-263).
+
+    Chunks go in windows of about `window_bytes` (default STREAM_WINDOW_BYTES) of output; each
+    window is one batched decode on a worker thread, and window w+1's decode runs while the
+    caller consumes window w (the validator streams them into the HTTP response,
+    validator.py:1630-1638).  Chunks come out in order; a chunk without enough pieces raises
+    the reference's ValueError when the stream reaches it, after every earlier chunk."""
+    by_chunk: dict[int, list[Piece]] = {}
+    for p in pieces:
+        by_chunk.setdefault(p.chunk_idx, []).append(p)
+    wb = STREAM_WINDOW_BYTES if window_bytes is None else window_bytes
+    wins = _windows(chunks, wb, lambda c: max(c.original_chunk_size, 1))
+    pool = _pool("stream")
+    nxt = next(wins, None)
+    fut = pool.submit(_decode_window, nxt, by_chunk) if nxt is not None else None
+    while fut is not None:
+        nxt = next(wins, None)
+        ahead = pool.submit(_decode_window, nxt, by_chunk) if nxt is not None else None
+        outs, err = fut.result()
+        yield from outs
+        if err is not None:
+            if ahead is not None:
+                ahead.cancel()
+            raise err
+        fut = ahead
+
+
+def _encode_window(window: list, first_idx: int, piece_ids: bool):
+    """Worker side of encode_chunks_stream: one batched GPU encode for the window (+ SHA-1 piece
+    ids on the hash pool: data pieces start before the GPU call, parity pieces after it)."""
+    if not piece_ids:
+        return [(c, None) for c in encode_chunks(window, first_idx)], None
+    try:
+        shapes = []
+        for c in window:
+            piece_length(len(c))
+            shapes.append(chunk_shape(len(c)))
+        hp = _pool("hash")
+        prims = [_split(c, k, B) for c, (k, _, B, _) in zip(window, shapes)]
+        dfuts = [[hp.submit(_sha1_hex, b) for b in prim] for prim in prims]
+        parity = get_engine().encode_host(list(window), [(k, m) for (k, m, _, _) in shapes])
+        out = []
+        for i, (c, (k, m, B, padlen), prim, par, df) in enumerate(zip(window, shapes, prims, parity, dfuts)):
+            pf = [hp.submit(_sha1_hex, b) for b in par]
+            out.append((_build(first_idx + i, k, m, B, padlen, len(c), prim + par), df + pf))
+        return [(ec, [f.result() for f in fs]) for ec, fs in out], None
+    except Exception as e:  # noqa: BLE001 - re-raised on the caller's thread
+        return [], e
+
+
+def encode_chunks_stream(chunks: Iterable[bytes], first_chunk_idx: int = 0, *, piece_ids: bool = False,
+                         window_bytes: int | None = None) -> Iterator:
+    """``encode_chunk`` over a stream of chunks (the validator's upload loop: chunks read from
+    the request, encoded, handed to the miners, validator.py:1338-1446), pipelined.
+
+    Chunks are pulled from `chunks` on the caller's thread into windows of about
+    `window_bytes` (default STREAM_WINDOW_BYTES); each window is one batched GPU encode on a
+    worker thread, running while the caller consumes the previous window's results.  Yields
+    ``EncodedChunk`` per chunk in order (chunk i gets index first_chunk_idx + i), or with
+    ``piece_ids=True`` ``(EncodedChunk, [piece_hash of each of its m pieces])``."""
+    wb = STREAM_WINDOW_BYTES if window_bytes is None else window_bytes
+    pool = _pool("stream")
+    idx = first_chunk_idx
+    pending = None
+    for win in _windows(chunks, wb, lambda c: max(len(c), 1)):
+        fut = pool.submit(_encode_window, win, idx, piece_ids)
+        idx += len(win)
+        if pending is not None:
+            yield from _emit(pending, piece_ids)
+        pending = fut
+    if pending is not None:
+        yield from _emit(pending, piece_ids)
+
+
+def _emit(fut: Future, piece_ids: bool):
+    outs, err = fut.result()
+    if err is not None:
+        raise err
+    for ec, ids in outs:
+        yield (ec, ids) if piece_ids else ec

@@ -467,3 +467,58 @@ def test_pageable_large_calls_lock_pages_per_call(monkeypatch):
         assert eng.host_paths() == (0, 4, 1)
     finally:
         eng.close()
+
+
+def test_threads_pageable_locking_interleaved(monkeypatch):
+    """Per-call page locking under concurrent engines: big calls whose input and
+    parity ranges are 2 MiB apart (locked as one registration, gap included) run beside calls
+    whose buffers live in that gap.  A range touching another call's transient registration
+    must never count as pinned for this call (it is staged instead), so every result is exact
+    however the calls interleave, and the locked path does run."""
+    import threading
+
+    from storb_amd.engine import Engine
+
+    monkeypatch.setenv("SEC_REGISTER_MIN", str(1 << 20))
+    MiB = 1 << 20
+    big = np.random.default_rng(5).integers(0, 256, 64 * MiB, dtype=np.uint8)
+    k, m = 4, 6
+    errors, paths = [], []
+
+    def run(lo_in, n_in, lo_par, iters, seed):
+        try:
+            eng = Engine(0)
+            try:
+                nch = n_in // MiB
+                d = np.zeros(nch, dtype=ENC_DTYPE)
+                d["in_off"] = np.arange(nch, dtype=np.uint64) * MiB
+                d["n"], d["parity_off"], d["parity_stride"] = MiB, np.arange(nch, dtype=np.uint64) * (MiB // 2), MiB // 4
+                d["k"], d["m"] = k, m
+                src = big[lo_in:lo_in + n_in]
+                par = big[lo_par:lo_par + n_in // 2]
+                rng = random.Random(seed)
+                for _ in range(iters):
+                    par[:] = 0
+                    eng.encode_batch(d, src, par, host=True)
+                    ci = rng.randrange(nch)
+                    want = b"".join(oracle_parity(src[ci * MiB:(ci + 1) * MiB].tobytes(), k, m))
+                    assert par[ci * MiB // 2:(ci + 1) * MiB // 2].tobytes() == want
+                paths.append(eng.host_paths())
+            finally:
+                eng.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = []
+    for t in range(2):
+        base = 32 * MiB * t
+        # big call: 8 MiB in at base, 4 MiB parity at base + 10 MiB (2 MiB gap between)
+        ts.append(threading.Thread(target=run, args=(base, 8 * MiB, base + 10 * MiB, 12, t)))
+        # small call inside that gap: 1 MiB in at base + 8 MiB, parity at base + 9 MiB
+        ts.append(threading.Thread(target=run, args=(base + 8 * MiB, 1 * MiB, base + 9 * MiB, 30, 10 + t)))
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    assert sum(p[1] for p in paths) > 0, paths  # the locked (registered) path ran

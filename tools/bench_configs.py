@@ -4,10 +4,7 @@ JSON object.  Complements bench.py (which is the C2+C3 headline line).
 
     python tools/bench_configs.py > gpurun_out/configs.json
 
-C1  4 MiB object (reference policy: 8 x 512 KiB chunks, zfec(4,6)) and the 1 MiB object
-    (4 x 256 KiB, zfec(2,3) = BASELINE's "RS(k=2,m=1)"): loopback upload -> SHA-1 -> in-memory
-    miner dict -> retrieve -> reconstruct.  Timed twice: the reference's CPU path restated
-    (oracle/fec_oracle.c through the same piece logic, 1 thread) and storb_amd.piece on the GPU.
+C1  see tools/c1_loopback.py.
 C2/C3  1024 x 1 MiB RS(4,2) encode / decode ({1,3} erased), device-resident.
 C4  8192 x 64 KiB RS(10,4) (one GPU's share of 65536), device-resident encode / decode with
     data blocks {0,2,5,7} erased (block 9, zfec's padded one, read in place: avail = B - padlen).
@@ -20,7 +17,6 @@ from __future__ import annotations
 
 import hashlib
 import json
-import math
 import os
 import sys
 import time
@@ -40,50 +36,6 @@ def timed(fn, reps):
     for _ in range(reps):
         fn()
     return (time.perf_counter() - t0) / reps
-
-
-# ---------------------------------------------------------------- C1 loopback
-def c1_reference_cpu(data: bytes) -> float:
-    """Reference CPU path (restated): piece.py policy + zfec arithmetic via the C oracle."""
-    from oracle import cfec, zfec_ref
-
-    def run():
-        chunk_size = zfec_ref.piece_length(len(data))
-        store, meta = {}, []
-        for ci in range(math.ceil(len(data) / chunk_size)):
-            chunk = data[ci * chunk_size:(ci + 1) * chunk_size]
-            k, m, B, pad = zfec_ref.chunk_shape(len(chunk))
-            blocks = cfec.easy_encode(chunk, k, m)
-            ids = []
-            for b in blocks:
-                h = hashlib.sha1(b).hexdigest()
-                store[h] = b
-                ids.append(h)
-            meta.append((k, m, pad, ids))
-        out = []
-        for k, m, pad, ids in meta:
-            blocks = [store[h] for h in ids[:k]]
-            out.append(cfec.easy_decode(blocks, list(range(k)), pad, k, m))
-        assert b"".join(out) == data
-
-    return len(data) / timed(run, 5) / MIB
-
-
-def c1_gpu_dropin(data: bytes) -> float:
-    from storb_amd import piece
-
-    def run():
-        chunk_size = piece.piece_length(len(data))
-        store, chunks = {}, []
-        for ci in range(math.ceil(len(data) / chunk_size)):
-            info = piece.encode_chunk(data[ci * chunk_size:(ci + 1) * chunk_size], ci)
-            for p in info.pieces:
-                store[piece.piece_hash(p.data)] = p
-            chunks.append(info.model_copy(update={"pieces": None}))
-        pieces = list(store.values())
-        assert piece.reconstruct_data(pieces, chunks) == data
-
-    return len(data) / timed(run, 5) / MIB
 
 
 # ---------------------------------------------------------------- device-resident
@@ -230,13 +182,7 @@ def main():
 
     eng = Engine(0)
     res = {}
-    rng = np.random.default_rng(1)
-    for label, size in (("c1_4MiB_object_zfec(4,6)", 4 << 20), ("c1_1MiB_object_zfec(2,3)", 1 << 20)):
-        data = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
-        res[label] = {"reference_cpu_restated_MiBs": round(c1_reference_cpu(data), 1),
-                      "storb_amd_gpu_dropin_MiBs": round(c1_gpu_dropin(data), 1),
-                      "note": "loopback: encode_chunk -> sha1 -> dict store -> reconstruct_data; "
-                              "reference path = piece.py policy + oracle/fec_oracle.c (zfec restated), 1 thread"}
+
     res["c2_c3_1024x1MiB_rs(4,2)"] = device_case(eng, [1 << 20] * 1024, 4, 6, (1, 3))
     res["c4_8192x64KiB_rs(10,4)_per_gpu"] = device_case(eng, [65536] * 8192, 10, 14, (0, 2, 5, 7))
     sizes = c5_sizes()

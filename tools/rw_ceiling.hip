@@ -1,0 +1,170 @@
+// rw_ceiling.hip — HBM ceilings for the EC kernels' traffic mixes, launches timed back to back.
+//
+// Not product code: a calibration tool ("remeasure hbm_study2's decode
+// pattern back-to-back").  Each variant is timed as 20 back-to-back launches between two HIP
+// events (the way bench.py times the product kernels), median of 7 such batches; prints one
+// JSON object, GB/s of algorithmic bytes.  16 B per lane, nontemporal loads and stores, one
+// 256-lane workgroup per 4 KiB * U of each stream, like the product kernels.
+//   read        1 GiB of loads (XOR-reduced into one dword per workgroup, kept live)
+//   write       1 GiB of stores
+//   copy_U*     1 GiB -> 1 GiB (the 1:1 mix of a decode)
+//   enc         RS(4,2)-shaped: 4 blocks read, 2 written per 1 MiB chunk (2:1, C2 encode)
+//   dec         RS(4,2) reassemble-shaped ({1,3} erased): blocks 0, 2 and both parity blocks
+//               read, 4 rows written (1:1, C3 decode), copies stored after the recovered rows
+//   dec_early   the same with the two copies stored before the recovered rows
+//   rec         recover-only-shaped: 4 blocks read, 2 rows written (2:1, like enc, but the
+//               reads come from two buffers as in a decode)
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <vector>
+
+typedef unsigned int u32;
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned char u8;
+
+#define CK(x)                                                                  \
+    do {                                                                       \
+        hipError_t e = (x);                                                    \
+        if (e != hipSuccess) {                                                 \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));             \
+            return 1;                                                          \
+        }                                                                      \
+    } while (0)
+
+__device__ __forceinline__ u32x4 ld(const u8 *p) { return __builtin_nontemporal_load((const u32x4 *)p); }
+__device__ __forceinline__ void st(u8 *p, u32x4 v) { __builtin_nontemporal_store(v, (u32x4 *)p); }
+
+constexpr size_t G = 1ull << 30, CH = 1u << 20, BB = CH / 4;
+
+template <int U>
+__global__ __launch_bounds__(256) void k_read(const u8 *__restrict__ in, u32 *__restrict__ sink)
+{
+    const u8 *p = in + (size_t)blockIdx.x * 4096 * U + threadIdx.x * 16;
+    u32x4 a = {0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        a ^= ld(p + u * 4096);
+    const u32 v = a.x ^ a.y ^ a.z ^ a.w;
+    if (v == 0x12345678u)  // practically never: keeps the loads live without a store per lane
+        sink[blockIdx.x] = v;
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_write(u8 *__restrict__ out)
+{
+    u8 *p = out + (size_t)blockIdx.x * 4096 * U + threadIdx.x * 16;
+    const u32x4 v = {blockIdx.x, threadIdx.x, 3u, 4u};
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        st(p + u * 4096, v);
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_copy(const u8 *__restrict__ in, u8 *__restrict__ out)
+{
+    const size_t o = (size_t)blockIdx.x * 4096 * U + threadIdx.x * 16;
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        x[u] = ld(in + o + u * 4096);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        st(out + o + u * 4096, x[u]);
+}
+
+__global__ __launch_bounds__(256) void k_enc(const u8 *__restrict__ in, u8 *__restrict__ par)
+{
+    constexpr u32 per = BB / 4096;
+    const u32 chunk = blockIdx.x / per, t0 = (blockIdx.x % per) * 4096 + threadIdx.x * 16;
+    const u8 *s = in + (size_t)chunk * CH + t0;
+    u8 *d = par + (size_t)chunk * 2 * BB + t0;
+    const u32x4 x0 = ld(s), x1 = ld(s + BB), x2 = ld(s + 2 * BB), x3 = ld(s + 3 * BB);
+    st(d, x0 ^ x1 ^ x2 ^ x3);
+    st(d + BB, x0 ^ (x1 << 1) ^ x2 ^ (x3 << 2));
+}
+
+template <bool EARLY, bool COPIES>
+__global__ __launch_bounds__(256) void k_dec(const u8 *__restrict__ in, const u8 *__restrict__ par,
+                                             u8 *__restrict__ out)
+{
+    constexpr u32 per = BB / 4096;
+    const u32 chunk = blockIdx.x / per, t0 = (blockIdx.x % per) * 4096 + threadIdx.x * 16;
+    const u8 *d = in + (size_t)chunk * CH + t0;
+    const u8 *p = par + (size_t)chunk * 2 * BB + t0;
+    const u32x4 x0 = ld(d), x2 = ld(d + 2 * BB), x4 = ld(p), x5 = ld(p + BB);
+    if constexpr (COPIES) {
+        u8 *w = out + (size_t)chunk * CH + t0;
+        if (EARLY) {
+            st(w, x0);
+            st(w + 2 * BB, x2);
+        }
+        st(w + BB, x0 ^ x4 ^ x5);
+        st(w + 3 * BB, x2 ^ x4 ^ (x5 << 1));
+        if (!EARLY) {
+            st(w, x0);
+            st(w + 2 * BB, x2);
+        }
+    } else {  // recover-only: the two recovered rows, dense
+        u8 *w = out + (size_t)chunk * 2 * BB + t0;
+        st(w, x0 ^ x4 ^ x5);
+        st(w + BB, x2 ^ x4 ^ (x5 << 1));
+    }
+}
+
+template <class F>
+double time_ms(F launch)
+{
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int i = 0; i < 5; ++i)
+        launch();
+    std::vector<float> t;
+    for (int i = 0; i < 7; ++i) {
+        (void)hipEventRecord(a);
+        for (int r = 0; r < 20; ++r)
+            launch();
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms;
+        (void)hipEventElapsedTime(&ms, a, b);
+        t.push_back(ms / 20);
+    }
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+int main()
+{
+    u8 *a, *b, *c;
+    u32 *sink;
+    CK(hipMalloc(&a, G));
+    CK(hipMalloc(&b, G));
+    CK(hipMalloc(&c, G));
+    CK(hipMalloc(&sink, G / 4096 * 4));
+    CK(hipMemset(a, 7, G));
+    CK(hipMemset(b, 1, G));
+    CK(hipMemset(c, 3, G));
+    auto rate = [&](double bytes, double ms) { return bytes / (ms * 1e-3) / 1e9; };
+    const dim3 blk(256);
+    const double rd = rate(G, time_ms([&] { hipLaunchKernelGGL((k_read<1>), dim3(G / 4096), blk, 0, 0, a, sink); }));
+    const double rd4 = rate(G, time_ms([&] { hipLaunchKernelGGL((k_read<4>), dim3(G / 16384), blk, 0, 0, a, sink); }));
+    const double wr = rate(G, time_ms([&] { hipLaunchKernelGGL((k_write<1>), dim3(G / 4096), blk, 0, 0, c); }));
+    const double wr4 = rate(G, time_ms([&] { hipLaunchKernelGGL((k_write<4>), dim3(G / 16384), blk, 0, 0, c); }));
+    const double cp1 = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_copy<1>), dim3(G / 4096), blk, 0, 0, a, c); }));
+    const double cp2 = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_copy<2>), dim3(G / 8192), blk, 0, 0, a, c); }));
+    const double cp4 = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_copy<4>), dim3(G / 16384), blk, 0, 0, a, c); }));
+    const double en = rate(1.5 * G, time_ms([&] { hipLaunchKernelGGL(k_enc, dim3(G / 16384), blk, 0, 0, a, b); }));
+    const double de = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_dec<false, true>), dim3(G / 16384), blk, 0, 0, a, b, c); }));
+    const double dee = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_dec<true, true>), dim3(G / 16384), blk, 0, 0, a, b, c); }));
+    const double re = rate(1.5 * G, time_ms([&] { hipLaunchKernelGGL((k_dec<false, false>), dim3(G / 16384), blk, 0, 0, a, b, c); }));
+    printf("{\"unit\": \"GB/s\", \"read_U1\": %.1f, \"read_U4\": %.1f, \"write_U1\": %.1f, \"write_U4\": %.1f, "
+           "\"copy_U1\": %.1f, \"copy_U2\": %.1f, \"copy_U4\": %.1f, \"enc\": %.1f, \"dec\": %.1f, \"dec_early\": %.1f, "
+           "\"rec\": %.1f}\n", rd, rd4, wr, wr4, cp1, cp2, cp4, en, de, dee, re);
+    CK(hipDeviceSynchronize());
+    return 0;
+}

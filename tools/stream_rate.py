@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""F2 at the API storb calls: the upload and download loops over one large object, per-chunk
+(the reference's call pattern) against the pipelined entry points.  Not product code.
+
+    python tools/stream_rate.py [--mib 1024] > gpurun_out/stream_rate.json
+
+Object: --mib MiB of random bytes; the policy gives its chunk size (1 GiB -> 8 MiB chunks,
+zfec(16,24)).  Rates are object bytes / wall time (GiB/s), best of --reps:
+  upload_per_chunk       encode_chunk per chunk + piece_hash per piece (validator.py:1380,1081)
+  upload_stream          encode_chunks_stream(piece_ids=True)
+  download_per_chunk     decode_chunk per chunk (the reference's reconstruct_data_stream body)
+  download_stream        reconstruct_data_stream, consumed chunk by chunk
+each download both with every data piece present (joined, no GPU work) and with data piece 0
+of every chunk lost (recovered on the GPU).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GIB = float(1 << 30)
+
+
+def best(fn, reps):
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return min(ts)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mib", type=int, default=1024)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    from storb_amd import piece
+
+    data = np.random.default_rng(3).integers(0, 256, a.mib << 20, dtype=np.uint8).tobytes()
+    cs = piece.piece_length(len(data))
+    parts = [data[o:o + cs] for o in range(0, len(data), cs)]
+    res = {"object_bytes": len(data), "chunk_bytes": cs, "chunks": len(parts),
+           "shape": list(piece.chunk_shape(cs)[:2]), "unit": "GiB/s of object bytes, best of %d" % a.reps}
+
+    def up_per_chunk():
+        out = []
+        for i, c in enumerate(parts):
+            ec = piece.encode_chunk(c, i)
+            out.append((ec, [piece.piece_hash(p.data) for p in ec.pieces]))
+        return out
+
+    def up_stream():
+        return list(piece.encode_chunks_stream(iter(parts), piece_ids=True))
+
+    enc = up_stream()
+    res["upload_per_chunk"] = round(len(data) / best(up_per_chunk, a.reps) / GIB, 3)
+    res["upload_stream"] = round(len(data) / best(up_stream, a.reps) / GIB, 3)
+    chunks = [ec.model_copy(update={"pieces": None}) for ec, _ in enc]
+    for label, drop in (("all_data_present", ()), ("data_piece_0_lost", (0,))):
+        pieces = [p for ec, _ in enc for p in ec.pieces if p.piece_idx not in drop]
+
+        def down_per_chunk():
+            for ch in chunks:
+                ch.pieces = sorted([p for p in pieces if p.chunk_idx == ch.chunk_idx], key=lambda p: p.piece_idx)
+                piece.decode_chunk(ch)
+
+        def down_stream():
+            n = 0
+            for b in piece.reconstruct_data_stream(pieces, chunks):
+                n += len(b)
+            assert n == len(data)
+
+        assert b"".join(piece.reconstruct_data_stream(pieces, chunks)) == data
+        res[f"download_per_chunk_{label}"] = round(len(data) / best(down_per_chunk, a.reps) / GIB, 3)
+        res[f"download_stream_{label}"] = round(len(data) / best(down_stream, a.reps) / GIB, 3)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

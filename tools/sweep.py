@@ -52,7 +52,7 @@ VARIANTS = {
     "pair8": {"SEC_PAIR_ROWS": 8},
     # launch bound of the > 4-row kernels (VGPR cap: 1024 lanes leave 128), with / without pairs
     "lb256": {"SEC_LB_WIDE_ROWS": 256},
-    "sha1pf": {"SEC_SHA1_PF": 1},  # SHA-1 next-block prefetch forced on / off (default: < 65536 messages)
+    "sha1pf": {"SEC_SHA1_PF": 1},  # SHA-1 next-block prefetch on (the default) / off
     "sha1nopf": {"SEC_SHA1_PF": 0},
     "sha1d1": {"SEC_SHA1_DEPTH": 1},  # prefetch depth in blocks (default 2)
     "sha1d3": {"SEC_SHA1_DEPTH": 3},
