@@ -1,14 +1,18 @@
 #!/bin/bash
-# tests -> smoke -> bench (-> optional sweep) ; stops at the first failure
+# Round evidence in one GPU call: gpu tests -> smoke -> bench -> rocprofv3 kernel stats of the
+# bench -> bench --workload c4 -> every BASELINE config (tools/bench_configs.py).  Each step
+# under its own timeout; the first failure ends the script.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
-echo "== pytest gpu" && timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
-tail -1 $O/pytest_gpu.log; grep -h "took the" $O/pytest_gpu.log || true
-echo "== smoke" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -30 $O/smoke.log; exit 1; }
+export TMPDIR=/tmp
+echo "== pytest gpu" && timeout -k 10 900 python3 -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+echo "== smoke" && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -30 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-echo "== bench" && timeout -k 10 300 python -u bench.py > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
+echo "== bench" && timeout -k 10 300 python3 -u bench.py > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
 tail -1 $O/bench.log
-if [ -n "$SWEEP" ]; then
-  echo "== sweep" && timeout -k 10 400 python -u tools/sweep.py $SWEEP > $O/sweep.jsonl 2>&1 || { tail -20 $O/sweep.jsonl; exit 1; }
-  cat $O/sweep.jsonl
-fi
+echo "== rocprofv3 stats" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu --no-e2e > $O/prof.log 2>&1 || { tail -30 $O/prof.log; exit 1; }
+echo "== bench c4" && timeout -k 10 300 python3 -u bench.py --workload c4 > $O/bench_c4.log 2>&1 || { tail -30 $O/bench_c4.log; exit 1; }
+tail -1 $O/bench_c4.log
+echo "== configs" && timeout -k 10 600 python3 -u tools/bench_configs.py > $O/configs.json 2> $O/configs.err || { tail -30 $O/configs.err; exit 1; }
+cat $O/configs.json
