@@ -71,6 +71,9 @@ def parse():
                     help="c2c3: the headline line (BASELINE configs[1]+[2], weak scaling); c4: configs[3], "
                          "65536 x 64 KiB RS(10,4) encode split over the ranks (strong scaling)")
     ap.add_argument("--c4-chunks", type=int, default=65536, help="c4: chunks in the whole job (default 65536)")
+    ap.add_argument("--no-recover", action="store_true",
+                    help="skip the recover-only decode measurement (it shares the decode kernel's name, so a "
+                         "rocprofv3 --stats run of the headline line wants it off)")
     ap.add_argument("--no-events", action="store_true",
                     help="A/B only: no per-launch HIP events in the timed region (roofline fields then null)")
     return ap.parse_args()
@@ -328,7 +331,7 @@ def main():
             "encode_gibs": round(N_CHUNKS * n / enc_avg_s / GIB, 2),
             "decode_gibs": round(N_CHUNKS * n / dec_avg_s / GIB, 2),
         }
-        if not args.no_events:  # after the timed region; not part of `value`
+        if not args.no_events and not args.no_recover:  # after the timed region; not part of `value`
             res["decode_recover_only_kernel"] = recover_only_rate(eng, torch, src, par, N_CHUNKS, n, k, m, B)
 
     # host-buffer (PCIe-inclusive) rate: reported, never `value`

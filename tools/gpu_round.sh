@@ -11,7 +11,7 @@ echo "== smoke" && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.
 tail -1 $O/smoke.log
 echo "== bench" && timeout -k 10 300 python3 -u bench.py > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
 tail -1 $O/bench.log
-echo "== rocprofv3 stats" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu --no-e2e > $O/prof.log 2>&1 || { tail -30 $O/prof.log; exit 1; }
+echo "== rocprofv3 stats" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 20 --warmup 3 --no-cpu --no-e2e --no-recover > $O/prof.log 2>&1 || { tail -30 $O/prof.log; exit 1; }
 echo "== bench c4" && timeout -k 10 300 python3 -u bench.py --workload c4 > $O/bench_c4.log 2>&1 || { tail -30 $O/bench_c4.log; exit 1; }
 tail -1 $O/bench_c4.log
 echo "== configs" && timeout -k 10 600 python3 -u tools/bench_configs.py > $O/configs.json 2> $O/configs.err || { tail -30 $O/configs.err; exit 1; }
