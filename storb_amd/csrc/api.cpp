@@ -129,6 +129,7 @@ size_t env_size(const char *name, size_t dflt)
 struct Group {
     int rows, U, lanes, wide;  // wide: k > kBatchVecs / U, blocks loaded in several batches
     uint32_t first, count;
+    int mfma = 0;              // sec_encode_mfma_kernel<G = U, TILES = rows> (encode, k = 32 * G)
 };
 
 // One launch unit: all chunks (device mode) or one slab of chunks (host mode).
@@ -136,6 +137,7 @@ struct SubPlan {
     int64_t c0 = 0, c1 = 0;  // chunk range
     std::vector<Group> groups;
     size_t off_desc = 0, off_tiles = 0, off_tail = 0, off_soff = 0, off_srow = 0, off_mrow = 0, off_savail = 0;
+    size_t off_mtab = 0;  // encode: MFMA bit-matrix tables (shared by every sub-plan)
     uint32_t ntail = 0;
     uint64_t in_bytes = 0, out_bytes = 0;  // dense slab sizes (host mode)
     size_t off_msgs = 0;                   // messages of this unit (SHA-1, bignum)
@@ -222,7 +224,7 @@ bool is_wide(int k, int U, int rows)
     return U == 1 && rows > 4 && k > k8;
 }
 
-using Bins = std::map<std::tuple<int, int, int, int>, std::vector<sec::Tile>>;  // (rows, U, lanes, wide)
+using Bins = std::map<std::tuple<int, int, int, int, int>, std::vector<sec::Tile>>;  // (mfma, rows, U, lanes, wide)
 
 uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 
@@ -236,7 +238,7 @@ uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 // byte launch cost C4 13-17 % on top of its main kernels (profiles/r01_c4_kernel_stats).
 // Chunks with valid < 16 get no tile: all of [0, B) becomes one-thread tail items.
 void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B, int64_t valid,
-              int rows_total, int k, bool decode)
+              int rows_total, int k, bool decode, uint64_t start = 0)
 {
     if (B == 0)
         return;
@@ -260,21 +262,28 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
         const int wide = is_wide(k, U, rows);  // U == 1 then (pick_u)
         const int flanes = U == 1 ? std::min(full_lanes(decode), sec::max_lanes(rows, 1)) : sec::kLanes;
         const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * U;
-        auto &full = bins[{rows, U, flanes, wide}];
+        auto &full = bins[{0, rows, U, flanes, wide}];
         sec::Tile *last = nullptr;
         if (!exact) {
             // every U = 1 tile is flanes wide, the chunk's last one with idle lanes past
             // `valid`: one launch per (rows, wide) class however mixed the chunk sizes are
-            const uint64_t nfull = U == 1 ? (v + step - 1) / step : v / step;
+            // tiles from `start` (the end of a chunk's MFMA range, a multiple of 16), or one
+            // tile at `valid` that only carries the ragged end when that range reaches it
+            const uint64_t from = std::min<uint64_t>(start, v);
+            const uint64_t nfull = U == 1 ? (v - from + step - 1) / step : (v - from) / step;
             for (uint64_t i = 0; i < nfull; ++i) {
-                full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
+                full.push_back(sec::Tile{chunk, (uint32_t)(from + i * step), (uint32_t)r0, 0});
                 last = &full.back();
             }
             const int ul = std::min(full_lanes(decode), sec::max_lanes(rows, 1));
-            auto &ones = bins[{rows, 1, ul, is_wide(k, 1, rows)}];
-            for (uint64_t t0 = nfull * step; t0 < v; t0 += (uint64_t)sec::kLaneBytes * ul) {  // U > 1 remainder
+            auto &ones = bins[{0, rows, 1, ul, is_wide(k, 1, rows)}];
+            for (uint64_t t0 = from + nfull * step; t0 < v; t0 += (uint64_t)sec::kLaneBytes * ul) {  // U > 1 remainder
                 ones.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
                 last = &ones.back();
+            }
+            if (!last && B > v) {
+                full.push_back(sec::Tile{chunk, (uint32_t)v, (uint32_t)r0, 0});
+                last = &full.back();
             }
         } else {
             // A/B (SEC_EXACT_LANES): partial tiles sized to what is left of the chunk, up to
@@ -287,14 +296,44 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
             for (uint64_t t0 = nfull * step; t0 < v;) {
                 const uint64_t lanes =
                     std::min<uint64_t>(sec::max_lanes(rows, 1), round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
-                auto &bin = bins[{rows, 1, (int)lanes, is_wide(k, 1, rows)}];
+                auto &bin = bins[{0, rows, 1, (int)lanes, is_wide(k, 1, rows)}];
                 bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
                 last = &bin.back();
                 t0 += lanes * sec::kLaneBytes;
             }
         }
-        last->ntail = ragged_kernel ? 0 : (uint32_t)(B - v);  // the ragged end [v, B) rides on the last tile
+        if (last)  // the ragged end [v, B) rides on the last tile
+            last->ntail = ragged_kernel ? 0 : (uint32_t)(B - v);
     }
+}
+
+// Bit-sliced MFMA encode (kernels_mfma.hip) for k = 32 or 64: whole 128-position groups below
+// `valid` in tiles of sec::kMfmaTile positions, one tile per row group of mfma_group_rows(G)
+// parity rows; add_mfma_work returns where the MFMA range ends (the VALU tiles start there).
+// Off unless SEC_MFMA=1: in-process A/Bs measured it below the v_perm kernels on every wide
+// shape (zfec(32,48) 1.75-2.32 against 2.25-2.60 TB/s, zfec(64,96) 0.76-1.07 against 1.24-1.33;
+// profiles/r02_mfma_ab.jsonl).
+bool mfma_eligible(int k, int m)
+{
+    const char *e = getenv("SEC_MFMA");
+    if (!e || e[0] != '1')
+        return false;
+    return m > k && (k == 32 || k == 64);
+}
+
+uint64_t add_mfma_work(Bins &bins, uint32_t chunk, int64_t valid, int k, int m)
+{
+    const uint64_t vm = valid > 0 ? (uint64_t)valid / sec::kMfmaGroup * sec::kMfmaGroup : 0;
+    if (vm == 0)
+        return 0;
+    const int G = k / 32, p = m - k, RGR = sec::mfma_group_rows(G);
+    for (int r0 = 0; r0 < p; r0 += RGR) {
+        const int tiles = (std::min(RGR, p - r0) + 3) / 4;
+        auto &bin = bins[{1, tiles, G, 256, 0}];
+        for (uint64_t t0 = 0; t0 < vm; t0 += sec::kMfmaTile)
+            bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
+    }
+    return vm;
 }
 
 // XCD order.  Workgroup b of a launch is dispatched to XCD b % 8, so with the tiles in chunk
@@ -311,6 +350,8 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
 
 bool use_xcd_order(bool decode, const Group &g)
 {
+    if (g.mfma)
+        return false;
     if (SEC_XCD_ORDER >= 0)
         return SEC_XCD_ORDER == 1;
     return decode && g.U > 1 && g.lanes == sec::kLanes;
@@ -335,8 +376,9 @@ void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile
     for (auto &kv : bins) {
         if (kv.second.empty())
             continue;
-        groups.push_back(Group{std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first),
-                               std::get<3>(kv.first), (uint32_t)tiles.size(), (uint32_t)kv.second.size()});
+        groups.push_back(Group{std::get<1>(kv.first), std::get<2>(kv.first), std::get<3>(kv.first),
+                               std::get<4>(kv.first), (uint32_t)tiles.size(), (uint32_t)kv.second.size(),
+                               std::get<0>(kv.first)});
         const size_t first = tiles.size();
         tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
         if (use_xcd_order(decode, groups.back())) {
@@ -638,9 +680,22 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
     }
     Image img;
     plan.subs.clear();
+    // bit-matrix tables of the MFMA encode, one per (k, m) shape it serves
+    std::map<std::pair<int, int>, uint32_t> mtab_of;  // -> offset in 16 B units
+    std::vector<uint8_t> mblob;
+    for (int64_t i = 0; i < nchunks; ++i) {
+        const int k = chunks[i].k, m = chunks[i].m;
+        if (mfma_eligible(k, m) && !mtab_of.count({k, m})) {
+            const std::vector<uint8_t> t = sec::mfma_table(k, m);
+            mtab_of[{k, m}] = (uint32_t)(mblob.size() / 16);
+            mblob.insert(mblob.end(), t.begin(), t.end());
+        }
+    }
+    const size_t off_mtab = mblob.empty() ? 0 : img.put(mblob.data(), mblob.size());
     uint64_t dig = 0;
     for (auto [c0, c1] : ranges) {
         SubPlan sp;
+        sp.off_mtab = off_mtab;
         sp.c0 = c0;
         sp.c1 = c1;
         sp.dig_first = dig;
@@ -662,7 +717,8 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             d.p = (uint32_t)p;
             d.tab = tab_of[i];
             d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)B));
-            d.pad = 0;
+            auto mt = mtab_of.find({c.k, c.m});
+            d.pad = mt != mtab_of.end() ? mt->second : 0;
             if (digest) {  // data blocks from the input (padding synthesised), then parity
                 for (int j = 0; j < c.k; ++j) {
                     const int64_t av = (int64_t)c.n - (int64_t)j * (int64_t)B;
@@ -676,8 +732,10 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             }
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
-            if (p > 0)
-                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false);
+            if (p > 0) {
+                const uint64_t start = mt != mtab_of.end() ? add_mfma_work(bins, (uint32_t)(i - c0), valid, c.k, c.m) : 0;
+                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, start);
+            }
         }
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles, false);
@@ -704,9 +762,11 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
     for (const Group &g : sp.groups) {
-        int e = sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
+        int e = g.mfma ? sec_launch_encode_mfma(g.U, g.rows, in, par, dd, dt + g.first, g.count,
+                                                plan.meta.as<uint8_t>(sp.off_mtab), s)
+                       : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
         if (e)
-            return hip_fail((hipError_t)e, "sec_encode_kernel");
+            return hip_fail((hipError_t)e, g.mfma ? "sec_encode_mfma_kernel" : "sec_encode_kernel");
     }
     if (sp.ntail) {
         int e = sec_launch_encode_tail(in, par, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs, s);

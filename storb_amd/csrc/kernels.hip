@@ -873,6 +873,14 @@ hipError_t dispatch_dec(int rows, const u8 *b, u8 *o, const sec::DecDesc *d, con
 
 }  // namespace
 
+void sec_next_launch_events(void **start, void **stop)
+{
+    *start = t_start;
+    t_start = nullptr;
+    *stop = t_stop;
+    ++t_launched;
+}
+
 int sec_launch_events(void *start, void *stop)
 {
     const int n = t_launched;

@@ -31,6 +31,12 @@ constexpr int kBatchVecs = 16;      // 16 B vectors a lane loads per batch (SEC_
 #endif
 constexpr int max_lanes(int rows, int U) { return U != 1 ? kLanes : (rows > 4 ? SEC_LB_WIDE_ROWS : 1024); }
 
+// Bit-sliced MFMA encode (kernels_mfma.hip, k = 32 * G): one wave covers groups of this many
+// positions, kMfmaGroupsPerWave of them per tile (4 waves), so a tile spans kMfmaTile.
+constexpr int kMfmaGroup = 128;
+constexpr int kMfmaGroupsPerWave = 16;
+constexpr int kMfmaTile = kMfmaGroup * 4 * kMfmaGroupsPerWave;  // 8192 positions
+
 // One encode chunk, device copy (48 B).
 struct EncDesc {
     uint64_t in_off;      // chunk start in `in`
@@ -41,7 +47,7 @@ struct EncDesc {
     uint32_t p;           // parity blocks (m - k)
     uint32_t tab;         // dword offset of this chunk's tables, layout [j][r][5]
     uint32_t valid;       // n - (k-1)*B: bytes of the last (zero-padded) data block
-    uint32_t pad;
+    uint32_t pad;         // MFMA encode: offset (16 B units) of the chunk's bit-matrix tables
 };
 
 // One decode chunk, device copy (40 B).
@@ -98,11 +104,17 @@ extern "C++" {
 // Timing: the next launch's dispatch records `start`, every launch records `stop` (both
 // hipEvent_t, or null), until the next call; returns the launches since the previous call.
 int sec_launch_events(void *start, void *stop);
+// For launchers in other translation units: the events the next dispatch records (as above),
+// counted as a launch; pass them to hipExtLaunchKernelGGL.
+void sec_next_launch_events(void **start, void **stop);
 int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void *stream);
 // wide: k > kBatchVecs / U (U must be 1): the kernels that load the blocks in several batches
 int sec_launch_encode(int rows, int U, int wide, int lanes, const uint8_t *in, uint8_t *par,
                       const sec::EncDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
                       void *stream);
+// k = 32 * G (G = 1, 2), `tiles` 32-row accumulator tiles per row group (G = 1: 1..4, G = 2: 1..2)
+int sec_launch_encode_mfma(int G, int tiles, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
+                           const sec::Tile *t, uint32_t ntiles, const void *mtabs, void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
                            uint32_t nitems, const uint32_t *tabs, void *stream);
 int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,

@@ -59,6 +59,8 @@ VARIANTS = {
     "sha1d4": {"SEC_SHA1_DEPTH": 4},
     "lb256p8": {"SEC_LB_WIDE_ROWS": 256, "SEC_PAIR_ROWS": 8},
     "lb512p8": {"SEC_LB_WIDE_ROWS": 512, "SEC_PAIR_ROWS": 8},
+    # bit-sliced MFMA encode (kernels_mfma.hip): one wave per SIMD with the q steps unrolled
+    "mfw1": {"SEC_MFMA_WAVES": 1, "SEC_MFMA_QU": 4},
 }
 
 
