@@ -228,6 +228,28 @@ class Engine:
         mv = memoryview(out)
         return [bytes(mv[20 * i:20 * (i + 1)]) for i in range(len(datas))]
 
+    def encode_host_raw(self, chunks, shapes):
+        """``encode_host`` without the per-block ``bytes``: returns (buf, layout) where buf is
+        this engine's pinned result scratch and layout[i] = (offset, B, m - k) of chunk i's
+        parity blocks in it, back to back.  buf is reused by the engine's next call."""
+        n = len(chunks)
+        descs = np.zeros(n, dtype=ENC_DTYPE)
+        keep = []
+        layout = []
+        total = 0
+        for i, (c, (k, m)) in enumerate(zip(chunks, shapes)):
+            a, kp = addr(c)
+            keep.append(kp)
+            ln = len(kp) if isinstance(kp, np.ndarray) else len(c)
+            B = -(-ln // k) if ln else 0
+            descs[i] = (a, ln, total, max(B, 1), k, m)
+            layout.append((total, B, m - k))
+            total += (m - k) * B
+        out = self._out_buffer(total)
+        if n:
+            self.encode_batch(descs, 0, out, host=True)
+        return out, layout
+
     def encode_host(self, chunks, shapes, digests: bool = False):
         """Parity blocks for each chunk.  chunks: bytes-like list; shapes: [(k, m)] per chunk.
 

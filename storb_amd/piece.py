@@ -28,6 +28,7 @@ Deliberate differences (documented in DESIGN.md §Boundary):
 
 from __future__ import annotations
 
+import ctypes
 import hashlib
 import logging
 import math
@@ -39,6 +40,7 @@ from collections.abc import Iterable, Iterator
 from concurrent.futures import Future, ThreadPoolExecutor
 from enum import IntEnum
 
+import numpy as np
 from pydantic import BaseModel, ConfigDict, Field
 
 from .constants import MAX_PIECE_SIZE, MIN_PIECE_SIZE, PIECE_LENGTH_OFFSET, PIECE_LENGTH_SCALING
@@ -60,6 +62,11 @@ PREFETCH_PIECE_IDS = True  # encode_chunk hashes its pieces on a thread pool (se
 # chunk without / with: 256 KiB 217 / 217, 512 KiB 395 / 303, 1 MiB 744 / 411, 4 MiB 2754 / 918.
 # Below 512 KiB each hand-off to a hashing thread (GIL + wake-up) costs what the hash saves.
 PREFETCH_MIN_CHUNK = 512 << 10
+# Pieces of at least this many bytes are copied on the thread pool too (_pieces_parallel):
+# 8 MiB chunks (512 KiB pieces) 1.79 -> 2.1-2.7 GiB/s per chunk, 3.47 -> 4.1-5.3 streamed
+# (tools/stream_rate.py); with 128 KiB pieces the hand-offs cost more than the copies (C1's
+# 4 MiB object fell from 1236-1289 to 811 MiB/s per chunk, 1327-1469 to 868 streamed).
+PARALLEL_COPY_MIN = 256 << 10
 STREAM_WINDOW_BYTES = 64 << 20  # chunk bytes per GPU call in the *_stream pipelines
 
 
@@ -190,6 +197,57 @@ def _split(chunk, k: int, B: int) -> list[bytes]:
     return prim
 
 
+# New bytes objects filled in place before anything else sees them: what a C extension does
+# with PyBytes_FromStringAndSize(NULL, n).  The fills are numpy copies, which release the GIL,
+# so the pieces of a chunk are copied on the thread pool in parallel (and beside the GPU call)
+# instead of one after another by the caller's thread.
+_PyBytes_New = ctypes.pythonapi.PyBytes_FromStringAndSize
+_PyBytes_New.restype = ctypes.py_object
+_PyBytes_New.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+_BYTES_DATA = bytes.__basicsize__ - 1  # offsetof(PyBytesObject, ob_sval)
+
+
+def _new_bytes(n: int):
+    """(a new unshared bytes object of n bytes, a writable uint8 view of its buffer)."""
+    b = _PyBytes_New(None, n)
+    if n == 0:
+        return b, np.empty(0, np.uint8)
+    return b, np.frombuffer((ctypes.c_char * n).from_address(id(b) + _BYTES_DATA), dtype=np.uint8)
+
+
+def _fill(dst: np.ndarray, src: np.ndarray) -> None:
+    dst[:len(src)] = src
+    if len(src) < len(dst):
+        dst[len(src):] = 0
+
+
+def _pieces_parallel(chunks: list, shapes: list) -> list[list[bytes]]:
+    """Every chunk's m pieces as bytes (k zero-padded data slices, then the parity): one GPU
+    call for all chunks; the piece copies run on the hash pool, the data slices beside the GPU
+    call.  Returns once every piece is filled."""
+    hp = _pool("hash")
+    out, jobs = [], []
+    for c, (k, m, B, _) in zip(chunks, shapes):
+        if k > 1 and (k - 1) * B > len(c):  # easyfec's short middle slice, as Encoder.encode
+            raise Error("Precondition violation: Input blocks are required to be all the same length.")
+        src = np.frombuffer(memoryview(c).cast("B"), dtype=np.uint8)
+        ps = []
+        for j in range(k):
+            b, v = _new_bytes(B)
+            ps.append(b)
+            jobs.append(hp.submit(_fill, v, src[j * B:min((j + 1) * B, len(src))]))
+        out.append(ps)
+    buf, layout = get_engine().encode_host_raw(list(chunks), [(k, m) for (k, m, _, _) in shapes])
+    for ps, (o, B, p) in zip(out, layout):
+        for r in range(p):
+            b, v = _new_bytes(B)
+            ps.append(b)
+            jobs.append(hp.submit(_fill, v, buf[o + r * B:o + (r + 1) * B]))
+    for f in jobs:  # the pieces must be complete before anyone sees them (and buf is reused)
+        f.result()
+    return out
+
+
 def _build(chunk_idx: int, k: int, m: int, B: int, padlen: int, n: int, blocks: list[bytes]) -> EncodedChunk:
     pieces = []
     for i, block in enumerate(blocks):
@@ -209,13 +267,17 @@ def encode_chunk(chunk: bytes, chunk_idx: int) -> EncodedChunk:
     enc_ = Encoder(k, m)
     if not PREFETCH_PIECE_IDS or chunk_size < PREFETCH_MIN_CHUNK:
         encoded_pieces = enc_.encode(chunk)
-    else:  # data pieces hash while the GPU computes the parity, parity pieces right after
-        prim = _split(chunk, k, B)
+    else:  # piece ids hashed on the pool: data pieces beside the GPU call, parity right after
         hp = _pool("hash")
-        futs = [hp.submit(_sha1_hex, b) for b in prim]
-        parity = enc_.encode_parity(chunk) if m > k and B else [b""] * (m - k)
-        futs += [hp.submit(_sha1_hex, b) for b in parity]
-        encoded_pieces = prim + parity
+        if B >= PARALLEL_COPY_MIN:  # large pieces: their copies on the pool as well
+            encoded_pieces = _pieces_parallel([chunk], [(k, m, B, padlen)])[0]
+            futs = [hp.submit(_sha1_hex, b) for b in encoded_pieces]
+        else:
+            prim = _split(chunk, k, B)
+            futs = [hp.submit(_sha1_hex, b) for b in prim]
+            parity = enc_.encode_parity(chunk) if m > k and B else [b""] * (m - k)
+            futs += [hp.submit(_sha1_hex, b) for b in parity]
+            encoded_pieces = prim + parity
         for b, f in zip(encoded_pieces, futs):
             _memo.put(b, f)
     enc = _build(chunk_idx, k, m, B, padlen, chunk_size, encoded_pieces)
@@ -230,7 +292,13 @@ def encode_chunks(chunks: typing.Sequence[bytes], first_chunk_idx: int = 0) -> l
         n = len(c)
         piece_length(n)  # same ValueError as encode_chunk for n == 0
         shapes.append(chunk_shape(n))
-    parity = get_engine().encode_host(list(chunks), [(k, m) for (k, m, _, _) in shapes]) if chunks else []
+    if not chunks:
+        return []
+    if min(B for (_, _, B, _) in shapes) >= PARALLEL_COPY_MIN:  # piece copies in parallel
+        pieces = _pieces_parallel(list(chunks), shapes)
+        return [_build(first_chunk_idx + i, k, m, B, padlen, len(c), ps)
+                for i, (c, (k, m, B, padlen), ps) in enumerate(zip(chunks, shapes, pieces))]
+    parity = get_engine().encode_host(list(chunks), [(k, m) for (k, m, _, _) in shapes])
     out = []
     for i, (c, (k, m, B, padlen), par) in enumerate(zip(chunks, shapes, parity)):
         out.append(_build(first_chunk_idx + i, k, m, B, padlen, len(c), _split(c, k, B) + par))
@@ -390,14 +458,19 @@ def _encode_window(window: list, first_idx: int, piece_ids: bool):
             piece_length(len(c))
             shapes.append(chunk_shape(len(c)))
         hp = _pool("hash")
-        prims = [_split(c, k, B) for c, (k, _, B, _) in zip(window, shapes)]
-        dfuts = [[hp.submit(_sha1_hex, b) for b in prim] for prim in prims]
-        parity = get_engine().encode_host(list(window), [(k, m) for (k, m, _, _) in shapes])
-        out = []
-        for i, (c, (k, m, B, padlen), prim, par, df) in enumerate(zip(window, shapes, prims, parity, dfuts)):
-            pf = [hp.submit(_sha1_hex, b) for b in par]
-            out.append((_build(first_idx + i, k, m, B, padlen, len(c), prim + par), df + pf))
-        return [(ec, [f.result() for f in fs]) for ec, fs in out], None
+        if min(B for (_, _, B, _) in shapes) >= PARALLEL_COPY_MIN:
+            pieces = _pieces_parallel(window, shapes)
+            futs = [[hp.submit(_sha1_hex, b) for b in ps] for ps in pieces]
+        else:  # small pieces: caller-thread copies; data pieces hash while the GPU runs
+            prims = [_split(c, k, B) for c, (k, _, B, _) in zip(window, shapes)]
+            futs = [[hp.submit(_sha1_hex, b) for b in prim] for prim in prims]
+            parity = get_engine().encode_host(list(window), [(k, m) for (k, m, _, _) in shapes])
+            pieces = [prim + par for prim, par in zip(prims, parity)]
+            for fs, par in zip(futs, parity):
+                fs.extend(hp.submit(_sha1_hex, b) for b in par)
+        out = [_build(first_idx + i, k, m, B, padlen, len(c), ps)
+               for i, (c, (k, m, B, padlen), ps) in enumerate(zip(window, shapes, pieces))]
+        return [(ec, [f.result() for f in fs]) for ec, fs in zip(out, futs)], None
     except Exception as e:  # noqa: BLE001 - re-raised on the caller's thread
         return [], e
 
