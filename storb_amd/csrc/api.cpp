@@ -183,10 +183,17 @@ struct Image {
     }
 };
 
-// lanes of every U = 1 tile (U > 1 tiles are 256 lanes); SEC_FULL_LANES overrides, for A/B
-int full_lanes(bool decode)
+// Lanes of every U = 1 tile (U > 1 tiles are 256 lanes).  An encode batch whose blocks are all
+// >= 64 KiB gets tiles one wave wide (1 KiB of each block per workgroup): in-process A/B
+// (profiles/r02_enc_lanes.jsonl) C2 encode +1.9-2.0 %, RS(8,3) on 1 MiB chunks +2.3-2.6 %,
+// zfec(16,24) even, while C4's 6554 B blocks lose 4.7 %; a mixed batch (C5) keeps one tile
+// width, since its large chunks alone at 64 lanes (a second launch) cost it 9 %.  The 1:1
+// copy behind a decode measured no gain from narrower tiles (-1 %).
+// SEC_ENC_LANES / SEC_FULL_LANES override, for A/B.
+int full_lanes(bool decode, bool narrow = false)
 {
-    const int l = (int)env_size(decode ? "SEC_FULL_LANES" : "SEC_ENC_LANES", env_size("SEC_FULL_LANES", sec::kLanes));
+    const size_t dflt = !decode && narrow ? 64 : sec::kLanes;
+    const int l = (int)env_size(decode ? "SEC_FULL_LANES" : "SEC_ENC_LANES", env_size("SEC_FULL_LANES", dflt));
     return std::max(64, std::min(1024, l)) / 64 * 64;
 }
 
@@ -238,7 +245,7 @@ uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 // byte launch cost C4 13-17 % on top of its main kernels (profiles/r01_c4_kernel_stats).
 // Chunks with valid < 16 get no tile: all of [0, B) becomes one-thread tail items.
 void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B, int64_t valid,
-              int rows_total, int k, bool decode, uint64_t start = 0)
+              int rows_total, int k, bool decode, uint64_t start = 0, bool narrow = false)
 {
     if (B == 0)
         return;
@@ -260,7 +267,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
         const int rows = std::min(sec::kMaxRows, rows_total - r0);
         const int U = pick_u(B, rows, k);
         const int wide = is_wide(k, U, rows);  // U == 1 then (pick_u)
-        const int flanes = U == 1 ? std::min(full_lanes(decode), sec::max_lanes(rows, 1)) : sec::kLanes;
+        const int flanes = U == 1 ? std::min(full_lanes(decode, narrow), sec::max_lanes(rows, 1)) : sec::kLanes;
         const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * U;
         auto &full = bins[{0, rows, U, flanes, wide}];
         sec::Tile *last = nullptr;
@@ -275,7 +282,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
                 full.push_back(sec::Tile{chunk, (uint32_t)(from + i * step), (uint32_t)r0, 0});
                 last = &full.back();
             }
-            const int ul = std::min(full_lanes(decode), sec::max_lanes(rows, 1));
+            const int ul = std::min(full_lanes(decode, narrow), sec::max_lanes(rows, 1));
             auto &ones = bins[{0, rows, 1, ul, is_wide(k, 1, rows)}];
             for (uint64_t t0 = from + nfull * step; t0 < v; t0 += (uint64_t)sec::kLaneBytes * ul) {  // U > 1 remainder
                 ones.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
@@ -692,6 +699,10 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
         }
     }
     const size_t off_mtab = mblob.empty() ? 0 : img.put(mblob.data(), mblob.size());
+    bool narrow = true;  // every block of the batch >= 64 KiB: one-wave encode tiles (full_lanes)
+    for (int64_t i = 0; i < nchunks && narrow; ++i)
+        if (chunks[i].m > chunks[i].k && enc_B(chunks[i]) < ((uint64_t)64 << 10))
+            narrow = false;
     uint64_t dig = 0;
     for (auto [c0, c1] : ranges) {
         SubPlan sp;
@@ -734,7 +745,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             sp.out_bytes += (uint64_t)p * B;
             if (p > 0) {
                 const uint64_t start = mt != mtab_of.end() ? add_mfma_work(bins, (uint32_t)(i - c0), valid, c.k, c.m) : 0;
-                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, start);
+                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, start, narrow);
             }
         }
         std::vector<sec::Tile> tiles;

@@ -522,3 +522,33 @@ def test_threads_pageable_locking_interleaved(monkeypatch):
         t.join()
     assert not errors, errors
     assert sum(p[1] for p in paths) > 0, paths  # the locked (registered) path ran
+
+
+def test_largest_block_size(engine):
+    """B just under the 2^31-byte limit (u32 positions in the plan and kernels): zfec(2,3) on a
+    4 GiB chunk, parity checked against the field arithmetic at the start, the middle and the
+    end; B = 2^31 is refused with SEC_ESIZE as zfec-style precondition error."""
+    from oracle import zfec_ref
+    from storb_amd.engine import Error
+
+    k, m = 2, 3
+    B = (1 << 31) - 1
+    n = 2 * B - 1  # padlen 1
+    src = _dev(n, seed=31)
+    d, B2 = _enc_descs(1, n, k, m)
+    assert B2 == B
+    par = torch.empty(B, dtype=torch.uint8, device="cuda")
+    engine.encode_batch(d, src, par)
+    c0, c1 = (int(c) for c in zfec_ref.parity_rows(k, m)[0])
+    mul = zfec_ref.MUL
+    for lo in (0, B // 2 - 4096, B - 8192):
+        hi = min(lo + 8192, B)
+        x0 = src[lo:hi].cpu().numpy()
+        x1 = src[B + lo:min(B + hi, n)].cpu().numpy()
+        x1 = np.concatenate([x1, np.zeros(hi - lo - len(x1), np.uint8)])  # the padded tail
+        want = mul[c0][x0] ^ mul[c1][x1]
+        assert par[lo:hi].cpu().numpy().tobytes() == want.tobytes(), lo
+    del par, src
+    d2, _ = _enc_descs(1, 2 * (1 << 31), k, m)
+    with pytest.raises(Error):
+        engine.encode_batch(d2, 1, 1)  # rejected before any address is touched

@@ -82,3 +82,17 @@ def test_product_policy_custom_clamps_and_empty():
     assert piece.piece_length(1 << 20, max_size=1 << 16) == 1 << 16
     with pytest.raises(ValueError):  # math.log2(0), as the reference
         piece.piece_length(0)
+
+
+def test_new_bytes_fill_in_place():
+    # storb_amd.piece._new_bytes: a fresh bytes object filled through its buffer before it is
+    # shared (the parallel piece copies); it must behave as any other bytes afterwards
+    from storb_amd.piece import _fill, _new_bytes
+    import numpy as np
+
+    b, v = _new_bytes(1000)
+    _fill(v, np.arange(700, dtype=np.uint8))
+    want = bytes(np.arange(700, dtype=np.uint8)) + bytes(300)
+    assert type(b) is bytes and b == want and hash(b) == hash(want)
+    e, ev = _new_bytes(0)
+    assert e == b"" and ev.size == 0

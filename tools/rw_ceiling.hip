@@ -7,7 +7,8 @@
 // 256-lane workgroup per 4 KiB * U of each stream, like the product kernels.
 //   read        1 GiB of loads (XOR-reduced into one dword per workgroup, kept live)
 //   write       1 GiB of stores
-//   copy_U*     1 GiB -> 1 GiB (the 1:1 mix of a decode)
+//   copy_U*     1 GiB -> 1 GiB (the 1:1 mix of a decode); copy_lanes* the same with 64- to
+//               1024-lane workgroups (16 B per lane, one step)
 //   enc         RS(4,2)-shaped: 4 blocks read, 2 written per 1 MiB chunk (2:1, C2 encode)
 //   dec         RS(4,2) reassemble-shaped ({1,3} erased): blocks 0, 2 and both parity blocks
 //               read, 4 rows written (1:1, C3 decode), copies stored after the recovered rows
@@ -62,16 +63,16 @@ __global__ __launch_bounds__(256) void k_write(u8 *__restrict__ out)
 }
 
 template <int U>
-__global__ __launch_bounds__(256) void k_copy(const u8 *__restrict__ in, u8 *__restrict__ out)
+__global__ __launch_bounds__(1024) void k_copy(const u8 *__restrict__ in, u8 *__restrict__ out)
 {
-    const size_t o = (size_t)blockIdx.x * 4096 * U + threadIdx.x * 16;
+    const size_t o = (size_t)blockIdx.x * blockDim.x * 16 * U + threadIdx.x * 16;
     u32x4 x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        x[u] = ld(in + o + u * 4096);
+        x[u] = ld(in + o + u * blockDim.x * 16);
 #pragma unroll
     for (int u = 0; u < U; ++u)
-        st(out + o + u * 4096, x[u]);
+        st(out + o + u * blockDim.x * 16, x[u]);
 }
 
 __global__ __launch_bounds__(256) void k_enc(const u8 *__restrict__ in, u8 *__restrict__ par)
@@ -158,13 +159,18 @@ int main()
     const double cp1 = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_copy<1>), dim3(G / 4096), blk, 0, 0, a, c); }));
     const double cp2 = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_copy<2>), dim3(G / 8192), blk, 0, 0, a, c); }));
     const double cp4 = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_copy<4>), dim3(G / 16384), blk, 0, 0, a, c); }));
+    const double cpl64 = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_copy<1>), dim3(G / 1024), dim3(64), 0, 0, a, c); }));
+    const double cpl128 = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_copy<1>), dim3(G / 2048), dim3(128), 0, 0, a, c); }));
+    const double cpl512 = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_copy<1>), dim3(G / 8192), dim3(512), 0, 0, a, c); }));
+    const double cpl1024 = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_copy<1>), dim3(G / 16384), dim3(1024), 0, 0, a, c); }));
     const double en = rate(1.5 * G, time_ms([&] { hipLaunchKernelGGL(k_enc, dim3(G / 16384), blk, 0, 0, a, b); }));
     const double de = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_dec<false, true>), dim3(G / 16384), blk, 0, 0, a, b, c); }));
     const double dee = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_dec<true, true>), dim3(G / 16384), blk, 0, 0, a, b, c); }));
     const double re = rate(1.5 * G, time_ms([&] { hipLaunchKernelGGL((k_dec<false, false>), dim3(G / 16384), blk, 0, 0, a, b, c); }));
     printf("{\"unit\": \"GB/s\", \"read_U1\": %.1f, \"read_U4\": %.1f, \"write_U1\": %.1f, \"write_U4\": %.1f, "
            "\"copy_U1\": %.1f, \"copy_U2\": %.1f, \"copy_U4\": %.1f, \"enc\": %.1f, \"dec\": %.1f, \"dec_early\": %.1f, "
-           "\"rec\": %.1f}\n", rd, rd4, wr, wr4, cp1, cp2, cp4, en, de, dee, re);
+           "\"rec\": %.1f, \"copy_lanes64\": %.1f, \"copy_lanes128\": %.1f, \"copy_lanes512\": %.1f, "
+           "\"copy_lanes1024\": %.1f}\n", rd, rd4, wr, wr4, cp1, cp2, cp4, en, de, dee, re, cpl64, cpl128, cpl512, cpl1024);
     CK(hipDeviceSynchronize());
     return 0;
 }
