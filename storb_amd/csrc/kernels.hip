@@ -133,19 +133,45 @@ struct Sel {  // the 3 v_perm selectors of each dword of x: bits 0-2, 3-5, 6-7 o
 };
 __device__ __forceinline__ u32 perm(u32 hi, u32 lo, u32 sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
 
+// SEC_LDS_TAB: v_perm is VOP3, which reads at most one SGPR, so with every table dword in
+// SGPRs (scalar loads) one source of perm(c[1], c[0]) and of perm(c[3], c[2]) is first copied
+// into a VGPR: 2 v_mov per coefficient and wave, 0.5 per dword and row at U = 1 (8 % of C4's
+// encode VALU).  With the knob on, each wave keeps dwords 1 and 3 of its batch's coefficients
+// in its own slice of LDS (filled by vector loads at the batch's start; the same wave writes
+// and reads it, so no barrier), and the products read them with one ds_read_b64 per
+// coefficient instead of the two v_mov.
+// SEC_LDS_TAB = 0 off, 1 every tile kernel, 2 (default) the encode kernels of 8-row groups
+// only.  Against the SGPR-only build (profiles/r02_ldstab.jsonl, one process per shape):
+// encode of 8-row groups zfec(16,24) +4 %, (32,48) +1 %, (64,96) +5 %; but C2 encode -6 %,
+// C4 -3 %, C5 -6 %, and the wide decodes -35 % (VGPR spills), so it stays off there.
+#ifndef SEC_LDS_TAB
+#define SEC_LDS_TAB 2
+#endif
+template <int R, bool DEC>
+__host__ __device__ constexpr bool lds_tab() { return SEC_LDS_TAB == 1 || (SEC_LDS_TAB == 2 && !DEC && R == 8); }
+using u32x2 = uint2;
+
 // acc[r] ^= coefficient(r) * x for one block: 3 v_perm + 2 XOR per dword and row
-template <int R, int U>
-__device__ __forceinline__ void gf_mac(u32x4 (&acc)[R][U], const u32x4 (&x)[U], const u32 *__restrict__ t)
+// (t: the block's first row's 5 table dwords; v: its dwords 1 and 3 in LDS, SEC_LDS_TAB only)
+template <int R, int U, bool LT = false>
+__device__ __forceinline__ void gf_mac(u32x4 (&acc)[R][U], const u32x4 (&x)[U], const u32 *__restrict__ t,
+                                       const u32x2 *v)
 {
     const Sel<U> s(x);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const u32 *c = t + r * 5;
+        u32 c1 = c[1], c3 = c[3];
+        if constexpr (LT) {
+            const u32x2 h = v[r];
+            c1 = h.x;
+            c3 = h.y;
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int w = 0; w < 4; ++w)
-                acc[r][u][w] = xor3(acc[r][u][w], perm(c[1], c[0], s.s0[u][w]), perm(c[3], c[2], s.s1[u][w])) ^
+                acc[r][u][w] = xor3(acc[r][u][w], perm(c1, c[0], s.s0[u][w]), perm(c3, c[2], s.s1[u][w])) ^
                                perm(c[4], c[4], s.s2[u][w]);
     }
 }
@@ -167,24 +193,60 @@ __host__ __device__ constexpr bool kPairRows() { return R <= (W ? SEC_WIDE_PAIR_
 
 // Two blocks at once: the 6 products of a dword and row go into acc by 3 XOR3s, so 3 v_perm
 // + 1.5 XOR per dword, row and block (a 4-term XOR chain in C took 3 v_xor_b32 per block)
-template <int R, int U>
+template <int R, int U, bool LT = false>
 __device__ __forceinline__ void gf_mac2(u32x4 (&acc)[R][U], const u32x4 (&x)[U], const u32 *__restrict__ t,
-                                        const u32x4 (&y)[U], const u32 *__restrict__ q)
+                                        const u32x2 *v, const u32x4 (&y)[U], const u32 *__restrict__ q,
+                                        const u32x2 *vq)
 {
     const Sel<U> s(x), z(y);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const u32 *c = t + r * 5, *d = q + r * 5;
+        u32 c1 = c[1], c3 = c[3], d1 = d[1], d3 = d[3];
+        if constexpr (LT) {
+            const u32x2 h = v[r], g = vq[r];
+            c1 = h.x;
+            c3 = h.y;
+            d1 = g.x;
+            d3 = g.y;
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
-                u32 a = xor3(acc[r][u][w], perm(c[1], c[0], s.s0[u][w]), perm(c[3], c[2], s.s1[u][w]));
-                a = xor3(a, perm(c[4], c[4], s.s2[u][w]), perm(d[1], d[0], z.s0[u][w]));
-                acc[r][u][w] = xor3(a, perm(d[3], d[2], z.s1[u][w]), perm(d[4], d[4], z.s2[u][w]));
+                u32 a = xor3(acc[r][u][w], perm(c1, c[0], s.s0[u][w]), perm(c3, c[2], s.s1[u][w]));
+                a = xor3(a, perm(c[4], c[4], s.s2[u][w]), perm(d1, d[0], z.s0[u][w]));
+                acc[r][u][w] = xor3(a, perm(d3, d[2], z.s1[u][w]), perm(d[4], d[4], z.s2[u][w]));
             }
     }
 }
+
+// SEC_LDS_TAB: this wave's LDS slice, filled by its active lanes with dwords 1 and 3 of the tables of blocks
+// j0 .. j0 + KB - 1 (those < k), rows 0 .. R - 1 (tj: row 0 of block 0, tstep: dwords per
+// block), entry c * R + r.  The launch passes (lanes / 64) * KB * R * 8 bytes of dynamic LDS.
+template <int KB, int R, bool LT>
+__device__ __forceinline__ const u32x2 *wave_tabs(const u32 *__restrict__ tj, u32 tstep, u32 j0, u32 k)
+{
+    extern __shared__ u32x2 s_vt[];
+    u32x2 *vt = s_vt + (threadIdx.x >> 6) * (KB * R);
+    if constexpr (LT && R > 0) {
+        // the wave's active lanes share the fill (lanes past a tile's `valid` never get here)
+        const u64 live = __builtin_amdgcn_read_exec();
+        const u32 rank = __builtin_amdgcn_mbcnt_hi((u32)(live >> 32), __builtin_amdgcn_mbcnt_lo((u32)live, 0u));
+        const u32 nlive = (u32)__builtin_popcountll(live);
+        for (u32 i = rank; i < (u32)(KB * R); i += nlive) {
+            const u32 c = i / R, r = i % R;
+            if (j0 + c < k) {
+                const u32 *src = tj + (j0 + c) * tstep + r * sec::kTabDwords;
+                vt[i] = u32x2{src[1], src[3]};
+            }
+        }
+    }
+    return vt;
+}
+// Dynamic LDS bytes of a tile launch (0 without SEC_LDS_TAB)
+template <int KB, int R, bool DEC>
+constexpr u32 lds_tab_bytes(u32 lanes) { return lds_tab<R, DEC>() ? lanes / 64 * KB * R * 8 : 0; }
 
 // Build knobs (A/B variants are compiled as separate libraries by tools/sweep.py):
 //   SEC_NT_LOAD / SEC_NT_STORE  nontemporal (streaming) global loads / stores: every
@@ -234,6 +296,13 @@ __device__ __forceinline__ void gf_mac2(u32x4 (&acc)[R][U], const u32x4 (&x)[U],
 #ifndef SEC_FIXED_K
 #define SEC_FIXED_K 0
 #endif
+// Blocks (slots) per batch of a tile kernel: KB * U = the batch's 16 B vectors per lane
+template <int U, bool W, bool DEC>
+constexpr int batch_blocks()
+{
+    constexpr int v = (W && SEC_WIDE_BATCH > 0) ? SEC_WIDE_BATCH : (DEC ? SEC_DEC_BATCH : SEC_ENC_BATCH);
+    return v / U > 0 ? v / U : 1;
+}
 
 __device__ __forceinline__ u32x4 load16(const u8 *p)
 {
@@ -319,9 +388,10 @@ __device__ __forceinline__ void encode_main(const u8 *__restrict__ in, u8 *__res
     // loads in flight; C2 (k = 4) and C4 (k = 10) are one batch.  A one-block-ahead prefetch
     // loop compiled to a full wait at its head (the next block's load included): one load in
     // flight per lane and u-step, C2 -3.5 %, C4 -9 % (profiles/r01_sweep_enc_batch.jsonl).
-    constexpr int KBV = (W && SEC_WIDE_BATCH > 0) ? SEC_WIDE_BATCH : SEC_ENC_BATCH;
-    constexpr int KB = KBV / U > 0 ? KBV / U : 1;
+    constexpr int KB = batch_blocks<U, W, false>();
     auto batch = [&](u32 j0) {
+        constexpr bool LT = lds_tab<R, false>();
+        const u32x2 *vt = wave_tabs<KB, R, LT>(tj, tstep, j0, k);
         u32x4 xs[KB][U];
 #pragma unroll
         for (int c = 0; c < KB; ++c)
@@ -334,15 +404,16 @@ __device__ __forceinline__ void encode_main(const u8 *__restrict__ in, u8 *__res
 #pragma unroll
             for (int c = 0; c < KB; c += 2) {
                 if (c + 1 < KB && j0 + c + 1 < k)
-                    gf_mac2<R, U>(acc, xs[c], tj + (j0 + c) * tstep, xs[c + 1], tj + (j0 + c + 1) * tstep);
+                    gf_mac2<R, U, LT>(acc, xs[c], tj + (j0 + c) * tstep, vt + c * R, xs[c + 1],
+                                  tj + (j0 + c + 1) * tstep, vt + (c + 1) * R);
                 else if (j0 + c < k)
-                    gf_mac<R, U>(acc, xs[c], tj + (j0 + c) * tstep);
+                    gf_mac<R, U, LT>(acc, xs[c], tj + (j0 + c) * tstep, vt + c * R);
             }
         } else {
 #pragma unroll
             for (int c = 0; c < KB; ++c)
                 if (j0 + c < k)
-                    gf_mac<R, U>(acc, xs[c], tj + (j0 + c) * tstep);
+                    gf_mac<R, U, LT>(acc, xs[c], tj + (j0 + c) * tstep, vt + c * R);
         }
     };
     // W (wide k, U = 1 only): k > KB, several batches.  A separate instantiation: merely
@@ -532,9 +603,10 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
     // Slots go in batches of KB, as in encode_main: every load of a batch before any store
     // or arithmetic, then the batch in order — each present primary copied to its output
     // row, every slot fed to the R accumulators.  C2 / C4 are one batch (all loads in flight).
-    constexpr int KBV = (W && SEC_WIDE_BATCH > 0) ? SEC_WIDE_BATCH : SEC_DEC_BATCH;
-    constexpr int KB = KBV / U > 0 ? KBV / U : 1;
+    constexpr int KB = batch_blocks<U, W, true>();
     auto batch = [&](u32 c0) {
+        constexpr bool LT = lds_tab<R, true>();
+        const u32x2 *vt = wave_tabs<KB, R, LT>(tj, tstep, c0, k);
         u32x4 xs[KB][U];
 #pragma unroll
         for (int c = 0; c < KB; ++c)
@@ -549,15 +621,16 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
 #pragma unroll
                 for (int c = 0; c < KB; c += 2) {
                     if (c + 1 < KB && c0 + c + 1 < k)
-                        gf_mac2<R, U>(acc, xs[c], tj + (c0 + c) * tstep, xs[c + 1], tj + (c0 + c + 1) * tstep);
+                        gf_mac2<R, U, LT>(acc, xs[c], tj + (c0 + c) * tstep, vt + c * R, xs[c + 1],
+                                      tj + (c0 + c + 1) * tstep, vt + (c + 1) * R);
                     else if (c0 + c < k)
-                        gf_mac<R, U>(acc, xs[c], tj + (c0 + c) * tstep);
+                        gf_mac<R, U, LT>(acc, xs[c], tj + (c0 + c) * tstep, vt + c * R);
                 }
             } else if constexpr (R > 0) {
 #pragma unroll
                 for (int c = 0; c < KB; ++c)
                     if (c0 + c < k)
-                        gf_mac<R, U>(acc, xs[c], tj + (c0 + c) * tstep);
+                        gf_mac<R, U, LT>(acc, xs[c], tj + (c0 + c) * tstep, vt + c * R);
             }
         } else {
 #pragma unroll
@@ -571,7 +644,7 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
                             store16<SEC_DEC_ST>(o + pos[u], xs[c][u]);
                     }
                     if constexpr (R > 0)
-                        gf_mac<R, U>(acc, xs[c], tj + (c0 + c) * tstep);
+                        gf_mac<R, U, LT>(acc, xs[c], tj + (c0 + c) * tstep, vt + c * R);
                 }
         }
         if (SEC_DEC_LATE)  // the batch's copies after its arithmetic
@@ -813,27 +886,34 @@ thread_local hipEvent_t t_start = nullptr, t_stop = nullptr;
 thread_local int t_launched = 0;
 
 template <class K, class... A>
-hipError_t launch(K kernel, dim3 grid, dim3 block, hipStream_t s, A... args)
+hipError_t launch_shm(K kernel, dim3 grid, dim3 block, u32 shm, hipStream_t s, A... args)
 {
     hipEvent_t a = t_start;
     t_start = nullptr;
     ++t_launched;
-    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, a, t_stop, 0, args...);
+    hipExtLaunchKernelGGL(kernel, grid, block, shm, s, a, t_stop, 0, args...);
     return hipGetLastError();
+}
+template <class K, class... A>
+hipError_t launch(K kernel, dim3 grid, dim3 block, hipStream_t s, A... args)
+{
+    return launch_shm(kernel, grid, block, 0, s, args...);
 }
 
 template <int R, int U, bool W>
 hipError_t launch_enc(const u8 *in, u8 *par, const sec::EncDesc *descs, const sec::Tile *tiles, u32 ntiles,
                       const u32 *tabs, u32 lanes, hipStream_t s)
 {
-    return launch(sec_encode_kernel<R, U, W>, dim3(ntiles), dim3(lanes), s, in, par, descs, tiles, tabs);
+    return launch_shm(sec_encode_kernel<R, U, W>, dim3(ntiles), dim3(lanes),
+                      lds_tab_bytes<batch_blocks<U, W, false>(), R, false>(lanes), s, in, par, descs, tiles, tabs);
 }
 
 template <int R, int U, bool W>
 hipError_t launch_dec(const u8 *blocks, u8 *out, const sec::DecDesc *descs, const sec::Tile *tiles, u32 ntiles,
                       const u32 *tabs, sec::DecSlots sl, u32 lanes, hipStream_t s)
 {
-    return launch(sec_decode_kernel<R, U, W>, dim3(ntiles), dim3(lanes), s, blocks, out, descs, tiles, tabs, sl);
+    return launch_shm(sec_decode_kernel<R, U, W>, dim3(ntiles), dim3(lanes),
+                      lds_tab_bytes<batch_blocks<U, W, true>(), R, true>(lanes), s, blocks, out, descs, tiles, tabs, sl);
 }
 
 template <int U, bool W>

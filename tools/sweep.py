@@ -61,6 +61,11 @@ VARIANTS = {
     "lb512p8": {"SEC_LB_WIDE_ROWS": 512, "SEC_PAIR_ROWS": 8},
     # bit-sliced MFMA encode (kernels_mfma.hip): one wave per SIMD with the q steps unrolled
     "mfw1": {"SEC_MFMA_WAVES": 1, "SEC_MFMA_QU": 4},
+    # table dwords 1 and 3 from a per-wave LDS copy instead of v_mov from SGPRs (SEC_LDS_TAB)
+    # (default 2: encode kernels of 8-row groups only; 1: every tile kernel; 0: none)
+    "ldstab": {"SEC_LDS_TAB": 1},
+    "ldstab_fk10": {"SEC_LDS_TAB": 1, "SEC_FIXED_K": 10},
+    "noldstab": {"SEC_LDS_TAB": 0},
 }
 
 
