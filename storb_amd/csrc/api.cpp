@@ -954,6 +954,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         sp.off_desc = img.put(descs.data(), descs.size() * sizeof(sec::DecDesc));
         sp.off_tiles = img.put(tiles.data(), tiles.size() * sizeof(sec::Tile));
         sp.off_tail = img.put(tail.data(), tail.size() * sizeof(sec::TailItem));
+        soff.resize(soff.size() + sec::kBatchVecs, 0);  // the kernels load a batch's offsets unconditionally
         sp.off_soff = img.put(soff.data(), soff.size() * 8);
         sp.off_srow = img.put(srow.data(), srow.size() * 4);
         sp.off_mrow = img.put(mrow.data(), mrow.size() * 4);

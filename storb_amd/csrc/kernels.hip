@@ -607,11 +607,18 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
     auto batch = [&](u32 c0) {
         constexpr bool LT = lds_tab<R, true>();
         const u32x2 *vt = wave_tabs<KB, R, LT>(tj, tstep, c0, k);
+        // the batch's block offsets in one go (the plan pads sl.off by kBatchVecs entries): one
+        // offset loaded and waited for per slot would put KB scalar round trips before the last load
+        u64 so[KB];
+        const u64 *sop = sl.off + d.slot0 + c0;
+#pragma unroll
+        for (int c = 0; c < KB; ++c)
+            so[c] = sop[c];
         u32x4 xs[KB][U];
 #pragma unroll
         for (int c = 0; c < KB; ++c)
             if (c0 + c < k) {
-                const u8 *s = blocks + sl.off[d.slot0 + c0 + c];
+                const u8 *s = blocks + so[c];
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     xs[c][u] = load16(s + pos[u]);

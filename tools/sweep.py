@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--us", default="1,2,4")
     ap.add_argument("--palign", type=int, default=1, help="parity stride rounded up to this many bytes")
     ap.add_argument("--workload", default="c2", help="c2 | c4 | nch,n,k,m (custom shape)")
+    ap.add_argument("--recover", action="store_true", help="also time recover-only decodes (not c5)")
     a = ap.parse_args()
     # a variant is TAG or TAG@ENV=VALUE: the TAG build, with ENV set while its plan is built
     specs = a.variants.split(",")
@@ -130,6 +131,12 @@ def main():
         dd, sn, offs, av = dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), erased, ps)
         enc_bytes = nch * (n + (m - k) * B)
         dec_bytes = nch * (k * B + n)
+        if a.recover:  # SEC_F_RECOVER: the e missing primaries only, e * B per chunk
+            ne = sum(1 for s in erased if s < k)
+            rd, rsn, roffs, rav = dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), erased, ps, recover=True)
+            rec = torch.empty(nch * ne * B, dtype=torch.uint8, device="cuda")
+            rec_bytes = nch * (k + ne) * B
+    recov = a.recover and a.workload != "c5"
 
     configs = [(v, int(u)) for v in specs for u in a.us.split(",")]
     engines = {}
@@ -145,13 +152,15 @@ def main():
         out.zero_()
         e.encode_batch(ed, src, par, asynchronous=True)
         e.decode_batch(dd, sn, offs, 0, out, block_avail=av, asynchronous=True)
+        if recov:
+            e.decode_batch(rd, rsn, roffs, 0, rec, block_avail=rav, recover_only=True, asynchronous=True)
         e.sync()
         assert torch.equal(out, src), (v, u)
         engines[(v, u)] = e
         if env:
             os.environ.pop(env.split("=")[0])
     os.environ.pop("SEC_TILE_U", None)
-    samples = {c: ([], []) for c in configs}
+    samples = {c: ([], [], []) for c in configs}
     for _ in range(a.rounds):
         for c in configs:
             e = engines[c]
@@ -166,12 +175,28 @@ def main():
             samples[c][0].append(ms / nl)
             ms, nl = e.collect_timing("decode")
             samples[c][1].append(ms / nl)
+            if recov:
+                e.set_timing(True)
+                for _ in range(a.reps):
+                    e.decode_batch(rd, rsn, roffs, 0, rec, block_avail=rav, recover_only=True, asynchronous=True)
+                e.sync()
+                e.set_timing(False)
+                ms, nl = e.collect_timing("decode")
+                samples[c][2].append(ms / nl)
     # the timed calls must have produced the same bytes (a fast wrong kernel is not a result)
     ref_par = par.clone()
     engines[configs[0]].encode_batch(ed, src, ref_par, asynchronous=True)
     engines[configs[0]].sync()
     bad = set()
+    if recov:
+        ref_rec = rec.clone()
     for c in configs:
+        if recov:
+            rec.zero_()
+            engines[c].decode_batch(rd, rsn, roffs, 0, rec, block_avail=rav, recover_only=True, asynchronous=True)
+            engines[c].sync()
+            if not torch.equal(rec, ref_rec):
+                bad.add(c)
         out.zero_()
         par.zero_()
         engines[c].encode_batch(ed, src, par, asynchronous=True)
@@ -181,12 +206,16 @@ def main():
             bad.add(c)
     for c in configs:
         enc, dec = np.array(samples[c][0]), np.array(samples[c][1])
+        extra = {}
+        if recov:
+            rv = np.array(samples[c][2])
+            extra = {"rec_ms_med": round(float(np.median(rv)), 4), "rec_GBs": round(rec_bytes / np.median(rv) / 1e6, 1)}
         print(json.dumps({"variant": c[0], "U": c[1], "workload": a.workload, "palign": a.palign,
                           "enc_ms_med": round(float(np.median(enc)), 4), "enc_GBs": round(enc_bytes / np.median(enc) / 1e6, 1),
                           "enc_GBs_best": round(enc_bytes / enc.min() / 1e6, 1),
                           "dec_ms_med": round(float(np.median(dec)), 4), "dec_GBs": round(dec_bytes / np.median(dec) / 1e6, 1),
                           "dec_GBs_best": round(dec_bytes / dec.min() / 1e6, 1),
-                          "verified": c not in bad}), flush=True)
+                          **extra, "verified": c not in bad}), flush=True)
 
 
 if __name__ == "__main__":
