@@ -5,7 +5,8 @@ JSON object.  Complements bench.py (which is the C2+C3 headline line).
     python tools/bench_configs.py > gpurun_out/configs.json
 
 C1  see tools/c1_loopback.py.
-C2/C3  1024 x 1 MiB RS(4,2) encode / decode ({1,3} erased), device-resident.
+C2/C3  1024 x 1 MiB RS(4,2) encode / decode ({1,3} erased), device-resident; C3 also over
+    the erasure sets of SURVEY 8(d) (c3_patterns), reassemble and recover-only.
 C4  8192 x 64 KiB RS(10,4) (one GPU's share of 65536), device-resident encode / decode with
     data blocks {0,2,5,7} erased (block 9, zfec's padded one, read in place: avail = B - padlen).
 C5  mixed chunk sizes log-uniform in [4 KiB, 4 MiB] (seed 5) up to ~1 GiB, RS(8,3):
@@ -118,6 +119,65 @@ def device_case(eng, sizes, k, m, erased, reps=20):
             "decode_hbm_GBs": round(dec_bytes / td / 1e9, 1)}
 
 
+C3_PATTERNS = ((1, 3), (0, 1), (2, 3), (1, 4), (0, 5), (4, 5))
+
+
+def c3_patterns(eng, nch=1024, n=1 << 20, k=4, m=6, reps=10, rounds=5):
+    """C3 decode over several erasure sets: two data blocks ({1,3}, {0,1}, {2,3}),
+    a data block and a parity block ({1,4}, {0,5}: one row recovered) and both parity blocks
+    ({4,5}: a pure reassembly).  Reassemble (kB read + n written) and recover-only (kB read +
+    eB written) kernel rates, outputs checked against the source bytes.  The patterns are
+    timed round-robin, `rounds` times `reps` launches each, median per pattern (timed one after
+    the other, the first pattern of a process measured up to 5 % low)."""
+    import torch
+
+    sizes = [n] * nch
+    ed, B = enc_descs_var(sizes, k, m)
+    B = int(B[0])
+    src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
+    par = torch.empty(nch * (m - k) * B, dtype=torch.uint8, device="cuda")
+    out = torch.empty_like(src)
+    eng.encode_batch(ed, src, par)
+    cases = []  # (name, mode, bytes per launch, launch function)
+    for erased in C3_PATTERNS:
+        name = "{" + ",".join(map(str, erased)) + "}"
+        dd, sn, offs, av = dec_descs_var(sizes, k, m, np.full(nch, B, np.uint64), src.data_ptr(), par.data_ptr(), erased)
+        out.zero_()
+        eng.decode_batch(dd, sn, offs, 0, out, block_avail=av)
+        assert torch.equal(out, src), erased
+        cases.append((name, "reassemble", nch * (k * B + n),
+                      lambda dd=dd, sn=sn, offs=offs, av=av: eng.decode_batch(dd, sn, offs, 0, out, block_avail=av,
+                                                                                 asynchronous=True)))
+        lost = sorted(s for s in erased if s < k)
+        if lost:
+            e = len(lost)
+            rd = dd.copy()
+            rd["out_off"] = np.arange(nch, dtype=np.uint64) * (e * B)
+            rec = torch.empty(nch * e * B, dtype=torch.uint8, device="cuda")
+            eng.decode_batch(rd, sn, offs, 0, rec, block_avail=av, recover_only=True)
+            r3, s3 = rec.view(nch, e, B), src.view(nch, k, B)
+            for j, blk in enumerate(lost):
+                assert torch.equal(r3[:, j], s3[:, blk]), (erased, blk)
+            cases.append((name, "recover_only", nch * (k + e) * B,
+                          lambda rd=rd, sn=sn, offs=offs, av=av, rec=rec: eng.decode_batch(
+                              rd, sn, offs, 0, rec, block_avail=av, recover_only=True, asynchronous=True)))
+    samples = {(c[0], c[1]): [] for c in cases}
+    for _ in range(rounds):
+        for name, mode, _, fn in cases:
+            eng.set_timing(True)
+            for _ in range(reps):
+                fn()
+            eng.sync()
+            eng.set_timing(False)
+            ms, nl = eng.collect_timing("decode")
+            samples[(name, mode)].append(ms / nl / 1e3)
+    res = {}
+    for name, mode, nbytes, _ in cases:
+        t = float(np.median(samples[(name, mode)]))
+        res.setdefault(name, {}).update({f"{mode}_ms": round(t * 1e3, 4), f"{mode}_hbm_GBs": round(nbytes / t / 1e9, 1)})
+    return res
+
+
 def sha1_case(eng, nch=1024, n=1 << 20, k=4, m=6, reps=5):
     """F1: SHA-1 of all m pieces of every C2 chunk on the device, alone and fused after encode."""
     import torch
@@ -184,6 +244,7 @@ def main():
     res = {}
 
     res["c2_c3_1024x1MiB_rs(4,2)"] = device_case(eng, [1 << 20] * 1024, 4, 6, (1, 3))
+    res["c3_erasure_patterns_1024x1MiB_rs(4,2)"] = c3_patterns(eng)
     res["c4_8192x64KiB_rs(10,4)_per_gpu"] = device_case(eng, [65536] * 8192, 10, 14, (0, 2, 5, 7))
     sizes = c5_sizes()
     res["c5_mixed_4KiB-4MiB_rs(8,3)_device"] = device_case(eng, sizes, 8, 11, (1, 3, 5))

@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--palign", type=int, default=1, help="parity stride rounded up to this many bytes")
     ap.add_argument("--workload", default="c2", help="c2 | c4 | nch,n,k,m (custom shape)")
     ap.add_argument("--recover", action="store_true", help="also time recover-only decodes (not c5)")
+    ap.add_argument("--erased", default="", help="erased block numbers, e.g. 1,3 (not c5; default per workload)")
     a = ap.parse_args()
     # a variant is TAG or TAG@ENV=VALUE: the TAG build, with ENV set while its plan is built
     specs = a.variants.split(",")
@@ -122,6 +123,8 @@ def main():
         else:
             nch, n, k, m = map(int, a.workload.split(","))
             erased = tuple(range(0, k, 2))[: m - k]
+        if a.erased:
+            erased = tuple(int(x) for x in a.erased.split(","))
         src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
         B = -(-n // k)
         ps = -(-B // a.palign) * a.palign
@@ -211,6 +214,7 @@ def main():
             rv = np.array(samples[c][2])
             extra = {"rec_ms_med": round(float(np.median(rv)), 4), "rec_GBs": round(rec_bytes / np.median(rv) / 1e6, 1)}
         print(json.dumps({"variant": c[0], "U": c[1], "workload": a.workload, "palign": a.palign,
+                          **({"erased": a.erased} if a.erased else {}),
                           "enc_ms_med": round(float(np.median(enc)), 4), "enc_GBs": round(enc_bytes / np.median(enc) / 1e6, 1),
                           "enc_GBs_best": round(enc_bytes / enc.min() / 1e6, 1),
                           "dec_ms_med": round(float(np.median(dec)), 4), "dec_GBs": round(dec_bytes / np.median(dec) / 1e6, 1),
