@@ -226,3 +226,29 @@ def test_avail_is_honoured_not_read_past():
     out = torch.empty(n, dtype=torch.uint8, device="cuda")
     eng.decode_batch(dd, sn, offs, 0, out, block_avail=np.array([B, B - 3, B, B], np.uint64))
     assert out.cpu().numpy().tobytes() == data
+
+
+def test_pure_reassembly_shapes(engine):
+    """Decodes with nothing to recover (every primary present, parity ignored: the R = 0
+    kernel) over tiny chunks (tail items), ragged ends with block k-1 short and read in place,
+    wide k (the W instantiation), and mixed with recovering chunks in one batch; the output is
+    the source bytes."""
+    rng = random.Random(7)
+    for k, m in [(1, 2), (2, 3), (4, 6), (10, 14), (32, 48)]:
+        sizes = [1, 5, 16 * k - 3, 4096 * k, 65536, 1 << 20, 3 * 65536 + 7] + [rng.randrange(1, 200000) for _ in range(9)]
+        # zfec needs a non-empty last block: n > (k - 1) * ceil(n / k)
+        sizes = [s for s in sizes if s > (k - 1) * -(-s // k)]
+        total = sum(sizes)
+        src = _dev(total, 100 + k)
+        par = _encode(engine, sizes, k, m, src)
+        # every other chunk keeps its primaries (pure reassembly); the rest lose block 0
+        keeps = [list(range(k)) if i % 2 == 0 else [s for s in range(1, m)][:k] for i in range(len(sizes))]
+        d, sn, offs, avail, nout = _dec_inputs(sizes, k, m, keeps, src.data_ptr(), par.data_ptr())
+        out = torch.zeros(nout, dtype=torch.uint8, device="cuda")
+        engine.decode_batch(d, sn, offs, 0, out, block_avail=avail)
+        assert torch.equal(out, src), (k, m)
+        keeps = [list(range(k))] * len(sizes)  # all chunks pure reassembly
+        d, sn, offs, avail, nout = _dec_inputs(sizes, k, m, keeps, src.data_ptr(), par.data_ptr())
+        out.zero_()
+        engine.decode_batch(d, sn, offs, 0, out, block_avail=avail)
+        assert torch.equal(out, src), (k, m, "all e=0")
