@@ -7,7 +7,8 @@
 // offset t of S streams chunk + t + s * D (s < S), 16 B per lane, nontemporal, XOR-reduced.
 // Also: the same S streams with a write of each stream to a second buffer (a 1:1 copy of S
 // rows), which is the reassembling decode's mix.  20 launches per timing, median of 7.
-// Prints one JSON object per (S, D): read GB/s and copy GB/s.
+// Prints one JSON object per (S, D): read GB/s and copy GB/s; first, hipMemcpyAsync's own
+// device-to-device rate over the same 1 GiB (read + write bytes).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
@@ -101,6 +102,11 @@ int main()
         return 1;
     (void)hipMemset(a, 7, G);
     (void)hipMemset(c, 3, G);
+    {  // the runtime's own device-to-device copy (its blit kernel), for reference
+        const double ms = time_ms([&] { (void)hipMemcpyAsync(c, a, G, hipMemcpyDeviceToDevice, 0); });
+        printf("{\"hipMemcpyAsync_d2d_1GiB_GBs\": %.1f}\n", 2.0 * G / (ms * 1e-3) / 1e9);
+        fflush(stdout);
+    }
     const size_t K = 1024;
     for (size_t d : {64 * K, 128 * K, 256 * K, 384 * K, 512 * K, 640 * K, 1024 * K, 2048 * K}) {
         run<1>(a, c, sink, d);
