@@ -252,3 +252,80 @@ def test_pure_reassembly_shapes(engine):
         out.zero_()
         engine.decode_batch(d, sn, offs, 0, out, block_avail=avail)
         assert torch.equal(out, src), (k, m, "all e=0")
+
+
+def test_fuzz_mixed_shapes_erasures_one_batch(engine):
+    """Randomized: 160 chunks of random (k, m) (1 <= k <= 40, up to m = 2k + 3) and random
+    sizes in ONE device encode and ONE device decode, each chunk with a random set of k
+    surviving blocks in random order (parity-only survivors included), block k-1 read in place
+    when it survives; then the recover-only decode of the same batch.  Parity and every
+    recovered row against the oracle (oracle/fec_oracle.c) on a sample, reassembly against the
+    source bytes everywhere."""
+    rng = random.Random(2024)
+    shapes, sizes = [], []
+    while len(shapes) < 160:
+        k = rng.choice([1, 2, 3, 4, 5, 8, 10, 13, 16, 17, 24, 32, 40])
+        m = min(256, k + rng.randrange(1, k + 4))
+        n = rng.randrange(1, 150000)
+        if n <= (k - 1) * -(-n // k):  # zfec: the last block must be non-empty
+            continue
+        shapes.append((k, m))
+        sizes.append(n)
+    total = sum(sizes)
+    src = _dev(total, 77)
+    # encode: one batch of mixed shapes (per-chunk layout as _layout, but per-chunk k, m)
+    B = [-(-n // k) for n, (k, m) in zip(sizes, shapes)]
+    in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    pcount = [b * (m - k) for b, (k, m) in zip(B, shapes)]
+    par_off = np.concatenate([[0], np.cumsum(pcount)[:-1]]).astype(np.uint64)
+    ed = np.zeros(len(sizes), dtype=ENC_DTYPE)
+    ed["in_off"], ed["n"], ed["parity_off"], ed["parity_stride"] = in_off, sizes, par_off, B
+    ed["k"] = [k for k, _ in shapes]
+    ed["m"] = [m for _, m in shapes]
+    par = torch.empty(max(1, int(sum(pcount))), dtype=torch.uint8, device="cuda")
+    engine.encode_batch(ed, src, par)
+    src_h, par_h = src.cpu().numpy(), par.cpu().numpy()
+    for i in rng.sample(range(len(sizes)), 24):
+        k, m = shapes[i]
+        data = src_h[int(in_off[i]):int(in_off[i]) + sizes[i]].tobytes()
+        want = b"".join(cfec.easy_encode(data, k, m)[k:])
+        assert par_h[int(par_off[i]):int(par_off[i]) + pcount[i]].tobytes() == want, (i, k, m, sizes[i])
+    # decode: random survivors per chunk, every slot read in place
+    keeps = [rng.sample(range(m), k) for (k, m) in shapes]
+    nslots = sum(k for k, _ in shapes)
+    for recover in (False, True):
+        dd = np.zeros(len(sizes), dtype=DEC_DTYPE)
+        sn = np.zeros(nslots, np.int32)
+        offs = np.zeros(nslots, np.uint64)
+        avail = np.zeros(nslots, np.uint64)
+        o, slot, lost = 0, 0, []
+        for i, ((k, m), keep) in enumerate(zip(shapes, keeps)):
+            b = B[i]
+            dd["out_off"][i], dd["B"][i], dd["padlen"][i] = o, b, b * k - sizes[i]
+            dd["k"][i], dd["m"][i], dd["slot0"][i] = k, m, slot
+            miss = sorted(s for s in range(k) if s not in keep)
+            lost.append(miss)
+            o += len(miss) * b if recover else sizes[i]
+            for s in keep:
+                sn[slot] = s
+                if s < k:
+                    offs[slot] = src.data_ptr() + int(in_off[i]) + s * b
+                    avail[slot] = sizes[i] - s * b if s == k - 1 else b
+                else:
+                    offs[slot] = par.data_ptr() + int(par_off[i]) + (s - k) * b
+                    avail[slot] = b
+                slot += 1
+        out = torch.zeros(max(o, 1), dtype=torch.uint8, device="cuda")
+        engine.decode_batch(dd, sn, offs, 0, out, block_avail=avail, recover_only=recover)
+        if not recover:
+            assert torch.equal(out[:o], src)
+            continue
+        out_h = out.cpu().numpy()
+        for i, miss in enumerate(lost):
+            k, m = shapes[i]
+            data = src_h[int(in_off[i]):int(in_off[i]) + sizes[i]].tobytes()
+            blocks = cfec.easy_encode(data, k, m)
+            base = int(dd["out_off"][i])
+            for j, r in enumerate(miss):
+                got = out_h[base + j * B[i]:base + (j + 1) * B[i]].tobytes()
+                assert got == blocks[r], (i, k, m, r)
