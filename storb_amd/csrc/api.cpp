@@ -129,7 +129,8 @@ size_t env_size(const char *name, size_t dflt)
 struct Group {
     int rows, U, lanes, wide;  // wide: k > kBatchVecs / U, blocks loaded in several batches
     uint32_t first, count;
-    int mfma = 0;              // sec_encode_mfma_kernel<G = U, TILES = rows> (encode, k = 32 * G)
+    int mfma = 0;              // 1: sec_encode_mfma_kernel<G = U, TILES = rows> (encode, k = 32 * G);
+                               // 2: sec_encode_xb_kernel of shape `rows`, W = U (encode)
 };
 
 // One launch unit: all chunks (device mode) or one slab of chunks (host mode).
@@ -231,7 +232,7 @@ bool is_wide(int k, int U, int rows)
     return U == 1 && rows > 4 && k > k8;
 }
 
-using Bins = std::map<std::tuple<int, int, int, int, int>, std::vector<sec::Tile>>;  // (mfma, rows, U, lanes, wide)
+using Bins = std::map<std::tuple<int, int, int, int, int>, std::vector<sec::Tile>>;  // (kind, rows, U, lanes, wide)
 
 uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 
@@ -341,6 +342,37 @@ uint64_t add_mfma_work(Bins &bins, uint32_t chunk, int64_t valid, int k, int m)
             bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
     }
     return vm;
+}
+
+// Compile-time-matrix encode (kernels_xb.hip) for the shapes it is built for ((64,96), (32,48)):
+// positions [0, sec_xb_end(valid)) in 256-lane tiles of 1024 * W positions, all parity rows
+// per tile; add_xb_work returns where its range ends (sec_encode_kernel's tiles start there,
+// as after add_mfma_work).  Dwords per lane: 2 for (32,48), 1 for (64,96), whose 32
+// accumulators per dword leave no registers for a second (profiles/r02_xb_ab.jsonl: the other
+// width measured -1.5 % / -5 %).  SEC_XB=0 turns it off, SEC_XB_W (1 or 2) forces the width;
+// both read per plan build.
+int xb_shape(int k, int m)
+{
+    const char *e = getenv("SEC_XB");
+    if (e && e[0] == '0')
+        return -1;
+    return sec_xb_shape(k, m);
+}
+
+int xb_width(int shape)
+{
+    const size_t w = env_size("SEC_XB_W", 0);
+    return w == 1 || w == 2 ? (int)w : shape == 1 ? 2 : 1;
+}
+
+uint64_t add_xb_work(Bins &bins, uint32_t chunk, int64_t valid, int shape)
+{
+    const uint64_t vx = valid > 0 ? sec_xb_end((uint32_t)valid) : 0;
+    const int W = xb_width(shape);
+    auto &bin = bins[{2, shape, W, 256, 0}];
+    for (uint64_t t0 = 0; t0 < vx; t0 += (uint64_t)sec::kLanes * 4 * W)
+        bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
+    return vx;
 }
 
 // XCD order.  Workgroup b of a launch is dispatched to XCD b % 8, so with the tiles in chunk
@@ -744,7 +776,10 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
             if (p > 0) {
-                const uint64_t start = mt != mtab_of.end() ? add_mfma_work(bins, (uint32_t)(i - c0), valid, c.k, c.m) : 0;
+                const int xs = mt == mtab_of.end() ? xb_shape(c.k, c.m) : -1;
+                const uint64_t start = mt != mtab_of.end() ? add_mfma_work(bins, (uint32_t)(i - c0), valid, c.k, c.m)
+                                       : xs >= 0             ? add_xb_work(bins, (uint32_t)(i - c0), valid, xs)
+                                                             : 0;
                 add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, start, narrow);
             }
         }
@@ -773,11 +808,14 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
     for (const Group &g : sp.groups) {
-        int e = g.mfma ? sec_launch_encode_mfma(g.U, g.rows, in, par, dd, dt + g.first, g.count,
-                                                plan.meta.as<uint8_t>(sp.off_mtab), s)
-                       : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
+        int e = g.mfma == 1 ? sec_launch_encode_mfma(g.U, g.rows, in, par, dd, dt + g.first, g.count,
+                                                     plan.meta.as<uint8_t>(sp.off_mtab), s)
+                : g.mfma == 2 ? sec_launch_encode_xb(g.rows, g.U, in, par, dd, dt + g.first, g.count, s)
+                              : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
         if (e)
-            return hip_fail((hipError_t)e, g.mfma ? "sec_encode_mfma_kernel" : "sec_encode_kernel");
+            return hip_fail((hipError_t)e, g.mfma == 1   ? "sec_encode_mfma_kernel"
+                                           : g.mfma == 2 ? "sec_encode_xb_kernel"
+                                                         : "sec_encode_kernel");
     }
     if (sp.ntail) {
         int e = sec_launch_encode_tail(in, par, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs, s);

@@ -115,6 +115,13 @@ int sec_launch_encode(int rows, int U, int wide, int lanes, const uint8_t *in, u
 // k = 32 * G (G = 1, 2), `tiles` 32-row accumulator tiles per row group (G = 1: 1..4, G = 2: 1..2)
 int sec_launch_encode_mfma(int G, int tiles, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
                            const sec::Tile *t, uint32_t ntiles, const void *mtabs, void *stream);
+// Compile-time-matrix encode (kernels_xb.hip) for the shapes sec_xb_shape knows (else -1):
+// positions [0, sec_xb_end(valid)) of each chunk, all parity rows per tile, W = 1 or 2 dwords
+// per lane, 256-lane tiles of 1024 * W positions
+int sec_xb_shape(int k, int m);
+uint32_t sec_xb_end(uint32_t valid);
+int sec_launch_encode_xb(int shape, int W, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
+                         const sec::Tile *t, uint32_t ntiles, void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
                            uint32_t nitems, const uint32_t *tabs, void *stream);
 int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,

@@ -552,3 +552,30 @@ def test_largest_block_size(engine):
     d2, _ = _enc_descs(1, 2 * (1 << 31), k, m)
     with pytest.raises(Error):
         engine.encode_batch(d2, 1, 1)  # rejected before any address is touched
+
+
+@pytest.mark.parametrize("xb_w", ["1", "2", "off"])
+def test_encode_compile_time_matrix_shapes(xb_w, monkeypatch):
+    """(64,96) and (32,48) encode through kernels_xb.hip (compile-time zfec matrix, SEC_XB_W
+    dwords per lane) for [0, valid rounded down to 16) and sec_encode_kernel for the rest,
+    against the oracle: ragged tails, padded last blocks, chunks too small for any XB tile,
+    unaligned B, mixed with other shapes in one batch; "off" (SEC_XB=0) is the v_perm path."""
+    from storb_amd.engine import Engine
+
+    if xb_w == "off":
+        monkeypatch.setenv("SEC_XB", "0")
+    else:
+        monkeypatch.setenv("SEC_XB_W", xb_w)
+    eng = Engine(0)  # its own plan cache: the knobs are read when a plan is built
+    rng = random.Random(96)
+    chunks, km = [], []
+    for k, m in [(64, 96), (32, 48), (16, 24), (64, 96), (32, 48)]:
+        for n in [k * k, 16 * k, 16 * k * 64 + 5, 4096 * k + 1, 65536 * k - 3, (1 << 20) + 17, rng.randrange(k * k, 900000)]:
+            if -(-n // k) * (k - 1) > n:
+                continue
+            chunks.append(rng.randbytes(n))
+            km.append((k, m))
+    par = eng.encode_host(chunks, km)
+    for c, (k, m), p in zip(chunks, km, par):
+        assert p == oracle_parity(c, k, m), (xb_w, k, m, len(c))
+    eng.close()

@@ -1,0 +1,2 @@
+set -o pipefail
+bash tools/gpu_tests.sh tests/test_gpu_parity.py && VARIANTS=base,base@SEC_XB_W=2,base@SEC_XB=0 WORKLOADS="1024,1048576,32,48 256,1048576,64,96 16,16777216,64,96 64,16777216,32,48" bash tools/gpu_ab.sh
