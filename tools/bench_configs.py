@@ -7,6 +7,8 @@ JSON object.  Complements bench.py (which is the C2+C3 headline line).
 C1  see tools/c1_loopback.py.
 C2/C3  1024 x 1 MiB RS(4,2) encode / decode ({1,3} erased), device-resident; C3 also over
     the erasure sets of SURVEY 8(d) (c3_patterns), reassemble and recover-only.
+Policy shapes for 1 GiB / 16 GiB / 1 TiB files: zfec(16,24), (32,48), (64,96) on 8 / 32 / 256
+    MiB chunks, 1 GiB per case.
 C4  8192 x 64 KiB RS(10,4) (one GPU's share of 65536), device-resident encode / decode with
     data blocks {0,2,5,7} erased (block 9, zfec's padded one, read in place: avail = B - padlen).
 C5  mixed chunk sizes log-uniform in [4 KiB, 4 MiB] (seed 5) up to ~1 GiB, RS(8,3):
@@ -245,6 +247,11 @@ def main():
 
     res["c2_c3_1024x1MiB_rs(4,2)"] = device_case(eng, [1 << 20] * 1024, 4, 6, (1, 3))
     res["c3_erasure_patterns_1024x1MiB_rs(4,2)"] = c3_patterns(eng)
+    # the policy's shapes for large files at their own chunk sizes, 1 GiB each,
+    # half as many data blocks lost as there are parity blocks
+    for chunk, k, m in ((8 << 20, 16, 24), (32 << 20, 32, 48), (256 << 20, 64, 96)):
+        res[f"policy_{chunk >> 20}MiB_chunks_zfec({k},{m})"] = device_case(
+            eng, [chunk] * ((1 << 30) // chunk), k, m, tuple(range(0, m - k, 2)), reps=10)
     res["c4_8192x64KiB_rs(10,4)_per_gpu"] = device_case(eng, [65536] * 8192, 10, 14, (0, 2, 5, 7))
     sizes = c5_sizes()
     res["c5_mixed_4KiB-4MiB_rs(8,3)_device"] = device_case(eng, sizes, 8, 11, (1, 3, 5))
