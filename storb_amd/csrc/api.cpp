@@ -1141,6 +1141,9 @@ template <class Launch>
 int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint8_t *out, size_t out_per,
               unsigned flags, size_t slab, int kind, const char *what, uint64_t seg_bytes, Launch launch_kernel)
 {
+    // SHA-1 launches through kernels.hip, whose dispatches carry the timing events; the bignum
+    // kernels (kind 3) are launched plainly, so their timing takes event records around them
+    const bool attached = kind != 3;
     if (!ctx || nmsgs < 0 || (nmsgs > 0 && (!msgs || !out)) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC)) ||
         nmsgs >= (int64_t)UINT32_MAX)
         return SEC_EINVAL;
@@ -1214,7 +1217,7 @@ int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint
     if (!host) {
         const SubPlan &sp = plan.subs[0];
         hipEvent_t t0;
-        RC(timing_begin(ctx, &t0, ctx->stream()));
+        RC(timing_begin(ctx, &t0, ctx->stream(), attached));
         int e = launch_kernel((const uint8_t *)nullptr, plan, sp, (size_t)0, out, ctx->stream());
         if (e)
             return hip_fail((hipError_t)e, what);
@@ -1236,7 +1239,7 @@ int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint
     };
     auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
         hipEvent_t t0;
-        RC(timing_begin(ctx, &t0, s));
+        RC(timing_begin(ctx, &t0, s, attached));
         int e = launch_kernel(din, plan, sp, (size_t)(&sp - plan.subs.data()), dout, s);
         if (e)
             return hip_fail((hipError_t)e, what);

@@ -246,3 +246,24 @@ def test_serialised_round_trip_verifies(fresh):
     ch = apdp.Challenge.model_validate_json(fresh.issue_challenge(tag.model_dump_json()).model_dump_json())
     pr = apdp.Proof.model_validate_json(fresh.generate_proof(data, ch.tag, ch).model_dump_json())
     assert fresh.verify_proof(pr, ch, tag)
+
+
+def test_kernel_timing_covers_reduce_batches(mk, engine):
+    """Kernel timing (Engine.set_timing / collect_timing("bignum")) measures the message-batch
+    bignum launches (segment reduce + sum), which launch outside kernels.hip's event-carrying
+    dispatch: 64 pieces of 256 KiB take well over 20 us of kernel time, not ~0."""
+    rng = np.random.default_rng(9)
+    buf = torch.from_numpy(rng.integers(0, 256, 64 << 18, dtype=np.uint8)).cuda()
+    msgs = np.zeros(64, dtype=MSG_DTYPE)
+    for i in range(64):
+        msgs[i] = (buf.data_ptr() + i * (1 << 18), 1 << 18, 1 << 18)
+    out = torch.empty(64 * 256, dtype=torch.uint8, device="cuda")
+    mk.reduce_batch(msgs, out)  # warm (R^(32j) table growth)
+    engine.sync()
+    engine.collect_timing("bignum")
+    engine.set_timing(True)
+    mk.reduce_batch(msgs, out)
+    engine.sync()
+    engine.set_timing(False)
+    ms, n = engine.collect_timing("bignum")
+    assert n >= 1 and ms > 0.02, (ms, n)

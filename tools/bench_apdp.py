@@ -146,18 +146,29 @@ def main():
     cs.key.prf_key = prf_key
     K = min(P, 1024)
     datas = [os.urandom(L) for _ in range(K)]
+    # the first call of a key also derives it on the device (Montgomery constants, CRT halves,
+    # g's 16 MiB fixed-base table); a validator pays that once per key, so the steady state is
+    # timed separately (second call, same key)
+    t = time.perf_counter()
+    tags = cs.generate_tags(datas)
+    t_first = time.perf_counter() - t
     t = time.perf_counter()
     tags = cs.generate_tags(datas)
     t_tag = time.perf_counter() - t
-    chs = cs.issue_challenges(tags)
     t = time.perf_counter()
-    proofs = cs.generate_proofs(list(zip(datas, tags, chs)))
+    chs = cs.issue_challenges(tags)
+    t_ch = time.perf_counter() - t
+    pr_items = list(zip(datas, tags, chs))
+    cs.generate_proofs(pr_items[:8])  # the challenge moduli's keys are derived per call thread
+    t = time.perf_counter()
+    proofs = cs.generate_proofs(pr_items)
     t_pr = time.perf_counter() - t
     t = time.perf_counter()
     ok = cs.verify_proofs(list(zip(proofs, chs, tags)))
     t_ver = time.perf_counter() - t
     assert all(ok)
-    res["api_host"] = {"items": K, "generate_tags_per_s": round(K / t_tag, 1),
+    res["api_host"] = {"items": K, "piece_bytes": L, "generate_tags_first_call_per_s": round(K / t_first, 1),
+                       "generate_tags_per_s": round(K / t_tag, 1), "issue_challenges_per_s": round(K / t_ch, 1),
                        "generate_proofs_per_s": round(K / t_pr, 1), "verify_proofs_per_s": round(K / t_ver, 1)}
     print(json.dumps(res, indent=1))
 
