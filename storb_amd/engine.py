@@ -228,10 +228,12 @@ class Engine:
         mv = memoryview(out)
         return [bytes(mv[20 * i:20 * (i + 1)]) for i in range(len(datas))]
 
-    def encode_host_raw(self, chunks, shapes):
+    def encode_host_raw(self, chunks, shapes, digests: bool = False):
         """``encode_host`` without the per-block ``bytes``: returns (buf, layout) where buf is
         this engine's pinned result scratch and layout[i] = (offset, B, m - k) of chunk i's
-        parity blocks in it, back to back.  buf is reused by the engine's next call."""
+        parity blocks in it, back to back.  buf is reused by the engine's next call.  With
+        ``digests=True``: (buf, layout, dig), dig = the SHA-1 of every chunk's m blocks in order,
+        20 bytes each (GPU-computed after the encode, sec_encode_digest_batch)."""
         n = len(chunks)
         descs = np.zeros(n, dtype=ENC_DTYPE)
         keep = []
@@ -246,6 +248,11 @@ class Engine:
             layout.append((total, B, m - k))
             total += (m - k) * B
         out = self._out_buffer(total)
+        if digests:
+            dig = np.empty(max(20 * sum(m for (_, m) in shapes), 1), dtype=np.uint8)
+            if n:
+                self.encode_digest_batch(descs, 0, out, dig, host=True)
+            return out, layout, dig
         if n:
             self.encode_batch(descs, 0, out, host=True)
         return out, layout

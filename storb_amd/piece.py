@@ -68,6 +68,14 @@ PREFETCH_MIN_CHUNK = 512 << 10
 # 4 MiB object fell from 1236-1289 to 811 MiB/s per chunk, 1327-1469 to 868 streamed).
 PARALLEL_COPY_MIN = 256 << 10
 STREAM_WINDOW_BYTES = 64 << 20  # chunk bytes per GPU call in the *_stream pipelines
+# encode_chunks_stream(piece_ids=True) over windows whose pieces are all >= PARALLEL_COPY_MIN:
+# the ids come from the GPU SHA-1 kernel, fused after the window's encode, instead of hashlib
+# on the thread pool, in windows of STREAM_WINDOW_IDS_BYTES (when window_bytes is not given).
+# The kernel is one lane per piece, so a window's hashing takes about one piece's chain
+# whatever the window size: 1 GiB object, 8 MiB chunks, zfec(16,24): 7.1 / 9.1 GiB/s with
+# 256 / 512 MiB windows against 3.2-5.3 hashing on the host (profiles/r02_stream_rate.json).
+GPU_PIECE_IDS = True
+STREAM_WINDOW_IDS_BYTES = 256 << 20
 
 
 class PieceType(IntEnum):  # piece.py:21-23
@@ -221,10 +229,11 @@ def _fill(dst: np.ndarray, src: np.ndarray) -> None:
         dst[len(src):] = 0
 
 
-def _pieces_parallel(chunks: list, shapes: list) -> list[list[bytes]]:
+def _pieces_parallel(chunks: list, shapes: list, digests: bool = False):
     """Every chunk's m pieces as bytes (k zero-padded data slices, then the parity): one GPU
     call for all chunks; the piece copies run on the hash pool, the data slices beside the GPU
-    call.  Returns once every piece is filled."""
+    call.  Returns once every piece is filled.  ``digests=True``: (pieces, ids), ids[i] = the
+    piece ids (SHA-1 hex) of chunk i's m pieces, hashed on the GPU after the encode."""
     hp = _pool("hash")
     out, jobs = [], []
     for c, (k, m, B, _) in zip(chunks, shapes):
@@ -237,15 +246,22 @@ def _pieces_parallel(chunks: list, shapes: list) -> list[list[bytes]]:
             ps.append(b)
             jobs.append(hp.submit(_fill, v, src[j * B:min((j + 1) * B, len(src))]))
         out.append(ps)
-    buf, layout = get_engine().encode_host_raw(list(chunks), [(k, m) for (k, m, _, _) in shapes])
+    res = get_engine().encode_host_raw(list(chunks), [(k, m) for (k, m, _, _) in shapes], digests=digests)
+    buf, layout = res[0], res[1]
     for ps, (o, B, p) in zip(out, layout):
         for r in range(p):
             b, v = _new_bytes(B)
             ps.append(b)
             jobs.append(hp.submit(_fill, v, buf[o + r * B:o + (r + 1) * B]))
+    ids = None
+    if digests:
+        hx, ids, f = res[2].tobytes().hex(), [], 0
+        for (_, m, _, _) in shapes:
+            ids.append([hx[40 * (f + j):40 * (f + j + 1)] for j in range(m)])
+            f += m
     for f in jobs:  # the pieces must be complete before anyone sees them (and buf is reused)
         f.result()
-    return out
+    return (out, ids) if digests else out
 
 
 def _build(chunk_idx: int, k: int, m: int, B: int, padlen: int, n: int, blocks: list[bytes]) -> EncodedChunk:
@@ -458,6 +474,11 @@ def _encode_window(window: list, first_idx: int, piece_ids: bool):
             piece_length(len(c))
             shapes.append(chunk_shape(len(c)))
         hp = _pool("hash")
+        if GPU_PIECE_IDS and min(B for (_, _, B, _) in shapes) >= PARALLEL_COPY_MIN:
+            pieces, ids = _pieces_parallel(window, shapes, digests=True)
+            out = [_build(first_idx + i, k, m, B, padlen, len(c), ps)
+                   for i, (c, (k, m, B, padlen), ps) in enumerate(zip(window, shapes, pieces))]
+            return list(zip(out, ids)), None
         if min(B for (_, _, B, _) in shapes) >= PARALLEL_COPY_MIN:
             pieces = _pieces_parallel(window, shapes)
             futs = [[hp.submit(_sha1_hex, b) for b in ps] for ps in pieces]
@@ -484,8 +505,12 @@ def encode_chunks_stream(chunks: Iterable[bytes], first_chunk_idx: int = 0, *, p
     `window_bytes` (default STREAM_WINDOW_BYTES); each window is one batched GPU encode on a
     worker thread, running while the caller consumes the previous window's results.  Yields
     ``EncodedChunk`` per chunk in order (chunk i gets index first_chunk_idx + i), or with
-    ``piece_ids=True`` ``(EncodedChunk, [piece_hash of each of its m pieces])``."""
-    wb = STREAM_WINDOW_BYTES if window_bytes is None else window_bytes
+    ``piece_ids=True`` ``(EncodedChunk, [piece_hash of each of its m pieces])``; those ids
+    come from the GPU (GPU_PIECE_IDS) for windows of large pieces, whose default window is then
+    STREAM_WINDOW_IDS_BYTES."""
+    wb = window_bytes
+    if wb is None:
+        wb = STREAM_WINDOW_IDS_BYTES if piece_ids and GPU_PIECE_IDS else STREAM_WINDOW_BYTES
     pool = _pool("stream")
     idx = first_chunk_idx
     pending = None

@@ -142,3 +142,22 @@ def test_reassemble_kernel_pure_copy_through_abi(engine):
         out = np.zeros(n, np.uint8)
         engine.decode_batch(d, np.array(order, np.int32), offs, buf, out, host=True)
         assert out.tobytes() == data, (k, m, n)
+
+
+@pytest.mark.parametrize("gpu_ids", [True, False])
+def test_encode_stream_piece_ids_large_pieces(gpu_ids, monkeypatch):
+    """Upload stream with piece ids over chunks whose pieces are all >= PARALLEL_COPY_MIN (the
+    GPU SHA-1 path when GPU_PIECE_IDS, hashlib on the pool otherwise): ragged chunk sizes,
+    several windows, the last chunk short; pieces against the oracle and ids against hashlib."""
+    monkeypatch.setattr(piece, "GPU_PIECE_IDS", gpu_ids)
+    rng = random.Random(31)
+    # >= 2.5 MiB: 512 KiB pieces (piece_length), so every block is >= 256 KiB even when ragged
+    objs = [rng.randbytes(rng.randrange(5 << 19, 6 << 20)) for _ in range(9)] + [rng.randbytes(3 << 20)]
+    got = list(piece.encode_chunks_stream(iter(objs), 7, piece_ids=True, window_bytes=12 << 20))
+    assert len(got) == len(objs)
+    for i, ((ec, ids), o) in enumerate(zip(got, objs)):
+        assert ec.chunk_idx == 7 + i
+        blocks = cfec.easy_encode(o, ec.k, ec.m)
+        assert min(len(b) for b in blocks) >= piece.PARALLEL_COPY_MIN
+        assert [p.data for p in ec.pieces] == blocks
+        assert ids == [hashlib.sha1(b).hexdigest() for b in blocks]

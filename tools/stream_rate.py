@@ -7,7 +7,10 @@
 Object: --mib MiB of random bytes; the policy gives its chunk size (1 GiB -> 8 MiB chunks,
 zfec(16,24)).  Rates are object bytes / wall time (GiB/s), best of --reps:
   upload_per_chunk       encode_chunk per chunk + piece_hash per piece (validator.py:1380,1081)
-  upload_stream          encode_chunks_stream(piece_ids=True)
+  upload_stream          encode_chunks_stream(piece_ids=True), defaults (GPU piece ids for
+                         large pieces, STREAM_WINDOW_IDS_BYTES windows)
+  --gpu-ids: also per-window encode_chunks_with_ids, and the stream with GPU / host ids at
+             64..512 MiB windows
   download_per_chunk     decode_chunk per chunk (the reference's reconstruct_data_stream body)
   download_stream        reconstruct_data_stream, consumed chunk by chunk
 each download both with every data piece present (joined, no GPU work) and with data piece 0
@@ -42,6 +45,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--gpu-ids", action="store_true", help="also: piece ids from the GPU SHA-1, per window")
     a = ap.parse_args()
     from storb_amd import piece
 
@@ -61,9 +65,39 @@ def main():
     def up_stream():
         return list(piece.encode_chunks_stream(iter(parts), piece_ids=True))
 
+    def up_gpu_ids(window_mib):  # piece ids hashed on the GPU (fused after encode), one call per window
+        def run():
+            out, i = [], 0
+            per = max(1, (window_mib << 20) // cs)
+            for w in range(0, len(parts), per):
+                ecs, ids = piece.encode_chunks_with_ids(parts[w:w + per], w)
+                out.extend(zip(ecs, ids))
+            return out
+        return run
+
     enc = up_stream()
     res["upload_per_chunk"] = round(len(data) / best(up_per_chunk, a.reps) / GIB, 3)
     res["upload_stream"] = round(len(data) / best(up_stream, a.reps) / GIB, 3)
+    if a.gpu_ids:
+        ref = [ids for _, ids in enc]
+        for wm in (64, 256, 1024):
+            got = up_gpu_ids(wm)()
+            assert [ids for _, ids in got] == ref
+            res[f"upload_gpu_ids_window_{wm}MiB"] = round(len(data) / best(up_gpu_ids(wm), a.reps) / GIB, 3)
+        for wm in (64, 128, 256, 512):
+            for mode in (True, False):  # ids from the GPU SHA-1 / from hashlib on the pool
+                def up(wm=wm, mode=mode):
+                    old = piece.GPU_PIECE_IDS
+                    piece.GPU_PIECE_IDS = mode
+                    try:
+                        return list(piece.encode_chunks_stream(iter(parts), piece_ids=True, window_bytes=wm << 20))
+                    finally:
+                        piece.GPU_PIECE_IDS = old
+                got = up()
+                assert [ids for _, ids in got] == ref
+                assert [[p.data for p in ec.pieces] for ec, _ in got] == [[p.data for p in ec.pieces] for ec, _ in enc]
+                res[f"upload_stream_{'gpu' if mode else 'host'}_ids_window_{wm}MiB"] = round(
+                    len(data) / best(up, a.reps) / GIB, 3)
     chunks = [ec.model_copy(update={"pieces": None}) for ec, _ in enc]
     for label, drop in (("all_data_present", ()), ("data_piece_0_lost", (0,))):
         pieces = [p for ec, _ in enc for p in ec.pieces if p.piece_idx not in drop]
