@@ -143,6 +143,7 @@ struct SubPlan {
     uint64_t in_bytes = 0, out_bytes = 0;  // dense slab sizes (host mode)
     size_t off_msgs = 0;                   // messages of this unit (SHA-1, bignum)
     uint32_t nmsgs = 0;
+    bool sha_split = false;  // SHA-1 messages: the two-wave kernel (sha1_split)
     size_t off_segs = 0, off_seginfo = 0;  // bignum: segments of the messages, per-message (first, count)
     uint32_t nsegs = 0, max_seg = 0;       // segment count; most segments of one message
     uint64_t dig_first = 0;                // first digest slot of this unit
@@ -647,6 +648,24 @@ int timing_end(sec_ctx *ctx, hipEvent_t a, int kind, hipStream_t s)
     return SEC_OK;
 }
 
+// SHA-1 kernel for a launch's messages: sec_sha1_split_kernel (message schedule on a second
+// wave) when the messages are few and long, so the round chains are the bound; else one lane
+// per message.  SEC_SHA1_SPLIT = 0 / 1 forces it (read per plan build).
+bool sha1_split(const std::vector<sec::MsgDesc> &md)
+{
+    const char *e = getenv("SEC_SHA1_SPLIT");
+    if (e && (e[0] == '0' || e[0] == '1'))
+        return e[0] == '1';
+    if (md.empty())
+        return false;
+    uint64_t blocks = 0;
+    for (const sec::MsgDesc &m : md)
+        blocks += m.len / 64;
+    // measured (profiles/r02_sha1_split_ab.jsonl): faster up to 16384 messages of 64 KiB (256
+    // one-lane waves), slower at 65536 x 16 KiB and C4's 114688 x 6554 B
+    return md.size() <= ((size_t)16 << 10) && blocks / md.size() >= 256;  // >= 16 KiB on average
+}
+
 int check_sharenums(int k, int m, const int32_t *s)
 {
     bool seen[256] = {false};
@@ -787,6 +806,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
         flatten(bins, sp.groups, tiles, false);
         sp.ntail = (uint32_t)tail.size();
         sp.nmsgs = (uint32_t)msgs.size();
+        sp.sha_split = sha1_split(msgs);
         sp.dig_off = sp.out_bytes;  // host mode: digests follow the slab's parity
         if (host)
             sp.out_bytes += (uint64_t)msgs.size() * 20;
@@ -823,7 +843,7 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
             return hip_fail((hipError_t)e, "sec_encode_tail");
     }
     if (sp.nmsgs) {
-        int e = sec_launch_sha1(in, par, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, digests, s);
+        int e = sec_launch_sha1(in, par, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, digests, s, sp.sha_split);
         if (e)
             return hip_fail((hipError_t)e, "sec_sha1_kernel");
     }
@@ -1191,6 +1211,7 @@ int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint
                 sp.in_bytes += av;
             }
             sp.nmsgs = (uint32_t)md.size();
+            sp.sha_split = sha1_split(md);
             sp.out_bytes = (uint64_t)md.size() * out_per;
             sp.off_msgs = img.put(md.data(), md.size() * sizeof(sec::MsgDesc));
             if (seg_bytes) {
@@ -1801,7 +1822,7 @@ int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *di
                      env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 2, "sec_sha1_kernel", 0,
                      [](const uint8_t *base0, const Plan &plan, const SubPlan &sp, size_t, uint8_t *o, hipStream_t s) {
                          return sec_launch_sha1(base0, nullptr, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, o,
-                                                s);
+                                                s, sp.sha_split);
                      });
 }
 

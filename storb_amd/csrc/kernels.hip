@@ -884,6 +884,187 @@ __global__ __launch_bounds__(64) void sec_sha1_kernel(const u8 *__restrict__ bas
         out[q] = __builtin_bswap32(h[q]);
 }
 
+// SHA-1 with the message schedule on a second wave (few, long messages: the latency-bound
+// regime, e.g. C2's 6144 pieces of 256 KiB are 96 waves, one per SIMD at most).  A workgroup is
+// two waves for the same 64 messages: wave 1 loads each block (prefetched), byte-swaps it and
+// expands the 80 schedule words W_t + K_t into LDS; wave 0 runs only the 80 rounds from LDS
+// (rotl 5, f, add3, add, rotl 30: 5 VALU per round, 405 per block against 597 with the
+// schedule inline), one block behind, the two buffers handed over by one s_barrier per block.
+// Blocks past a message's real bytes (zfec's zero padding) and the final padded block(s) go
+// through sha1_compress on wave 0 afterwards, as in sec_sha1_kernel.
+constexpr u32 kShaK[4] = {0x5A827999u, 0x6ED9EBA1u, 0x8F1BBCDCu, 0xCA62C1D6u};
+
+__device__ __forceinline__ void sha1_rounds_wk(u32 (&h)[5], const u32x4 (&vs)[20])
+{
+    u32 a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+    for (int q = 0; q < 20; ++q) {
+        const u32x4 v = vs[q];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = 4 * q + j;
+            const u32 f = t < 20 ? bfi(b, c, d) : t < 40 ? xor3(b, c, d) : t < 60 ? maj(b, c, d) : xor3(b, c, d);
+            const u32 tmp = rotl(a, 5) + f + e + v[j];
+            e = d;
+            d = c;
+            c = rotl(b, 30);
+            b = a;
+            a = tmp;
+        }
+    }
+    h[0] += a;
+    h[1] += b;
+    h[2] += c;
+    h[3] += d;
+    h[4] += e;
+}
+
+// one block's 80 words from LDS into registers (left to the scheduler, the reads went out two
+// at a time, each pair waited for a few rounds later: 1.06x over the one-lane kernel, not 1.26x)
+__device__ __forceinline__ void sha1_fetch_wk(u32x4 (&vs)[20], const u32x4 *__restrict__ wk, u32 lane)
+{
+#pragma unroll
+    for (int q = 0; q < 20; ++q)
+        vs[q] = wk[q * 64 + lane];
+}
+
+// W_t + K_t of one block (16 big-endian words in w) into wk[t / 4][lane][t % 4]
+__device__ __forceinline__ void sha1_schedule_wk(u32 (&w)[16], u32x4 *__restrict__ wk, u32 lane)
+{
+#pragma unroll
+    for (int q = 0; q < 20; ++q) {
+        u32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = 4 * q + j;
+            u32 wt;
+            if (t < 16) {
+                wt = w[t];
+            } else {
+                wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
+                w[t & 15] = wt;
+            }
+            v[j] = wt + kShaK[t / 20];
+        }
+        wk[q * 64 + lane] = v;
+    }
+}
+
+__global__ __launch_bounds__(128) void sec_sha1_split_kernel(const u8 *__restrict__ base0, const u8 *__restrict__ base1,
+                                                              const sec::MsgDesc *__restrict__ msgs, u32 nmsgs,
+                                                              u8 *__restrict__ digests)
+{
+    __shared__ u32x4 s_wk[2][20 * 64];  // two blocks' W + K, [t / 4][lane]
+    const u32 lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const u32 i = blockIdx.x * 64 + lane;
+    const bool live = i < nmsgs;
+    sec::MsgDesc m{};
+    if (live)
+        m = msgs[i];
+    const u8 *p = (m.base ? base1 : base0) + m.off;
+    const uint64_t nfast = live ? min(m.len / 64, m.avail / 64) : 0;  // blocks wholly inside the real bytes
+    // the workgroup walks the longest message's blocks (shorter ones idle, masked)
+    uint64_t nmax = nfast;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+        nmax = max(nmax, (uint64_t)__shfl_xor((unsigned long long)nmax, o, 64));
+    u32 h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+    // Two LDS buffers, one barrier per block: before barrier j wave 1 has written block j into
+    // buffer j & 1, and wave 0 has finished block j - 1 (buffer (j - 1) & 1, which wave 1 fills
+    // next).  (Three buffers with block j + 1 read into registers during block j measured
+    // 1.22-1.25x over the one-lane kernel against 1.23-1.26x for this form.)
+    if (wave == 1) {  // the schedule, one block ahead of wave 0; loads two blocks ahead of that
+        u32x4 nx[2][4];
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+            if ((uint64_t)d < nfast) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    nx[d][q] = *reinterpret_cast<const u32x4_u *>(p + d * 64 + 16 * q);
+            }
+        for (uint64_t b0 = 0; b0 < nmax; b0 += 2) {
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+                const uint64_t blk = b0 + d;
+                if (blk >= nmax)
+                    break;
+                if (blk < nfast) {
+                    u32 w[16];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        w[4 * q + 0] = __builtin_bswap32(nx[d][q].x);
+                        w[4 * q + 1] = __builtin_bswap32(nx[d][q].y);
+                        w[4 * q + 2] = __builtin_bswap32(nx[d][q].z);
+                        w[4 * q + 3] = __builtin_bswap32(nx[d][q].w);
+                    }
+                    if (blk + 2 < nfast) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            nx[d][q] = *reinterpret_cast<const u32x4_u *>(p + (blk + 2) * 64 + 16 * q);
+                    }
+                    sha1_schedule_wk(w, s_wk[d], lane);
+                }
+                __syncthreads();  // barrier blk
+            }
+        }
+        __syncthreads();  // barrier nmax, wave 0's last (both waves take nmax + 1 barriers)
+        return;
+    }
+    __syncthreads();  // barrier 0: block 0 is in buffer 0
+    for (uint64_t blk = 0; blk < nmax; ++blk) {
+        if (blk < nfast) {
+            u32x4 v[20];
+            sha1_fetch_wk(v, s_wk[blk & 1], lane);
+            __builtin_amdgcn_sched_barrier(0);  // all 20 reads out before the first round
+            sha1_rounds_wk(h, v);
+        }
+        __syncthreads();  // barrier blk + 1: block blk + 1 is in its buffer, buffer blk & 1 free
+    }
+    if (!live)
+        return;
+    u32 w[16];
+    const uint64_t nfull = m.len / 64;
+    for (uint64_t blk = nfast; blk < nfull; ++blk) {
+        const uint64_t o = blk * 64;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            u32 x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                x = (x << 8) | msg_byte(p, o + 4 * q + b, m.avail);
+            w[q] = x;
+        }
+        sha1_compress(h, w);
+    }
+    const uint64_t o = nfull * 64;
+    const u32 rem = (u32)(m.len - o);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        u32 x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const u32 pos = 4 * q + b;
+            const u32 byte = pos < rem ? msg_byte(p, o + pos, m.avail) : (pos == rem ? 0x80u : 0u);
+            x = (x << 8) | byte;
+        }
+        w[q] = x;
+    }
+    const uint64_t bits = m.len * 8;
+    if (rem >= 56) {
+        sha1_compress(h, w);
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            w[q] = 0;
+    }
+    w[14] = (u32)(bits >> 32);
+    w[15] = (u32)bits;
+    sha1_compress(h, w);
+    u32 *out = reinterpret_cast<u32 *>(digests + (uint64_t)i * 20);
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+        out[q] = __builtin_bswap32(h[q]);
+}
+
 // Timing events for the next launch (sec_launch_events): the kernel's own dispatch records
 // them (hipExtLaunchKernelGGL), so timing adds no marker packets between kernels.  Two event
 // records per launch around back-to-back kernels cost the bench 3-5 % of its rate.
@@ -1033,10 +1214,13 @@ int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *block
 }
 
 int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDesc *msgs, uint32_t nmsgs,
-                    uint8_t *digests, void *stream)
+                    uint8_t *digests, void *stream, int split)
 {
     if (nmsgs == 0)
         return hipSuccess;
+    if (split)
+        return launch(sec_sha1_split_kernel, dim3((nmsgs + 63) / 64), dim3(128), (hipStream_t)stream, base0, base1,
+                      msgs, nmsgs, digests);
     if (SEC_SHA1_PF)
         return launch(sec_sha1_kernel<true>, dim3((nmsgs + 63) / 64), dim3(64), (hipStream_t)stream, base0, base1, msgs,
                       nmsgs, digests);

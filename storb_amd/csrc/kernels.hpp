@@ -127,8 +127,10 @@ int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *
 int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,
                       const sec::DecDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
                       sec::DecSlots slots, void *stream);
+// split: sec_sha1_split_kernel (two waves per 64 messages: schedule and rounds) instead of
+// one lane per message
 int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDesc *msgs, uint32_t nmsgs,
-                    uint8_t *digests, void *stream);
+                    uint8_t *digests, void *stream, int split = 0);
 int sec_launch_decode_tail(const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
                            const sec::TailItem *items, uint32_t nitems, const uint32_t *tabs, sec::DecSlots slots,
                            void *stream);

@@ -104,3 +104,40 @@ def test_piece_api_ids():
     assert ids == [[piece_hash(p.data) for p in e.pieces] for e in enc]
     datas = [p.data for e in enc for p in e.pieces]
     assert piece_hashes(datas) == [piece_hash(x) for x in datas]
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_sha1_split_kernel_forced(split, monkeypatch):
+    """The two-wave SHA-1 kernel (schedule wave + rounds wave, kernels.hip
+    sec_sha1_split_kernel), forced on (SEC_SHA1_SPLIT=1) and off, on messages of every length
+    class: empty, sub-block, exact blocks, long, zero tails past avail, ragged workgroups (more
+    and fewer than 64 messages, very unequal lengths in one workgroup), device buffers and the
+    host path, and fused after an encode; against hashlib."""
+    from storb_amd.engine import Engine
+
+    monkeypatch.setenv("SEC_SHA1_SPLIT", split)
+    eng = Engine(0)  # its own plan cache: the choice is made when a plan is built
+    rng = np.random.default_rng(11)
+    buf = torch.from_numpy(rng.integers(0, 256, 1 << 22, dtype=np.uint8)).cuda()
+    host = buf.cpu().numpy().tobytes()
+    for nm in (1, 63, 64, 65, 200):
+        msgs = np.zeros(nm, dtype=MSG_DTYPE)
+        expect = []
+        for i in range(nm):
+            ln = int(rng.choice([0, 1, 55, 64, 65, 4096, int(rng.integers(0, 300000)), 1 << 20]))
+            off = int(rng.integers(0, (1 << 22) - ln + 1))
+            av = int(rng.integers(0, ln + 1)) if i % 3 == 1 else ln
+            msgs[i] = (buf.data_ptr() + off, ln, av)
+            expect.append(hashlib.sha1(host[off:off + av] + b"\0" * (ln - av)).digest())
+        dig = torch.empty(nm * 20, dtype=torch.uint8, device="cuda")
+        eng.sha1_batch(msgs, dig)
+        got = dig.cpu().numpy().tobytes()
+        assert [got[20 * i:20 * i + 20] for i in range(nm)] == expect, nm
+    datas = [random.Random(5).randbytes(n) for n in (0, 70, 65536, 300001, 1 << 20, 123457)]
+    assert eng.sha1_host(datas) == [hashlib.sha1(d).digest() for d in datas]
+    chunks = [random.Random(6).randbytes(n) for n in (1 << 20, (4 << 20) + 3, 700001)]
+    par, digs = eng.encode_host(chunks, [(4, 6)] * 3, digests=True)
+    for c, p, ds in zip(chunks, par, digs):
+        blocks = cfec.easy_encode(c, 4, 6)
+        assert ds == [hashlib.sha1(b).digest() for b in blocks]
+    eng.close()
