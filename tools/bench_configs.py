@@ -215,7 +215,7 @@ def sha1_case(eng, nch=1024, n=1 << 20, k=4, m=6, reps=5):
             "sha1_GBs": round(hashed / t_sha / 1e9, 1), "encode_ms": round(t_enc * 1e3, 3),
             "encode_plus_sha1_fused_ms": round(t_both * 1e3, 3),
             "e2e_host_encode_plus_sha1_gibs": round(nch * n / t_host / GIB, 2),
-            "note": "wall time per call incl. launch + sync; one lane per piece (SHA-1 is sequential per message)"}
+            "note": "wall time per call incl. launch + sync; SHA-1 is sequential per message: one lane per piece, or for few long pieces (as here) two waves per 64 pieces (schedule + rounds)"}
 
 
 def host_case(eng, sizes, k, m, erased, reps=3, pinned=False):
