@@ -303,8 +303,8 @@ class Engine:
         return self._decode_parts(items, per_chunk=True)
 
     def _decode_parts(self, items, per_chunk: bool) -> list:
-        """Chunks with a missing primary go to the GPU in ONE sec_decode_batch call; a chunk whose
-        k blocks are its k primaries needs no field arithmetic at all (zfec's fec_decode writes
+        """Chunks with a missing primary go to the GPU in ONE sec_decode_batch_ex call (recover-only);
+        a chunk whose k blocks are its k primaries needs no field arithmetic at all (zfec's fec_decode writes
         nothing for present primaries and easyfec joins them, /root/reference/storb/util/
         piece.py:196-197), so it is the join of its blocks, taken as views with no staging or
         PCIe round trip.  Returns per chunk either that chunk's bytes (per_chunk) or a list of
@@ -329,7 +329,11 @@ class Engine:
                 raise Error(_lib.strerror(_lib.SEC_EPADLEN))
             if any(x >= k for x in sn):
                 gpu.append(i)
-        dev = {}
+        # The GPU only recovers (SEC_F_RECOVER: zfec fec_decode's own output, the e missing
+        # primaries, B bytes each, in primary order); the chunk is then the join of its present
+        # primaries and those rows, so only e * B bytes per chunk come back over PCIe instead of
+        # the whole reassembled chunk.
+        rec = {}
         if gpu:
             descs = np.zeros(len(gpu), dtype=DEC_DTYPE)
             nslots = sum(items[i][0] for i in gpu)
@@ -345,28 +349,30 @@ class Engine:
                     keep.append(kp)
                     bo[slot + q] = a
                     sn_arr[slot + q] = int(sharenums[q])
+                e = sum(1 for x in sharenums if int(x) >= k)
                 descs[j] = (total, B, padlen, slot, k, m)
-                dev[i] = (total, k * B - padlen)
+                rec[i] = total
                 slot += k
-                total += k * B - padlen
+                total += e * B
             buf = self._out_buffer(total)
-            self.decode_batch(descs, sn_arr, bo, 0, buf, host=True)
+            self.decode_batch(descs, sn_arr, bo, 0, buf, host=True, recover_only=True)
             mv = memoryview(buf)
         parts = []
         for i in range(n):
-            if i in dev:
-                o, ln = dev[i]
-                parts.append(bytes(mv[o:o + ln]) if per_chunk else mv[o:o + ln])
-                continue
             k, m, blocks, sharenums, padlen = items[i]
             B = len(blocks[0])
-            order = sorted(range(k), key=lambda q: int(sharenums[q]))  # primary j's block
+            prim = {int(x): q for q, x in enumerate(sharenums) if int(x) < k}  # primary -> its block
+            o = rec.get(i)
             left = k * B - padlen
             views = []
-            for q in order:
+            for j in range(k):
                 if left <= 0:
                     break
-                v = memoryview(blocks[q]).cast("B")
+                if j in prim:
+                    v = memoryview(blocks[prim[j]]).cast("B")
+                else:  # the next recovered row (rows come in primary order)
+                    v = mv[o:o + B]
+                    o += B
                 views.append(v[:left] if left < B else v)
                 left -= B
             if per_chunk:
