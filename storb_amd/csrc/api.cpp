@@ -893,8 +893,10 @@ uint64_t dec_nout(const sec_dec_chunk &c, const int32_t *sharenums, bool recover
 }
 
 // block_avail: nullable (device / zero-copy mode only: staged slots are zero-filled to B)
+// nocopy (reassembly of host buffers, see sec_decode_batch_ex): recovered rows at their output
+// rows as in a reassembly, but no present primary copied (the host copies those)
 int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const uint64_t *block_offs,
-                      const uint64_t *block_avail, const DecLayout &L, bool host, bool recover)
+                      const uint64_t *block_avail, const DecLayout &L, bool host, bool recover, bool nocopy = false)
 {
     Plan &plan = ctx->dec_plan;
     TableCache &tc = ctx->dec_tabs;
@@ -978,7 +980,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 const int from = L.perm[base + s];
                 soff.push_back(host ? sp.in_bytes + (uint64_t)s * c.B : block_offs[c.slot0 + from]);
                 // recover-only: no copies, and recovered row r goes to output row r
-                srow.push_back(!recover && idx[s] < c.k ? (uint32_t)idx[s] : 0xFFFFFFFFu);
+                srow.push_back(!recover && !nocopy && idx[s] < c.k ? (uint32_t)idx[s] : 0xFFFFFFFFu);
                 const uint64_t av = host ? c.B : slot_avail(c, block_avail, from);
                 savail.push_back((uint32_t)av);
                 min_avail = std::min(min_avail, av);
@@ -1003,7 +1005,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)c.B));
             sp.in_bytes += (uint64_t)c.k * c.B;
             sp.out_bytes += nout;
-            if (nout > 0)
+            if (nout > 0 && !(nocopy && e_of[i] == 0))
                 add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true);
         }
         std::vector<sec::Tile> tiles;
@@ -2156,14 +2158,46 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
         return SEC_OK;
     if (!out)  // blocks may be NULL: block_offs are then absolute addresses
         return SEC_EINVAL;
+    // A reassembly of host buffers leaves the present primaries to the host (the copy pool, from
+    // the caller's blocks into `out`) and moves only what the GPU computes over PCIe: the
+    // recovered rows, e * B per chunk instead of the whole chunk (SEC_HOST_JOIN=0: the GPU
+    // writes every output byte, the A/B).
+    const char *hj = getenv("SEC_HOST_JOIN");
+    const bool join = host && !recover && !(hj && hj[0] == '0');
     // pinned (or lockable) caller buffers: the device path on them directly (see encode_impl)
     HostLock lock(ctx->stream());
+    bool direct = false;
     if (host &&
         host_direct(ctx, decode_ranges(chunks, nchunks, sharenums, block_offs, block_avail, blocks, out, recover),
                     lock)) {
         host = false;
+        direct = true;
         flags &= ~(SEC_F_HOST | SEC_F_ASYNC);
     }
+    // the primaries a joining call copies on the host: row j of chunk i from the slot holding
+    // primary j, up to that slot's avail (zero past it), rows clipped to the chunk's n bytes
+    std::vector<sec::CopyJob> joins;
+    if (join) {
+        for (int64_t i = 0; i < nchunks; ++i) {
+            const sec_dec_chunk &c = chunks[i];
+            const uint64_t n = (uint64_t)c.k * c.B - c.padlen;
+            for (int q = 0; q < c.k; ++q) {
+                const int j = sharenums[c.slot0 + q];
+                if (j >= c.k || (uint64_t)j * c.B >= n)
+                    continue;
+                const uint64_t row = std::min<uint64_t>(c.B, n - (uint64_t)j * c.B);
+                const uint64_t av = std::min<uint64_t>(row, slot_avail(c, block_avail, q));
+                uint8_t *dst = out + c.out_off + (uint64_t)j * c.B;
+                joins.push_back(sec::CopyJob{dst, blocks + block_offs[c.slot0 + q], av});
+                if (av < row)
+                    joins.push_back(sec::CopyJob{dst + av, nullptr, row - av});
+            }
+        }
+    }
+    // staged joining calls run the kernels in recover mode (dense rows); direct ones write the
+    // recovered rows in place with the copies switched off (nocopy)
+    const bool prec = recover || (join && host);
+    const bool nocopy = join && direct;
 
     // Plan key (see sec_encode_batch): host mode keys on shapes + sharenums only (its slots
     // are staged densely, zero-filled past their avail); device mode on every descriptor,
@@ -2191,8 +2225,10 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
         if (ka)
             memcpy(key.data() + kc + total_slots * 12, block_avail, ka);
     }
-    // ASYNC does not change the plan; whether an avail array came does (0x10000)
-    const unsigned kflags = (flags & ~SEC_F_ASYNC) | (!host && block_avail ? 0x10000u : 0u);
+    // ASYNC does not change the plan; whether an avail array came does (0x10000), and how a
+    // joining call runs the kernels (recover 0x4 / nocopy 0x20000)
+    const unsigned kflags = (flags & ~SEC_F_ASYNC) | (!host && block_avail ? 0x10000u : 0u) |
+                            (prec ? SEC_F_RECOVER : 0u) | (nocopy ? 0x20000u : 0u);
     key.insert(key.end(), (const uint8_t *)&kflags, (const uint8_t *)&kflags + sizeof(unsigned));
     const bool reuse = plan.valid && plan.gen == ctx->dec_tabs.gen && plan.key == key;
     DecLayout L;
@@ -2200,7 +2236,7 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
         L = dec_layout(chunks, nchunks, sharenums);
     if (!reuse) {
         plan.valid = false;
-        RC(build_decode_plan(ctx, chunks, nchunks, block_offs, block_avail, L, host, recover));
+        RC(build_decode_plan(ctx, chunks, nchunks, block_offs, block_avail, L, host, prec, nocopy));
         plan.key.swap(key);
         plan.valid = true;
     }
@@ -2210,6 +2246,8 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
         RC(timing_begin(ctx, &t0, ctx->stream()));
         RC(launch_decode_sub(ctx, plan, plan.subs[0], blocks, out, ctx->stream()));
         RC(timing_end(ctx, t0, 1, ctx->stream()));
+        if (nocopy)  // the present primaries, host to host, while the kernels run
+            pool(ctx).run(joins);
         if (!(flags & SEC_F_ASYNC))
             CK(hipStreamSynchronize(ctx->stream()));
         return SEC_OK;
@@ -2232,15 +2270,31 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
         uint64_t o = 0;
         for (int64_t i = sp.c0; i < sp.c1; ++i) {
             const sec_dec_chunk &c = chunks[i];
-            const uint64_t nout = dec_nout(c, sharenums, recover);
-            jobs.push_back(sec::CopyJob{out + c.out_off, stage + o, nout});
+            const uint64_t nout = dec_nout(c, sharenums, prec);
+            if (!join) {
+                jobs.push_back(sec::CopyJob{out + c.out_off, stage + o, nout});
+            } else {  // the recovered rows (dense, in primary order) to their output rows
+                const uint64_t n = (uint64_t)c.k * c.B - c.padlen;
+                uint64_t r = 0;
+                for (int s = 0; s < c.k; ++s) {  // slot s of the normalised layout = primary s
+                    if (L.idx[L.first[i] + s] < c.k)
+                        continue;
+                    if ((uint64_t)s * c.B < n)
+                        jobs.push_back(sec::CopyJob{out + c.out_off + (uint64_t)s * c.B, stage + o + r * c.B,
+                                                    std::min<uint64_t>(c.B, n - (uint64_t)s * c.B)});
+                    ++r;
+                }
+            }
             o += nout;
         }
     };
     auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
         return launch_decode_sub(ctx, plan, sp, din, dout, s);
     };
-    return run_pipeline(ctx, plan, gather, scatter, launch, true);
+    RC(run_pipeline(ctx, plan, gather, scatter, launch, true));
+    if (join)  // the present primaries, host to host
+        pool(ctx).run(joins);
+    return SEC_OK;
 }
 
 // ---------------------------------------------------------------------------
