@@ -329,3 +329,68 @@ def test_fuzz_mixed_shapes_erasures_one_batch(engine):
             for j, r in enumerate(miss):
                 got = out_h[base + j * B[i]:base + (j + 1) * B[i]].tobytes()
                 assert got == blocks[r], (i, k, m, r)
+
+
+@pytest.mark.parametrize("mode", ["staged", "locked", "pinned"])
+def test_fuzz_host_reassembly_join(mode, monkeypatch):
+    """Host-buffer reassembly (the host copies the present primaries, the GPU returns only the
+    recovered rows) on each host path, randomized: mixed (k, m), random survivors in random
+    order (parity-only ones included), block k-1 read in place with its short avail; the output
+    buffer is pre-filled so every byte must be written; against the source bytes."""
+    from storb_amd.engine import Engine
+
+    if mode == "staged":
+        monkeypatch.setenv("SEC_REGISTER_MIN", "0")  # never page-lock: stage through the slabs
+    eng = Engine(0)
+    try:
+        rng = random.Random(77)
+        shapes, sizes = [], []
+        while len(shapes) < 60:
+            k = rng.choice([1, 2, 4, 5, 8, 10, 16, 24])
+            m = min(256, k + rng.randrange(1, k + 3))
+            n = rng.randrange(1, 400000)
+            if n <= (k - 1) * -(-n // k):
+                continue
+            shapes.append((k, m))
+            sizes.append(n)
+        total = sum(sizes)
+        B = [-(-n // k) for n, (k, m) in zip(sizes, shapes)]
+        in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+        pcount = [b * (m - k) for b, (k, m) in zip(B, shapes)]
+        par_off = np.concatenate([[0], np.cumsum(pcount)[:-1]]).astype(np.uint64)
+        alloc = (lambda n: eng.host_empty(n)) if mode == "pinned" else (lambda n: np.empty(n, np.uint8))
+        hin = alloc(total)
+        hin[:] = np.frombuffer(rng.randbytes(total), np.uint8)
+        hpar = alloc(int(sum(pcount)))
+        ed = np.zeros(len(sizes), dtype=ENC_DTYPE)
+        ed["in_off"], ed["n"], ed["parity_off"], ed["parity_stride"] = in_off, sizes, par_off, B
+        ed["k"] = [k for k, _ in shapes]
+        ed["m"] = [m for _, m in shapes]
+        eng.encode_batch(ed, hin, hpar, host=True)
+        nslots = sum(k for k, _ in shapes)
+        dd = np.zeros(len(sizes), dtype=DEC_DTYPE)
+        sn = np.zeros(nslots, np.int32)
+        offs = np.zeros(nslots, np.uint64)
+        avail = np.zeros(nslots, np.uint64)
+        slot = 0
+        for i, (k, m) in enumerate(shapes):
+            b = B[i]
+            dd["out_off"][i], dd["B"][i], dd["padlen"][i] = int(in_off[i]), b, b * k - sizes[i]
+            dd["k"][i], dd["m"][i], dd["slot0"][i] = k, m, slot
+            for s in rng.sample(range(m), k):
+                sn[slot] = s
+                if s < k:
+                    offs[slot] = hin.ctypes.data + int(in_off[i]) + s * b
+                    avail[slot] = sizes[i] - s * b if s == k - 1 else b
+                else:
+                    offs[slot] = hpar.ctypes.data + int(par_off[i]) + (s - k) * b
+                    avail[slot] = b
+                slot += 1
+        out = alloc(total)
+        out[:] = 0xA5
+        eng.decode_batch(dd, sn, offs, 0, out, block_avail=avail, host=True)
+        assert np.array_equal(out, hin), mode
+        z, r, st = eng.host_paths()  # (zero-copy pinned, locked per call, staged) calls
+        assert {"pinned": z, "locked": r, "staged": st}[mode] >= 2, (mode, z, r, st)
+    finally:
+        eng.close()
