@@ -16,8 +16,8 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libstorbec.so")
 INCLUDE = os.path.join(ROOT, "include")
-SOURCES = ["kernels.hip", "kernels_mfma.hip", "kernels_xb.hip", "bignum.hip", "api.cpp"]
-HEADERS = ["kernels.hpp", "bignum.hpp", "gf_host.hpp", "copy_pool.hpp"]
+SOURCES = ["kernels.hip", "kernels_mfma.hip", "kernels_xb.hip", "kernels_bs.hip", "bignum.hip", "api.cpp"]
+HEADERS = ["kernels.hpp", "bignum.hpp", "gf_host.hpp", "gf_const.hpp", "copy_pool.hpp"]
 ARCH = os.environ.get("STORB_EC_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -46,9 +46,24 @@ def build(force: bool = False, verbose: bool = False, defines: dict | None = Non
             if f.read().strip() == dig:
                 return lib
     tmp = lib + ".tmp"
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", *defs, "-o", tmp]
-    cmd += [os.path.join(CSRC, s) for s in SOURCES]
+    # one hipcc per source, in parallel (the device code of each file is compiled on its own
+    # anyway), then one link
+    objdir = os.path.join(LIBDIR, "obj_" + (tag or "lib"))
+    os.makedirs(objdir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+             f"-I{INCLUDE}", *defs]
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = os.path.join(objdir, src + ".o")
+        objs.append(obj)
+        cmd = [HIPCC, *flags, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((src, subprocess.Popen(cmd)))
+    failed = [src for src, p in procs if p.wait() != 0]
+    if failed:
+        raise RuntimeError(f"hipcc failed on {', '.join(failed)}")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", tmp, *objs]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -131,6 +131,7 @@ struct Group {
     uint32_t first, count;
     int mfma = 0;              // 1: sec_encode_mfma_kernel<G = U, TILES = rows> (encode, k = 32 * G);
                                // 2: sec_encode_xb_kernel of shape `rows`, W = U (encode)
+                               // 3: sec_encode_bs_kernel of shape `rows`, row group U (encode)
 };
 
 // One launch unit: all chunks (device mode) or one slab of chunks (host mode).
@@ -366,6 +367,63 @@ int xb_width(int shape)
     return w == 1 || w == 2 ? (int)w : shape == 1 ? 2 : 1;
 }
 
+// Bit-sliced compile-time-matrix encode (kernels_bs.hip) for the shapes it is built for
+// (C4's zfec(10,14), C5's (8,11), the policy's (8,12), (16,24), (32,48), (64,96)): every
+// position [0, B) of a chunk with B >= 16, ragged end included, so such a chunk gets no
+// sec_encode_kernel tile.  Tiles of SEC_BS_LANES lanes (default 256 = 8 KiB of each block).
+// A shape of several row groups ((64,96): 2 x 16 rows) runs them in one launch, a run of 8
+// tiles of each group in turn, so the tiles that read the same blocks share an XCD's L2
+// (SEC_BS_SPLIT=1: one launch per group instead).  SEC_BS=0 turns the kernel off (then xb /
+// v_perm as before), SEC_BS=1 uses it for every shape it has; SEC_BS_R8=1 takes (32,48) in two
+// groups of 8 rows.  All read per plan build.
+constexpr int kBsAllGroups = 99;  // Group::U of an interleaved launch of every row group
+
+int bs_shape(int k, int m, uint64_t B)
+{
+    const char *e = getenv("SEC_BS");
+    if (e && e[0] == '0')
+        return -1;
+    if (B < 16 || B > 0xFFFFFFFFull - 8192)
+        return -1;
+    const int p = m - k;
+    if (!(e && e[0] == '1') && p < 8)  // p <= 4: the v_perm kernel is HBM-bound and as fast or faster
+        return -1;
+    if (k == 32 && m == 48 && env_size("SEC_BS_R8", 0))
+        return sec_bs_shape(k, m, 8);
+    return sec_bs_shape(k, m);
+}
+
+void add_bs_work(Bins &bins, uint32_t chunk, uint64_t B, int shape)
+{
+    const int lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
+    const uint64_t step = (uint64_t)sec_bs_span() * (lanes / 64);
+    const int ng = sec_bs_groups(shape);
+    if (ng > 1 && !env_size("SEC_BS_SPLIT", 0)) {  // flatten() interleaves the groups
+        auto &bin = bins[{3, shape, kBsAllGroups, lanes, 0}];
+        for (uint64_t t0 = 0; t0 < B; t0 += step)
+            bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
+        return;
+    }
+    for (int g = 0; g < ng; ++g) {
+        auto &bin = bins[{3, shape, g, lanes, 0}];
+        for (uint64_t t0 = 0; t0 < B; t0 += step)
+            bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
+    }
+}
+
+// Tiles of an interleaved bit-sliced launch: runs of 8 positions, each run once per row group
+// (tile r0 = the group's first row), so a position's tiles are 8 workgroups apart (one XCD).
+void bs_interleave(int shape, const std::vector<sec::Tile> &pos, std::vector<sec::Tile> &out)
+{
+    const int ng = sec_bs_groups(shape), nr = sec_bs_rows(shape);
+    for (size_t i = 0; i < pos.size(); i += 8) {
+        const size_t e = std::min(pos.size(), i + 8);
+        for (int g = 0; g < ng; ++g)
+            for (size_t j = i; j < e; ++j)
+                out.push_back(sec::Tile{pos[j].chunk, pos[j].t0, (uint32_t)(g * nr), 0});
+    }
+}
+
 uint64_t add_xb_work(Bins &bins, uint32_t chunk, int64_t valid, int shape)
 {
     const uint64_t vx = valid > 0 ? sec_xb_end((uint32_t)valid) : 0;
@@ -416,11 +474,14 @@ void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile
     for (auto &kv : bins) {
         if (kv.second.empty())
             continue;
-        groups.push_back(Group{std::get<1>(kv.first), std::get<2>(kv.first), std::get<3>(kv.first),
-                               std::get<4>(kv.first), (uint32_t)tiles.size(), (uint32_t)kv.second.size(),
-                               std::get<0>(kv.first)});
         const size_t first = tiles.size();
-        tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
+        if (std::get<0>(kv.first) == 3 && std::get<2>(kv.first) == kBsAllGroups)
+            bs_interleave(std::get<1>(kv.first), kv.second, tiles);
+        else
+            tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
+        groups.push_back(Group{std::get<1>(kv.first), std::get<2>(kv.first), std::get<3>(kv.first),
+                               std::get<4>(kv.first), (uint32_t)first, (uint32_t)(tiles.size() - first),
+                               std::get<0>(kv.first)});
         if (use_xcd_order(decode, groups.back())) {
             std::vector<sec::Tile> g(tiles.begin() + first, tiles.end());
             xcd_order(g);
@@ -794,7 +855,10 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             }
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
-            if (p > 0) {
+            const int bs = p > 0 && mt == mtab_of.end() ? bs_shape(c.k, c.m, B) : -1;
+            if (bs >= 0) {
+                add_bs_work(bins, (uint32_t)(i - c0), B, bs);
+            } else if (p > 0) {
                 const int xs = mt == mtab_of.end() ? xb_shape(c.k, c.m) : -1;
                 const uint64_t start = mt != mtab_of.end() ? add_mfma_work(bins, (uint32_t)(i - c0), valid, c.k, c.m)
                                        : xs >= 0             ? add_xb_work(bins, (uint32_t)(i - c0), valid, xs)
@@ -831,10 +895,13 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
         int e = g.mfma == 1 ? sec_launch_encode_mfma(g.U, g.rows, in, par, dd, dt + g.first, g.count,
                                                      plan.meta.as<uint8_t>(sp.off_mtab), s)
                 : g.mfma == 2 ? sec_launch_encode_xb(g.rows, g.U, in, par, dd, dt + g.first, g.count, s)
+                : g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsAllGroups ? -1 : g.U, g.lanes, in, par, dd,
+                                                     dt + g.first, g.count, s)
                               : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
         if (e)
             return hip_fail((hipError_t)e, g.mfma == 1   ? "sec_encode_mfma_kernel"
                                            : g.mfma == 2 ? "sec_encode_xb_kernel"
+                                           : g.mfma == 3 ? "sec_encode_bs_kernel"
                                                          : "sec_encode_kernel");
     }
     if (sp.ntail) {

@@ -122,6 +122,17 @@ int sec_xb_shape(int k, int m);
 uint32_t sec_xb_end(uint32_t valid);
 int sec_launch_encode_xb(int shape, int W, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
                          const sec::Tile *t, uint32_t ntiles, void *stream);
+// Bit-sliced compile-time-matrix encode (kernels_bs.hip) for the shapes sec_bs_shape knows
+// (else -1; rows = 0: the first kernel of that (k, m), else the one of `rows` rows per group):
+// all of [0, B) of chunks with B >= 16, row group `group` of sec_bs_groups(shape) (-1: every
+// group in one launch, each tile's r0 = group * sec_bs_rows(shape)), tiles of `lanes` (64..256)
+// lanes over lanes / 64 wave spans of sec_bs_span() positions
+int sec_bs_shape(int k, int m, int rows = 0);
+int sec_bs_groups(int shape);
+int sec_bs_rows(int shape);
+uint32_t sec_bs_span();
+int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
+                         const sec::Tile *t, uint32_t ntiles, void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
                            uint32_t nitems, const uint32_t *tabs, void *stream);
 int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,

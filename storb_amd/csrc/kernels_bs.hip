@@ -1,0 +1,359 @@
+// kernels_bs.hip — bit-sliced encode with the zfec matrix fixed at compile time, for the
+// shapes whose v_perm encode is VALU-bound: C4's RS(10,4) = zfec(10,14) and the policy's
+// zfec(8,12), (16,24), (32,48), (64,96), plus C5's RS(8,3).
+//
+// Multiplication by a constant c is GF(2)-linear on a byte's 8 bits: bit i of c*x is the XOR
+// of the bits s of x for which bit i of c*alpha^s is set (an 8-bit mask per (c, i), a
+// compile-time constant here).  So a lane turns 32 bytes of a block into 8 bit planes (one
+// dword per bit position, an 8x8 bit transpose of each byte column: 48 VALU for 8 dwords),
+// and every parity row's output plane i is
+//     acc[r][i] ^= lo[mask & 15] ^ hi[mask >> 4]        (one XOR3)
+// where lo / hi are the XORs of the subsets of planes 0..3 / 4..7 (at most 11 + 11 VALU per
+// block, only the subsets some row uses survive compilation).  The parity planes are
+// transposed back (the transpose is its own inverse) and stored.  Per input dword:
+//     6 (transpose) + <= 2.75 (subsets) + p (rows) + 6 p / k (transpose out)
+// against 5 + 4.5 p .. 5 p for sec_encode_kernel's v_perm rows and 35 + 22 + p for
+// sec_encode_xb_kernel: C4 15.8 instead of 25, zfec(16,24) 19.8 instead of ~45, (32,48) 27.8
+// instead of 69.
+//
+// Layout.  A wave covers 2048 positions of a chunk: lane l owns the 16 bytes at s + 16 l and
+// the 16 at s + 1024 + 16 l of every block (each load instruction is one coalesced 1 KiB
+// run).  A workgroup of `lanes` lanes covers lanes / 64 consecutive wave spans.  In the
+// chunk's last span a piece that would run past B is moved back to end at B (it recomputes
+// and stores bytes a neighbour also stores, identical), so the kernel covers all of [0, B) of
+// every chunk with B >= 16, the ragged end included: block k-1's bytes past `valid` (zfec's
+// zero padding) read as zero.  Parity rows [R0, R0 + NR) per launch; (64,96)'s 32 rows take
+// two launches of 16 (256 accumulator
+// dwords would not fit a lane's registers).  Loads stream through a ring of D blocks in
+// flight.  Results are zfec's fec_encode (restated in oracle/fec_oracle.c;
+// /root/reference/storb/util/piece.py:129-130).
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <utility>
+
+#include "gf_const.hpp"
+#include "kernels.hpp"
+
+namespace {
+
+using u8 = uint8_t;
+using u32 = uint32_t;
+using u64 = uint64_t;
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+
+constexpr u32 kSpan = 2048;  // positions per wave
+
+// mask of the input bits s that feed bit i of c * x
+constexpr u32 plane_mask(u32 c, int i)
+{
+    u32 m = 0;
+    for (int s = 0; s < 8; ++s)
+        if ((gfc::gmul(c, 1u << s) >> i) & 1u)
+            m |= 1u << s;
+    return m;
+}
+static_assert(plane_mask(1, 3) == 8 && plane_mask(2, 0) == 0x80 && plane_mask(2, 1) == 0x01, "plane masks");
+
+__device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c)
+{
+    u32 r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// (m & x) | (~m & y), as one v_bfi_b32 (opaque to the compiler: left to itself it folded the
+// transpose's masks into the later XORs and issued 1.4x the instructions)
+__device__ __forceinline__ u32 bfi(u32 m, u32 x, u32 y)
+{
+    u32 r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(x), "v"(y));
+    return r;
+}
+
+// Swap the bits of a at (MK << S) with the bits of b at MK: one 2x2 block step of an 8x8 bit
+// transpose applied to each byte column of rows a and b (4 VALU).
+template <int S, u32 MK>
+__device__ __forceinline__ void swap_bits(u32 &a, u32 &b)
+{
+    constexpr u32 HI = MK << S;
+    const u32 na = bfi(HI, b << S, a);
+    const u32 nb = bfi(MK, a >> S, b);
+    a = na;
+    b = nb;
+}
+
+// x[i] byte q bit b  <->  x[b] byte q bit i  (an involution)
+__device__ __forceinline__ void transpose8(u32 (&x)[8])
+{
+    swap_bits<4, 0x0F0F0F0Fu>(x[0], x[4]);
+    swap_bits<4, 0x0F0F0F0Fu>(x[1], x[5]);
+    swap_bits<4, 0x0F0F0F0Fu>(x[2], x[6]);
+    swap_bits<4, 0x0F0F0F0Fu>(x[3], x[7]);
+    swap_bits<2, 0x33333333u>(x[0], x[2]);
+    swap_bits<2, 0x33333333u>(x[1], x[3]);
+    swap_bits<2, 0x33333333u>(x[4], x[6]);
+    swap_bits<2, 0x33333333u>(x[5], x[7]);
+    swap_bits<1, 0x55555555u>(x[0], x[1]);
+    swap_bits<1, 0x55555555u>(x[2], x[3]);
+    swap_bits<1, 0x55555555u>(x[4], x[5]);
+    swap_bits<1, 0x55555555u>(x[6], x[7]);
+}
+
+__device__ __forceinline__ u32x4 ld16(const u8 *p)
+{
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(p));
+}
+
+// 16 bytes at base + off of which the first `avail - off` exist; the rest read as zero
+__device__ __forceinline__ u32x4 ld16_avail(const u8 *base, u32 off, u32 avail)
+{
+    if (off + 16 <= avail)
+        return ld16(base + off);
+    u32 w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 16; ++b)
+        if (off + b < avail)
+            w[b >> 2] |= (u32)base[off + b] << (8 * (b & 3));
+    return u32x4{w[0], w[1], w[2], w[3]};
+}
+
+__device__ __forceinline__ void st16(u8 *p, u32 a, u32 b, u32 c, u32 d)
+{
+    __builtin_nontemporal_store(u32x4{a, b, c, d}, reinterpret_cast<u32x4_u *>(p));
+}
+
+// acc (= or ^=) the output plane whose input mask is MSK
+template <u32 MSK, bool FIRST>
+__device__ __forceinline__ void upd(u32 &acc, const u32 (&lo)[16], const u32 (&hi)[16])
+{
+    constexpr u32 l = MSK & 15, h = MSK >> 4;
+    if constexpr (FIRST) {
+        if constexpr (l && h)
+            acc = lo[l] ^ hi[h];
+        else if constexpr (l)
+            acc = lo[l];
+        else if constexpr (h)
+            acc = hi[h];
+        else
+            acc = 0;
+    } else {
+        if constexpr (l && h)
+            acc = xor3(acc, lo[l], hi[h]);
+        else if constexpr (l)
+            acc ^= lo[l];
+        else if constexpr (h)
+            acc ^= hi[h];
+    }
+}
+
+// XORs of every subset of v[0..3] (s[S] for S = 1..15; those no row reads are dead code)
+__device__ __forceinline__ void subsets(u32 v0, u32 v1, u32 v2, u32 v3, u32 (&s)[16])
+{
+    s[0] = 0;
+    s[1] = v0;
+    s[2] = v1;
+    s[4] = v2;
+    s[8] = v3;
+    s[3] = v0 ^ v1;
+    s[5] = v0 ^ v2;
+    s[6] = v1 ^ v2;
+    s[9] = v0 ^ v3;
+    s[10] = v1 ^ v3;
+    s[12] = v2 ^ v3;
+    s[7] = s[3] ^ v2;
+    s[11] = s[3] ^ v3;
+    s[13] = s[5] ^ v3;
+    s[14] = s[6] ^ v3;
+    s[15] = s[7] ^ v3;
+}
+
+template <int K, int M, int R0, int J, bool FIRST, int... Q>
+__device__ __forceinline__ void block_rows(std::integer_sequence<int, Q...>, u32 (&acc)[sizeof...(Q)],
+                                           const u32 (&lo)[16], const u32 (&hi)[16])
+{
+    (upd<plane_mask(gfc::Matrix<K, M>::v.c[R0 + Q / 8][J], Q % 8), FIRST>(acc[Q], lo, hi), ...);
+}
+
+// the lane's two 16-byte pieces of a block: at pa and pb
+__device__ __forceinline__ void load_block(u32 (&x)[8], const u8 *blk, u32 pa, u32 pb, u32 avail, bool last)
+{
+    u32x4 a, b;
+    if (!last) {
+        a = ld16(blk + pa);
+        b = ld16(blk + pb);
+    } else {
+        a = ld16_avail(blk, pa, avail);
+        b = ld16_avail(blk, pb, avail);
+    }
+    x[0] = a.x;
+    x[1] = a.y;
+    x[2] = a.z;
+    x[3] = a.w;
+    x[4] = b.x;
+    x[5] = b.y;
+    x[6] = b.z;
+    x[7] = b.w;
+}
+
+template <int K, int M, int R0, int NR, int D, int J>
+__device__ __forceinline__ void one_block(u32 (&acc)[NR * 8], u32 (&ring)[D][8], const u8 *src, u64 B, u32 pa,
+                                          u32 pb, u32 valid)
+{
+    u32 x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        x[i] = ring[J % D][i];
+    if constexpr (J + D < K)
+        load_block(ring[J % D], src + (u64)(J + D) * B, pa, pb, valid, J + D == K - 1);
+    transpose8(x);
+    u32 lo[16], hi[16];
+    subsets(x[0], x[1], x[2], x[3], lo);
+    subsets(x[4], x[5], x[6], x[7], hi);
+    block_rows<K, M, R0, J, J == 0>(std::make_integer_sequence<int, NR * 8>{}, acc, lo, hi);
+}
+
+template <int K, int M, int R0, int NR, int D, int... Js>
+__device__ __forceinline__ void all_blocks(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], u32 (&ring)[D][8],
+                                           const u8 *src, u64 B, u32 pa, u32 pb, u32 valid)
+{
+    (one_block<K, M, R0, NR, D, Js>(acc, ring, src, B, pa, pb, valid), ...);
+}
+
+// One wave's span of one tile: rows [R0, R0 + NR) of the chunk's parity over the lane's pieces.
+template <int K, int M, int R0, int NR, int D>
+__device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d, u32 s)
+{
+    static_assert(D >= 1 && D <= K, "ring depth");
+    const u32 B = d.B;
+    // a piece past the chunk's end moves back to end at B: it recomputes (and stores) bytes
+    // its neighbour also stores, identical, instead of taking a byte path
+    const u32 lane = (threadIdx.x & 63) * 16;
+    const u32 pa = min(s + lane, B - 16), pb = min(s + 1024 + lane, B - 16);
+    const u8 *src = in + d.in_off;
+
+    u32 ring[D][8];
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        load_block(ring[j], src + (u64)j * B, pa, pb, d.valid, j == K - 1);
+    u32 acc[NR * 8];
+    all_blocks<K, M, R0, NR, D>(std::make_integer_sequence<int, K>{}, acc, ring, src, B, pa, pb, d.valid);
+
+    u8 *dst = par + d.par_off;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        u32 y[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            y[i] = acc[r * 8 + i];
+        transpose8(y);
+        u8 *o = dst + (u64)(R0 + r) * d.par_stride;
+        st16(o + pa, y[0], y[1], y[2], y[3]);
+        st16(o + pb, y[4], y[5], y[6], y[7]);
+    }
+}
+
+// Rows [R0, R0 + NR) of every tile.
+template <int K, int M, int R0, int NR, int D>
+__global__ __launch_bounds__(256) void sec_encode_bs_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+                                                            const sec::EncDesc *__restrict__ descs,
+                                                            const sec::Tile *__restrict__ tiles)
+{
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::EncDesc d = descs[tl.chunk];
+    const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
+    if (s >= d.B)
+        return;
+    bs_span<K, M, R0, NR, D>(in, par, d, s);
+}
+
+// Two row groups in one launch, the tile's r0 picking one: the plan puts a run of 8 tiles of
+// group 0 and the same 8 positions of group 1 next in the launch, so each pair lands on one
+// XCD (workgroup b runs on XCD b % 8) at about the same time and the second reads the blocks
+// from that XCD's L2 instead of HBM.
+template <int K, int M, int NR, int D>
+__global__ __launch_bounds__(256) void sec_encode_bs2_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+                                                             const sec::EncDesc *__restrict__ descs,
+                                                             const sec::Tile *__restrict__ tiles)
+{
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::EncDesc d = descs[tl.chunk];
+    const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
+    if (s >= d.B)
+        return;
+    if (tl.r0 == 0)
+        bs_span<K, M, 0, NR, D>(in, par, d, s);
+    else
+        bs_span<K, M, NR, NR, D>(in, par, d, s);
+}
+
+template <int K, int M, int R0, int NR, int D>
+hipError_t launch_bs(int lanes, const u8 *in, u8 *par, const sec::EncDesc *d, const sec::Tile *t, u32 nt,
+                     hipStream_t s)
+{
+    void *a = nullptr, *b = nullptr;
+    sec_next_launch_events(&a, &b);  // kernel timing (sec_ctx_set_timing) rides on the dispatch
+    if constexpr (R0 < 0)
+        hipExtLaunchKernelGGL((sec_encode_bs2_kernel<K, M, NR, D>), dim3(nt), dim3(lanes), 0, s, (hipEvent_t)a,
+                              (hipEvent_t)b, 0, in, par, d, t);
+    else
+        hipExtLaunchKernelGGL((sec_encode_bs_kernel<K, M, R0, NR, D>), dim3(nt), dim3(lanes), 0, s, (hipEvent_t)a,
+                              (hipEvent_t)b, 0, in, par, d, t);
+    return hipGetLastError();
+}
+
+// Shapes: (k, m, rows per launch).  Ring depths from the register budget: 8 NR accumulators
+// + 8 D ring dwords per lane; SEC_BS_RING (build knob, A/B) sets one depth for every shape.
+#ifdef SEC_BS_RING
+#define RING_K(k, d) (SEC_BS_RING < (k) ? SEC_BS_RING : (k))
+#else
+#define RING_K(k, d) (d)
+#endif
+struct BsShape {
+    int k, m, nr;
+};
+// 6: (32,48) in two groups of 8 rows (A/B against shape 3's one pass of 16)
+constexpr BsShape kShapes[] = {{10, 14, 4}, {8, 12, 4}, {16, 24, 8}, {32, 48, 16}, {64, 96, 16}, {8, 11, 3}, {32, 48, 8}};
+constexpr int kNShapes = (int)(sizeof(kShapes) / sizeof(kShapes[0]));
+
+}  // namespace
+
+int sec_bs_shape(int k, int m, int rows)
+{
+    for (int i = 0; i < kNShapes; ++i)
+        if (kShapes[i].k == k && kShapes[i].m == m && (rows == 0 || kShapes[i].nr == rows))
+            return i;
+    return -1;
+}
+
+int sec_bs_groups(int shape) { return (kShapes[shape].m - kShapes[shape].k + kShapes[shape].nr - 1) / kShapes[shape].nr; }
+
+int sec_bs_rows(int shape) { return kShapes[shape].nr; }
+
+uint32_t sec_bs_span() { return kSpan; }
+
+int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
+                         const sec::Tile *t, uint32_t ntiles, void *stream)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    if (lanes < 64 || lanes > 256 || lanes % 64 || shape < 0 || shape >= kNShapes)
+        return hipErrorInvalidValue;
+    hipStream_t s = (hipStream_t)stream;
+    // group -1: both row groups in one launch (sec_encode_bs2_kernel), tiles carry r0
+    switch (shape * 4 + group + 1) {
+    case 1: return launch_bs<10, 14, 0, 4, RING_K(10, 5)>(lanes, in, par, descs, t, ntiles, s);
+    case 5: return launch_bs<8, 12, 0, 4, RING_K(8, 4)>(lanes, in, par, descs, t, ntiles, s);
+    case 9: return launch_bs<16, 24, 0, 8, RING_K(16, 4)>(lanes, in, par, descs, t, ntiles, s);
+    case 13: return launch_bs<32, 48, 0, 16, RING_K(32, 2)>(lanes, in, par, descs, t, ntiles, s);
+    case 16: return launch_bs<64, 96, -1, 16, RING_K(64, 2)>(lanes, in, par, descs, t, ntiles, s);
+    case 17: return launch_bs<64, 96, 0, 16, RING_K(64, 2)>(lanes, in, par, descs, t, ntiles, s);
+    case 18: return launch_bs<64, 96, 16, 16, RING_K(64, 2)>(lanes, in, par, descs, t, ntiles, s);
+    case 21: return launch_bs<8, 11, 0, 3, RING_K(8, 4)>(lanes, in, par, descs, t, ntiles, s);
+    case 24: return launch_bs<32, 48, -1, 8, RING_K(32, 4)>(lanes, in, par, descs, t, ntiles, s);
+    case 25: return launch_bs<32, 48, 0, 8, RING_K(32, 4)>(lanes, in, par, descs, t, ntiles, s);
+    case 26: return launch_bs<32, 48, 8, 8, RING_K(32, 4)>(lanes, in, par, descs, t, ntiles, s);
+    default: return hipErrorInvalidValue;
+    }
+}

@@ -23,6 +23,7 @@
 
 #include <utility>
 
+#include "gf_const.hpp"
 #include "kernels.hpp"
 
 namespace {
@@ -34,64 +35,7 @@ typedef u32 u32_u __attribute__((aligned(1)));
 typedef u32 u32x2 __attribute__((ext_vector_type(2)));
 typedef u32x2 u32x2_u __attribute__((aligned(1)));
 
-// ---- GF(2^8) / 0x11D and zfec's systematic matrix, at compile time ---------------------
-struct Gf {
-    u8 exp[512];
-    u8 log[256];
-};
-
-constexpr Gf make_gf()
-{
-    Gf t{};
-    u32 v = 1;
-    for (int e = 0; e < 255; ++e) {
-        t.exp[e] = (u8)v;
-        t.exp[e + 255] = (u8)v;
-        t.log[v] = (u8)e;
-        v <<= 1;
-        if (v & 0x100)
-            v ^= 0x11D;
-    }
-    t.exp[510] = t.exp[0];
-    t.exp[511] = t.exp[1];
-    return t;
-}
-constexpr Gf kGf = make_gf();
-constexpr u32 gmul(u32 a, u32 b) { return (a && b) ? kGf.exp[kGf.log[a] + kGf.log[b]] : 0u; }
-constexpr u32 ginv(u32 a) { return kGf.exp[255 - kGf.log[a]]; }
-// zfec's evaluation points: p_0 = 0, p_i = alpha^(i-1)
-constexpr u32 point(int i) { return i == 0 ? 0u : kGf.exp[(i - 1) % 255]; }
-
-// Parity rows of zfec's encode matrix: c[r][j] = L_j(p_{k+r}), the Lagrange basis polynomial of
-// point j over points 0..k-1 (the closed form of _invert_vdm + _matmul; SURVEY.md Appendix A,
-// oracle/fec_oracle.c build_enc_matrix).
-template <int K, int M>
-struct EncMatrix {
-    u8 c[M - K][K];
-    constexpr EncMatrix() : c{}
-    {
-        u32 den[K] = {};  // prod over i != j of (p_j - p_i)
-        for (int j = 0; j < K; ++j) {
-            u32 d = 1;
-            for (int i = 0; i < K; ++i)
-                if (i != j)
-                    d = gmul(d, point(j) ^ point(i));
-            den[j] = d;
-        }
-        for (int r = 0; r < M - K; ++r) {
-            const u32 P = point(K + r);
-            u32 N = 1;  // prod over all i < K of (P - p_i)
-            for (int i = 0; i < K; ++i)
-                N = gmul(N, P ^ point(i));
-            for (int j = 0; j < K; ++j)
-                c[r][j] = (u8)gmul(gmul(N, ginv(P ^ point(j))), ginv(den[j]));
-        }
-    }
-};
-// zfec(4,6) and (2,3) rows as restated in SURVEY.md Appendix A (and tests/golden)
-static_assert(EncMatrix<4, 6>().c[0][0] == 0x77 && EncMatrix<4, 6>().c[0][3] == 0x0e, "zfec(4,6) row 0");
-static_assert(EncMatrix<4, 6>().c[1][0] == 0xc7 && EncMatrix<4, 6>().c[1][3] == 0x6c, "zfec(4,6) row 1");
-static_assert(EncMatrix<2, 3>().c[0][0] == 0x03 && EncMatrix<2, 3>().c[0][1] == 0x02, "zfec(2,3)");
+using gfc::Matrix;
 
 // ---- device arithmetic --------------------------------------------------------------------
 __device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c)
@@ -163,11 +107,6 @@ __device__ __forceinline__ u32 subset(const u32 (&v)[4], u32 pair23)
 __host__ __device__ constexpr u32 xb_end(u32 valid) { return valid / 16 * 16; }
 
 constexpr int kRing = 8;  // blocks whose loads are in flight ahead of the one being combined
-
-template <int K, int M>
-struct Matrix {
-    static constexpr EncMatrix<K, M> v{};
-};
 
 // Everything below is instantiated per (block J, row R): the coefficient is a template
 // constant, so each row's update compiles to at most one XOR3 with no run-time branch.

@@ -562,6 +562,7 @@ def test_encode_compile_time_matrix_shapes(xb_w, monkeypatch):
     unaligned B, mixed with other shapes in one batch; "off" (SEC_XB=0) is the v_perm path."""
     from storb_amd.engine import Engine
 
+    monkeypatch.setenv("SEC_BS", "0")  # the bit-sliced kernel would take these shapes first
     if xb_w == "off":
         monkeypatch.setenv("SEC_XB", "0")
     else:

@@ -66,6 +66,11 @@ VARIANTS = {
     "ldstab": {"SEC_LDS_TAB": 1},
     "ldstab_fk10": {"SEC_LDS_TAB": 1, "SEC_FIXED_K": 10},
     "noldstab": {"SEC_LDS_TAB": 0},
+    # bit-sliced encode (kernels_bs.hip): one ring depth (blocks in flight) for every shape
+    "bsr2": {"SEC_BS_RING": 2},
+    "bsr3": {"SEC_BS_RING": 3},
+    "bsr8": {"SEC_BS_RING": 8},
+    "bsr10": {"SEC_BS_RING": 10},
 }
 
 
