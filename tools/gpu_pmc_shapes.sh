@@ -3,8 +3,9 @@
 #   FETCH_SIZE, WRITE_SIZE (separate TCC passes), an SQ issue/wait pass with GRBM_GUI_ACTIVE,
 #   and a --kernel-trace --stats pass.  Each pass is its own rocprofv3 run under its own
 #   timeout; the first failure ends the script.  Summarised by tools/pmc_shapes.py.
+#   PMC_TAG: suffix of the output directory (for runs under different SEC_* settings).
 set -o pipefail
-R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/pmc_shapes; mkdir -p $O; cd $R
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/pmc_shapes${PMC_TAG:-}; mkdir -p $O; cd $R
 export TMPDIR=/tmp
 WL=${*:-c4 c2}
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"

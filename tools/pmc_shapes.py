@@ -33,7 +33,7 @@ def shape(w: str):
 
 
 def kind_of(name: str):
-    if "sec_encode_kernel" in name:
+    if "sec_encode_kernel" in name or "sec_encode_bs" in name or "sec_encode_xb" in name:
         return "encode"
     if "sec_decode_kernel" in name:
         return "decode"
