@@ -15,6 +15,8 @@
 //   dec_early   the same with the two copies stored before the recovered rows
 //   rec         recover-only-shaped: 4 blocks read, 2 rows written (2:1, like enc, but the
 //               reads come from two buffers as in a decode)
+//   c4_*        C4-shaped encode traffic (8192 x 64 KiB, 10 blocks of 6554 B read, 4 written),
+//               printed first as its own line; c4_aligned_* with B = 6656 (128 B multiple)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
@@ -114,6 +116,41 @@ __global__ __launch_bounds__(256) void k_dec(const u8 *__restrict__ in, const u8
     }
 }
 
+// C4-shaped (8192 x 64 KiB, k = 10, 4 parity rows of B = 6554 B, blocks back to back so most
+// are unaligned): the product's v_perm tiles (256 lanes, 4 KiB of each block, 2 per chunk,
+// last lane clamped to end at `valid`), every block read, 4 rows written, XOR only.  BB_ = B;
+// L = lanes per tile (tiles per chunk = ceil(valid / (16 L))).
+typedef u32x4 u32x4_u __attribute__((aligned(1)));
+template <u32 BB_, u32 L, u32 PS = BB_>
+__global__ __launch_bounds__(1024) void k_c4(const u8 *__restrict__ in, u8 *__restrict__ par, u32 n)
+{
+    constexpr u32 per = (BB_ + 16 * L - 1) / (16 * L);
+    const u32 valid = n - 9 * BB_;
+    const u32 chunk = blockIdx.x / per;
+    u32 t = (blockIdx.x % per) * 16 * L + threadIdx.x * 16;
+    if (t >= valid + 15)
+        return;
+    t = t + 16 > valid ? valid - 16 : t;
+    const u8 *s = in + (size_t)chunk * n + t;
+    u8 *d = par + (size_t)chunk * 4 * PS + t;
+    u32x4 x[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+        x[j] = __builtin_nontemporal_load((const u32x4_u *)(s + j * BB_));
+    u32x4 a = x[0], b = x[1], c = x[2], e = x[3];
+#pragma unroll
+    for (int j = 4; j < 10; ++j) {
+        a ^= x[j];
+        b ^= x[j] << 1;
+        c ^= x[j] << 2;
+        e ^= x[j] << 3;
+    }
+    __builtin_nontemporal_store(a, (u32x4_u *)d);
+    __builtin_nontemporal_store(b, (u32x4_u *)(d + PS));
+    __builtin_nontemporal_store(c, (u32x4_u *)(d + 2 * PS));
+    __builtin_nontemporal_store(e, (u32x4_u *)(d + 3 * PS));
+}
+
 template <class F>
 double time_ms(F launch)
 {
@@ -167,6 +204,25 @@ int main()
     const double de = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_dec<false, true>), dim3(G / 16384), blk, 0, 0, a, b, c); }));
     const double dee = rate(2.0 * G, time_ms([&] { hipLaunchKernelGGL((k_dec<true, true>), dim3(G / 16384), blk, 0, 0, a, b, c); }));
     const double re = rate(1.5 * G, time_ms([&] { hipLaunchKernelGGL((k_dec<false, false>), dim3(G / 16384), blk, 0, 0, a, b, c); }));
+    // C4-shaped: algorithmic bytes = n read + 4 B written per chunk
+    constexpr u32 NC4 = 8192;
+    auto c4 = [&](auto kern, u32 BBv, u32 L, u32 n) {
+        const u32 per = (BBv + 16 * L - 1) / (16 * L);
+        return rate((double)NC4 * (n + 4.0 * BBv),
+                    time_ms([&] { hipLaunchKernelGGL(kern, dim3(NC4 * per), dim3(L), 0, 0, a, b, n); }));
+    };
+    const double c4_256 = c4(k_c4<6554, 256>, 6554, 256, 65536);
+    const double c4_448 = c4(k_c4<6554, 448>, 6554, 448, 65536);
+    const double c4_64 = c4(k_c4<6554, 64>, 6554, 64, 65536);
+    const double c4a_256 = c4(k_c4<6656, 256>, 6656, 256, 66560);  // B a multiple of 128 (aligned blocks)
+    const double c4a_448 = c4(k_c4<6656, 448>, 6656, 448, 66560);
+    const double c4p_256 = c4(k_c4<6554, 256, 6656>, 6554, 256, 65536);  // parity stride 6656: aligned writes
+    const double c4p_448 = c4(k_c4<6554, 448, 6656>, 6554, 448, 65536);
+    const double c4r_256 = c4(k_c4<6656, 256, 6554>, 6656, 256, 66560);  // aligned reads, unaligned writes
+    printf("{\"c4_lanes256\": %.1f, \"c4_lanes448\": %.1f, \"c4_lanes64\": %.1f, \"c4_aligned_lanes256\": %.1f, "
+           "\"c4_aligned_lanes448\": %.1f, \"c4_pstride6656_lanes256\": %.1f, \"c4_pstride6656_lanes448\": %.1f, "
+           "\"c4_aligned_reads_only_lanes256\": %.1f}\n",
+           c4_256, c4_448, c4_64, c4a_256, c4a_448, c4p_256, c4p_448, c4r_256);
     printf("{\"unit\": \"GB/s\", \"read_U1\": %.1f, \"read_U4\": %.1f, \"write_U1\": %.1f, \"write_U4\": %.1f, "
            "\"copy_U1\": %.1f, \"copy_U2\": %.1f, \"copy_U4\": %.1f, \"enc\": %.1f, \"dec\": %.1f, \"dec_early\": %.1f, "
            "\"rec\": %.1f, \"copy_lanes64\": %.1f, \"copy_lanes128\": %.1f, \"copy_lanes512\": %.1f, "
