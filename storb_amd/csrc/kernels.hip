@@ -296,6 +296,18 @@ constexpr u32 lds_tab_bytes(u32 lanes) { return lds_tab<R, DEC>() ? lanes / 64 *
 #ifndef SEC_FIXED_K
 #define SEC_FIXED_K 0
 #endif
+//   SEC_DEC_WAVES / SEC_ENC_WAVES  A/B: minimum waves per SIMD the compiler must leave room
+//                               for (amdgpu_waves_per_eu, i.e. a VGPR cap) on the tile kernels
+#if defined(SEC_DEC_WAVES) && SEC_DEC_WAVES > 0
+#define SEC_DEC_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SEC_DEC_WAVES)))
+#else
+#define SEC_DEC_WAVES_ATTR
+#endif
+#if defined(SEC_ENC_WAVES) && SEC_ENC_WAVES > 0
+#define SEC_ENC_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SEC_ENC_WAVES)))
+#else
+#define SEC_ENC_WAVES_ATTR
+#endif
 // Blocks (slots) per batch of a tile kernel: KB * U = the batch's 16 B vectors per lane
 template <int U, bool W, bool DEC>
 constexpr int batch_blocks()
@@ -347,7 +359,7 @@ __device__ __forceinline__ void encode_ragged(const u8 *__restrict__ in, u8 *__r
                                            const sec::Tile &tl, const u32 *__restrict__ tabs);
 
 template <int R, int U, bool W>
-__global__ __launch_bounds__(sec::max_lanes(R, U)) void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+__global__ __launch_bounds__(sec::max_lanes(R, U)) SEC_ENC_WAVES_ATTR void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
                                                          const sec::EncDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
                                                          const u32 *__restrict__ tabs)
@@ -520,7 +532,7 @@ __device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 
                                            const sec::DecSlots sl);
 
 template <int R, int U, bool W>
-__global__ __launch_bounds__(sec::max_lanes(R, U)) void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+__global__ __launch_bounds__(sec::max_lanes(R, U)) SEC_DEC_WAVES_ATTR void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                          const sec::DecDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
                                                          const u32 *__restrict__ tabs,
