@@ -101,9 +101,18 @@ __device__ __forceinline__ void transpose8(u32 (&x)[8])
     swap_bits<1, 0x55555555u>(x[6], x[7]);
 }
 
+// SEC_BS_NT_LOAD (build knob, A/B): 1 = nontemporal (streaming) block loads, 0 = cached loads
+// (the second row group of an interleaved launch re-reads the blocks from L2)
+#ifndef SEC_BS_NT_LOAD
+#define SEC_BS_NT_LOAD 1
+#endif
 __device__ __forceinline__ u32x4 ld16(const u8 *p)
 {
+#if SEC_BS_NT_LOAD
     return __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(p));
+#else
+    return *reinterpret_cast<const u32x4_u *>(p);
+#endif
 }
 
 // 16 bytes at base + off of which the first `avail - off` exist; the rest read as zero
