@@ -101,25 +101,28 @@ __device__ __forceinline__ void transpose8(u32 (&x)[8])
     swap_bits<1, 0x55555555u>(x[6], x[7]);
 }
 
-// SEC_BS_NT_LOAD (build knob, A/B): 1 = nontemporal (streaming) block loads, 0 = cached loads
-// (the second row group of an interleaved launch re-reads the blocks from L2)
+// Block loads: nontemporal (streaming) in the one-group kernels, where every byte is read
+// once; cached in the interleaved two-group kernel, whose second group reads the blocks again
+// from L2 (measured: (64,96) +5-8 % cached, (16,24) -5 %, (32,48) even; r02_bs_ab.jsonl run 4).
+// SEC_BS_NT_LOAD (build knob, A/B): 0 = cached loads everywhere.
 #ifndef SEC_BS_NT_LOAD
 #define SEC_BS_NT_LOAD 1
 #endif
+template <bool NT>
 __device__ __forceinline__ u32x4 ld16(const u8 *p)
 {
-#if SEC_BS_NT_LOAD
-    return __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(p));
-#else
-    return *reinterpret_cast<const u32x4_u *>(p);
-#endif
+    if constexpr (NT && SEC_BS_NT_LOAD)
+        return __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(p));
+    else
+        return *reinterpret_cast<const u32x4_u *>(p);
 }
 
 // 16 bytes at base + off of which the first `avail - off` exist; the rest read as zero
+template <bool NT>
 __device__ __forceinline__ u32x4 ld16_avail(const u8 *base, u32 off, u32 avail)
 {
     if (off + 16 <= avail)
-        return ld16(base + off);
+        return ld16<NT>(base + off);
     u32 w[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int b = 0; b < 16; ++b)
@@ -186,15 +189,16 @@ __device__ __forceinline__ void block_rows(std::integer_sequence<int, Q...>, u32
 }
 
 // the lane's two 16-byte pieces of a block: at pa and pb
+template <bool NT>
 __device__ __forceinline__ void load_block(u32 (&x)[8], const u8 *blk, u32 pa, u32 pb, u32 avail, bool last)
 {
     u32x4 a, b;
     if (!last) {
-        a = ld16(blk + pa);
-        b = ld16(blk + pb);
+        a = ld16<NT>(blk + pa);
+        b = ld16<NT>(blk + pb);
     } else {
-        a = ld16_avail(blk, pa, avail);
-        b = ld16_avail(blk, pb, avail);
+        a = ld16_avail<NT>(blk, pa, avail);
+        b = ld16_avail<NT>(blk, pb, avail);
     }
     x[0] = a.x;
     x[1] = a.y;
@@ -206,7 +210,7 @@ __device__ __forceinline__ void load_block(u32 (&x)[8], const u8 *blk, u32 pa, u
     x[7] = b.w;
 }
 
-template <int K, int M, int R0, int NR, int D, int J>
+template <int K, int M, int R0, int NR, int D, bool NT, int J>
 __device__ __forceinline__ void one_block(u32 (&acc)[NR * 8], u32 (&ring)[D][8], const u8 *src, u64 B, u32 pa,
                                           u32 pb, u32 valid)
 {
@@ -215,7 +219,7 @@ __device__ __forceinline__ void one_block(u32 (&acc)[NR * 8], u32 (&ring)[D][8],
     for (int i = 0; i < 8; ++i)
         x[i] = ring[J % D][i];
     if constexpr (J + D < K)
-        load_block(ring[J % D], src + (u64)(J + D) * B, pa, pb, valid, J + D == K - 1);
+        load_block<NT>(ring[J % D], src + (u64)(J + D) * B, pa, pb, valid, J + D == K - 1);
     transpose8(x);
     u32 lo[16], hi[16];
     subsets(x[0], x[1], x[2], x[3], lo);
@@ -223,15 +227,22 @@ __device__ __forceinline__ void one_block(u32 (&acc)[NR * 8], u32 (&ring)[D][8],
     block_rows<K, M, R0, J, J == 0>(std::make_integer_sequence<int, NR * 8>{}, acc, lo, hi);
 }
 
-template <int K, int M, int R0, int NR, int D, int... Js>
+template <int K, int M, int R0, int NR, int D, bool NT, int... Js>
 __device__ __forceinline__ void all_blocks(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], u32 (&ring)[D][8],
                                            const u8 *src, u64 B, u32 pa, u32 pb, u32 valid)
 {
-    (one_block<K, M, R0, NR, D, Js>(acc, ring, src, B, pa, pb, valid), ...);
+    (one_block<K, M, R0, NR, D, NT, Js>(acc, ring, src, B, pa, pb, valid), ...);
 }
 
+// SEC_BS_WAVES (build knob, A/B): minimum waves per SIMD (amdgpu_waves_per_eu, a VGPR cap)
+#if defined(SEC_BS_WAVES) && SEC_BS_WAVES > 0
+#define SEC_BS_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SEC_BS_WAVES)))
+#else
+#define SEC_BS_WAVES_ATTR
+#endif
+
 // One wave's span of one tile: rows [R0, R0 + NR) of the chunk's parity over the lane's pieces.
-template <int K, int M, int R0, int NR, int D>
+template <int K, int M, int R0, int NR, int D, bool NT>
 __device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d, u32 s)
 {
     static_assert(D >= 1 && D <= K, "ring depth");
@@ -245,9 +256,9 @@ __device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restric
     u32 ring[D][8];
 #pragma unroll
     for (int j = 0; j < D; ++j)
-        load_block(ring[j], src + (u64)j * B, pa, pb, d.valid, j == K - 1);
+        load_block<NT>(ring[j], src + (u64)j * B, pa, pb, d.valid, j == K - 1);
     u32 acc[NR * 8];
-    all_blocks<K, M, R0, NR, D>(std::make_integer_sequence<int, K>{}, acc, ring, src, B, pa, pb, d.valid);
+    all_blocks<K, M, R0, NR, D, NT>(std::make_integer_sequence<int, K>{}, acc, ring, src, B, pa, pb, d.valid);
 
     u8 *dst = par + d.par_off;
 #pragma unroll
@@ -265,7 +276,7 @@ __device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restric
 
 // Rows [R0, R0 + NR) of every tile.
 template <int K, int M, int R0, int NR, int D>
-__global__ __launch_bounds__(256) void sec_encode_bs_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+__global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
                                                             const sec::EncDesc *__restrict__ descs,
                                                             const sec::Tile *__restrict__ tiles)
 {
@@ -274,7 +285,7 @@ __global__ __launch_bounds__(256) void sec_encode_bs_kernel(const u8 *__restrict
     const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
     if (s >= d.B)
         return;
-    bs_span<K, M, R0, NR, D>(in, par, d, s);
+    bs_span<K, M, R0, NR, D, true>(in, par, d, s);
 }
 
 // Two row groups in one launch, the tile's r0 picking one: the plan puts a run of 8 tiles of
@@ -282,7 +293,7 @@ __global__ __launch_bounds__(256) void sec_encode_bs_kernel(const u8 *__restrict
 // XCD (workgroup b runs on XCD b % 8) at about the same time and the second reads the blocks
 // from that XCD's L2 instead of HBM.
 template <int K, int M, int NR, int D>
-__global__ __launch_bounds__(256) void sec_encode_bs2_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+__global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs2_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
                                                              const sec::EncDesc *__restrict__ descs,
                                                              const sec::Tile *__restrict__ tiles)
 {
@@ -292,9 +303,9 @@ __global__ __launch_bounds__(256) void sec_encode_bs2_kernel(const u8 *__restric
     if (s >= d.B)
         return;
     if (tl.r0 == 0)
-        bs_span<K, M, 0, NR, D>(in, par, d, s);
+        bs_span<K, M, 0, NR, D, false>(in, par, d, s);
     else
-        bs_span<K, M, NR, NR, D>(in, par, d, s);
+        bs_span<K, M, NR, NR, D, false>(in, par, d, s);
 }
 
 template <int K, int M, int R0, int NR, int D>

@@ -72,6 +72,7 @@ VARIANTS = {
     "bsr8": {"SEC_BS_RING": 8},
     "bsr10": {"SEC_BS_RING": 10},
     "bsld": {"SEC_BS_NT_LOAD": 0},  # bit-sliced encode with cached (not streaming) loads
+    "bsw3": {"SEC_BS_WAVES": 3},  # bit-sliced encode capped for 3 waves per SIMD
     # VGPR caps through amdgpu_waves_per_eu on the tile kernels (decode<2,1> is 104 VGPRs = 4
     # waves per SIMD, encode<4,1> 109)
     "dw5": {"SEC_DEC_WAVES": 5},
