@@ -447,7 +447,9 @@ def main_c4(args):
                        "parallelism": f"chunk-partition x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(enc_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(enc_gbs / PEAK_HBM_GBS, 4), "traffic": None,
-                         "kernel": "sec_encode_kernel<4, 1, false>", "algorithmic_bytes_per_launch": enc_alg,
+                         "kernel": ("sec_encode_kernel<4, 1, false>" if os.environ.get("SEC_BS") == "0"
+                                    else "sec_encode_bs_kernel<10, 14, 0, 4, 5>"),  # api.cpp bs_shape
+                         "algorithmic_bytes_per_launch": enc_alg,
                          "avg_launch_ms": round(r["enc_avg_s"] * 1e3, 4), "launches": r["enc_launches"]},
             "decode_kernel": {"achieved": round(dec_alg / r["dec_avg_s"] / 1e9, 1), "unit": "GB/s",
                               "erased": list(C4_ERASED), "block_9": "read in place, avail = B - padlen",

@@ -385,8 +385,11 @@ int bs_shape(int k, int m, uint64_t B)
         return -1;
     if (B < 16 || B > 0xFFFFFFFFull - 8192)
         return -1;
+    // Default: the shapes with >= 8 parity rows, where the v_perm rows are VALU-bound (1.3-1.7x
+    // here), and C4's RS(10,4) (+0-4 %, whole 65536-chunk job +2 %); the other p <= 4 shapes
+    // measured 5-10 % slower here (C5's RS(8,3), zfec(8,12) on 4 MiB chunks; r02_bs_ab.jsonl)
     const int p = m - k;
-    if (!(e && e[0] == '1') && p < 8)  // p <= 4: the v_perm kernel is HBM-bound and as fast or faster
+    if (!(e && e[0] == '1') && p < 8 && !(k == 10 && m == 14))
         return -1;
     if (k == 32 && m == 48 && env_size("SEC_BS_R8", 0))
         return sec_bs_shape(k, m, 8);
