@@ -238,6 +238,23 @@ using Bins = std::map<std::tuple<int, int, int, int, int>, std::vector<sec::Tile
 
 uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 
+// Decodes that copy nothing (recover-only, and the copy-free host-join calls) of chunks with
+// k <= 4 run a kernel variant whose load batch is 4 slots instead of 16: 57 instead of 104
+// VGPRs, 8 waves per SIMD instead of 4.  Measured on C3 recover-only (tools/sweep.py
+// --recover, env held during the timed calls): 6.42 against 5.91 TB/s; the same batches cost
+// the reassembling decode 4 %, and 8-slot batches for k <= 8 measured 1.4 % slower on RS(8,3)
+// recover-only (profiles/r02_dec_small_kb_ab.jsonl).  SEC_DEC_REC_KB=0 turns it off, =8 adds
+// the 8-slot variant for 4 < k <= 8 (A/B); read per plan build.
+int dec_small_kb(int k)
+{
+    const char *e = getenv("SEC_DEC_REC_KB");
+    if (e && e[0] == '0')
+        return 0;
+    if (k <= 4)
+        return 4;
+    return e && e[0] == '8' && k <= 8 ? 8 : 0;
+}
+
 // Work for one chunk.  `valid` = positions where every block is fully readable and
 // every output row writable (the last data block's length, clamped to [0, B]).
 // Tiles of 256 lanes x 4 KiB * U cover [0, valid); the ragged rest (and small chunks
@@ -248,7 +265,7 @@ uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 // byte launch cost C4 13-17 % on top of its main kernels (profiles/r01_c4_kernel_stats).
 // Chunks with valid < 16 get no tile: all of [0, B) becomes one-thread tail items.
 void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B, int64_t valid,
-              int rows_total, int k, bool decode, uint64_t start = 0, bool narrow = false)
+              int rows_total, int k, bool decode, uint64_t start = 0, bool narrow = false, int small_kb = 0)
 {
     if (B == 0)
         return;
@@ -272,7 +289,9 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
         const int wide = is_wide(k, U, rows);  // U == 1 then (pick_u)
         const int flanes = U == 1 ? std::min(full_lanes(decode, narrow), sec::max_lanes(rows, 1)) : sec::kLanes;
         const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * U;
-        auto &full = bins[{0, rows, U, flanes, wide}];
+        // kind: 0, or the small-batch decode variant's batch (the group's kernel, see dec_small_kb)
+        const int kind = small_kb && U == 1 && !wide && k <= small_kb ? small_kb : 0;
+        auto &full = bins[{kind, rows, U, flanes, wide}];
         sec::Tile *last = nullptr;
         if (!exact) {
             // every U = 1 tile is flanes wide, the chunk's last one with idle lanes past
@@ -286,7 +305,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
                 last = &full.back();
             }
             const int ul = std::min(full_lanes(decode, narrow), sec::max_lanes(rows, 1));
-            auto &ones = bins[{0, rows, 1, ul, is_wide(k, 1, rows)}];
+            auto &ones = bins[{kind, rows, 1, ul, is_wide(k, 1, rows)}];
             for (uint64_t t0 = from + nfull * step; t0 < v; t0 += (uint64_t)sec::kLaneBytes * ul) {  // U > 1 remainder
                 ones.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
                 last = &ones.back();
@@ -1076,7 +1095,8 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             sp.in_bytes += (uint64_t)c.k * c.B;
             sp.out_bytes += nout;
             if (nout > 0 && !(nocopy && e_of[i] == 0))
-                add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true);
+                add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true, 0, false,
+                         recover || nocopy ? dec_small_kb(c.k) : 0);
         }
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles, true);
@@ -1105,7 +1125,8 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::DecSlots sl{plan.meta.as<uint64_t>(sp.off_soff), plan.meta.as<uint32_t>(sp.off_srow),
                            plan.meta.as<uint32_t>(sp.off_mrow), plan.meta.as<uint32_t>(sp.off_savail)};
     for (const Group &g : sp.groups) {
-        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, blocks, out, dd, dt + g.first, g.count, tabs, sl, s);
+        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, blocks, out, dd, dt + g.first, g.count, tabs, sl, s,
+                                  g.mfma);  // decode groups: the bin kind is the small-batch variant (or 0)
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_kernel");
     }

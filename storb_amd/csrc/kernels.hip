@@ -522,7 +522,7 @@ __global__ __launch_bounds__(256) void sec_encode_tail(const u8 *__restrict__ in
 // which reads a slot's bytes past its avail as zero (zfec's padded block k-1 read in place).
 // Recover-only decodes (SEC_F_RECOVER) use the same kernels: no copies (row = none) and the
 // recovered rows go to output rows 0..e-1.
-template <int R, int U, bool W>
+template <int R, int U, bool W, int KBX>
 __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                             const sec::DecDesc &d, const sec::Tile &tl, u32 t,
                                             const u32 *__restrict__ tabs, const sec::DecSlots sl);
@@ -531,7 +531,9 @@ __device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 
                                            const sec::Tile &tl, const u32 *__restrict__ tabs,
                                            const sec::DecSlots sl);
 
-template <int R, int U, bool W>
+// KBX > 0: slots per load batch fixed at KBX (the plan sends only chunks with k <= KBX; fewer
+// live registers, more waves): recover-only and copy-free decodes, see api.cpp dec_small_kb
+template <int R, int U, bool W, int KBX>
 __global__ __launch_bounds__(sec::max_lanes(R, U)) SEC_DEC_WAVES_ATTR void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                          const sec::DecDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
@@ -542,7 +544,7 @@ __global__ __launch_bounds__(sec::max_lanes(R, U)) SEC_DEC_WAVES_ATTR void sec_d
     const sec::DecDesc d = descs[tl.chunk];
     const u32 t = tl.t0 + threadIdx.x * sec::kLaneBytes;
     if (t < d.valid)
-        decode_main<R, U, W>(blocks, out, d, tl, t, tabs, sl);
+        decode_main<R, U, W, KBX>(blocks, out, d, tl, t, tabs, sl);
     if (tl.ntail)
         decode_ragged<R>(blocks, out, d, tl, tabs, sl);
 }
@@ -588,7 +590,7 @@ __device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 
     }
 }
 
-template <int R, int U, bool W>
+template <int R, int U, bool W, int KBX>
 __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                             const sec::DecDesc &d, const sec::Tile &tl, u32 t,
                                             const u32 *__restrict__ tabs,
@@ -615,7 +617,7 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
     // Slots go in batches of KB, as in encode_main: every load of a batch before any store
     // or arithmetic, then the batch in order — each present primary copied to its output
     // row, every slot fed to the R accumulators.  C2 / C4 are one batch (all loads in flight).
-    constexpr int KB = batch_blocks<U, W, true>();
+    constexpr int KB = KBX > 0 ? KBX : batch_blocks<U, W, true>();
     auto batch = [&](u32 c0) {
         constexpr bool LT = lds_tab<R, true>();
         const u32x2 *vt = wave_tabs<KB, R, LT>(tj, tstep, c0, k);
@@ -1108,12 +1110,13 @@ hipError_t launch_enc(const u8 *in, u8 *par, const sec::EncDesc *descs, const se
                       lds_tab_bytes<batch_blocks<U, W, false>(), R, false>(lanes), s, in, par, descs, tiles, tabs);
 }
 
-template <int R, int U, bool W>
+template <int R, int U, bool W, int KBX>
 hipError_t launch_dec(const u8 *blocks, u8 *out, const sec::DecDesc *descs, const sec::Tile *tiles, u32 ntiles,
                       const u32 *tabs, sec::DecSlots sl, u32 lanes, hipStream_t s)
 {
-    return launch_shm(sec_decode_kernel<R, U, W>, dim3(ntiles), dim3(lanes),
-                      lds_tab_bytes<batch_blocks<U, W, true>(), R, true>(lanes), s, blocks, out, descs, tiles, tabs, sl);
+    constexpr int KB = KBX > 0 ? KBX : batch_blocks<U, W, true>();
+    return launch_shm(sec_decode_kernel<R, U, W, KBX>, dim3(ntiles), dim3(lanes), lds_tab_bytes<KB, R, true>(lanes),
+                      s, blocks, out, descs, tiles, tabs, sl);
 }
 
 template <int U, bool W>
@@ -1133,20 +1136,20 @@ hipError_t dispatch_enc(int rows, const u8 *in, u8 *par, const sec::EncDesc *d, 
     }
 }
 
-template <int U, bool W>
+template <int U, bool W, int KBX = 0>
 hipError_t dispatch_dec(int rows, const u8 *b, u8 *o, const sec::DecDesc *d, const sec::Tile *t, u32 nt,
                         const u32 *tabs, sec::DecSlots sl, u32 lanes, hipStream_t s)
 {
     switch (rows) {
-    case 0: return launch_dec<0, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
-    case 1: return launch_dec<1, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
-    case 2: return launch_dec<2, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
-    case 3: return launch_dec<3, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
-    case 4: return launch_dec<4, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
-    case 5: return launch_dec<5, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
-    case 6: return launch_dec<6, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
-    case 7: return launch_dec<7, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
-    case 8: return launch_dec<8, U, W>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 0: return launch_dec<0, U, W, KBX>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 1: return launch_dec<1, U, W, KBX>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 2: return launch_dec<2, U, W, KBX>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 3: return launch_dec<3, U, W, KBX>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 4: return launch_dec<4, U, W, KBX>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 5: return launch_dec<5, U, W, KBX>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 6: return launch_dec<6, U, W, KBX>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 7: return launch_dec<7, U, W, KBX>(b, o, d, t, nt, tabs, sl, lanes, s);
+    case 8: return launch_dec<8, U, W, KBX>(b, o, d, t, nt, tabs, sl, lanes, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -1207,7 +1210,7 @@ int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *
 
 int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,
                       const sec::DecDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
-                      sec::DecSlots sl, void *stream)
+                      sec::DecSlots sl, void *stream, int kb)
 {
     if (ntiles == 0)
         return hipSuccess;
@@ -1215,6 +1218,15 @@ int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *block
         return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
     const u32 L = (u32)lanes;
+    if (kb) {  // small load batches: U = 1 tiles of chunks with k <= kb only
+        if (U != 1 || wide)
+            return hipErrorInvalidValue;
+        if (kb == 4)
+            return dispatch_dec<1, false, 4>(rows, blocks, out, descs, tiles, ntiles, tabs, sl, L, s);
+        if (kb == 8)
+            return dispatch_dec<1, false, 8>(rows, blocks, out, descs, tiles, ntiles, tabs, sl, L, s);
+        return hipErrorInvalidValue;
+    }
     if (wide)
         return dispatch_dec<1, true>(rows, blocks, out, descs, tiles, ntiles, tabs, sl, L, s);
     switch (U) {

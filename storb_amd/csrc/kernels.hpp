@@ -135,9 +135,11 @@ int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uin
                          const sec::Tile *t, uint32_t ntiles, void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
                            uint32_t nitems, const uint32_t *tabs, void *stream);
+// kb (4 or 8): the kernel variant whose load batch is kb slots (every chunk of the group has
+// k <= kb; U = 1, not wide); 0: the default batch
 int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,
                       const sec::DecDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
-                      sec::DecSlots slots, void *stream);
+                      sec::DecSlots slots, void *stream, int kb = 0);
 // split: sec_sha1_split_kernel (two waves per 64 messages: schedule and rounds) instead of
 // one lane per message
 int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDesc *msgs, uint32_t nmsgs,

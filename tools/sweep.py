@@ -176,9 +176,22 @@ def main():
             os.environ.pop(env.split("=")[0])
     os.environ.pop("SEC_TILE_U", None)
     samples = {c: ([], [], []) for c in configs}
+    def set_env(v, on):
+        # a config's ENV=VALUE stays set while its calls run: a ctx caches one plan per kind, so
+        # a workload that alternates decode modes rebuilds plans inside the timed loop, and those
+        # rebuilds must see the config's knobs too
+        env = v[0].partition("@")[2]
+        if env:
+            if on:
+                os.environ[env.split("=")[0]] = env.split("=")[1]
+            else:
+                os.environ.pop(env.split("=")[0], None)
+
     for _ in range(a.rounds):
         for c in configs:
             e = engines[c]
+            set_env(c, True)
+            os.environ["SEC_TILE_U"] = str(c[1])
             e.set_timing(True)
             for _ in range(a.reps):
                 e.encode_batch(ed, src, par, asynchronous=True)
@@ -198,6 +211,8 @@ def main():
                 e.set_timing(False)
                 ms, nl = e.collect_timing("decode")
                 samples[c][2].append(ms / nl)
+            set_env(c, False)
+    os.environ.pop("SEC_TILE_U", None)
     # the timed calls must have produced the same bytes (a fast wrong kernel is not a result)
     ref_par = par.clone()
     engines[configs[0]].encode_batch(ed, src, ref_par, asynchronous=True)
