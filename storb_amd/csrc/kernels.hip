@@ -1110,13 +1110,18 @@ hipError_t launch_enc(const u8 *in, u8 *par, const sec::EncDesc *descs, const se
                       lds_tab_bytes<batch_blocks<U, W, false>(), R, false>(lanes), s, in, par, descs, tiles, tabs);
 }
 
+// SEC_DEC_LDS_PAD (build knob, A/B): extra dynamic LDS bytes per decode workgroup, which caps
+// the workgroups a CU holds (160 KiB / pad) and so the waves per SIMD
+#ifndef SEC_DEC_LDS_PAD
+#define SEC_DEC_LDS_PAD 0
+#endif
 template <int R, int U, bool W, int KBX>
 hipError_t launch_dec(const u8 *blocks, u8 *out, const sec::DecDesc *descs, const sec::Tile *tiles, u32 ntiles,
                       const u32 *tabs, sec::DecSlots sl, u32 lanes, hipStream_t s)
 {
     constexpr int KB = KBX > 0 ? KBX : batch_blocks<U, W, true>();
-    return launch_shm(sec_decode_kernel<R, U, W, KBX>, dim3(ntiles), dim3(lanes), lds_tab_bytes<KB, R, true>(lanes),
-                      s, blocks, out, descs, tiles, tabs, sl);
+    return launch_shm(sec_decode_kernel<R, U, W, KBX>, dim3(ntiles), dim3(lanes),
+                      lds_tab_bytes<KB, R, true>(lanes) + SEC_DEC_LDS_PAD, s, blocks, out, descs, tiles, tabs, sl);
 }
 
 template <int U, bool W>

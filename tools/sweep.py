@@ -73,6 +73,9 @@ VARIANTS = {
     "bsr10": {"SEC_BS_RING": 10},
     "bsld": {"SEC_BS_NT_LOAD": 0},  # bit-sliced encode with cached (not streaming) loads
     "bsw3": {"SEC_BS_WAVES": 3},  # bit-sliced encode capped for 3 waves per SIMD
+    # decode workgroups per CU capped through padding LDS (160 KiB per CU): 3 or 2 per CU
+    "dpad3": {"SEC_DEC_LDS_PAD": 50000},
+    "dpad2": {"SEC_DEC_LDS_PAD": 60000},
     # VGPR caps through amdgpu_waves_per_eu on the tile kernels (decode<2,1> is 104 VGPRs = 4
     # waves per SIMD, encode<4,1> 109)
     "dw5": {"SEC_DEC_WAVES": 5},
