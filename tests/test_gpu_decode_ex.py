@@ -124,8 +124,16 @@ def _oracle_recovered(data, k, m, keep):
     return b"".join(blocks[s] for s in range(k) if s not in keep)
 
 
-@pytest.mark.parametrize("k,m", [(2, 3), (4, 6), (8, 11), (10, 14), (16, 24), (16, 40), (32, 48)])
-def test_recover_only_vs_oracle_device(engine, k, m):
+@pytest.mark.parametrize("kb", ["default", "0", "8"])
+@pytest.mark.parametrize("k,m", [(1, 2), (2, 3), (3, 5), (4, 6), (5, 7), (8, 11), (10, 14), (16, 24), (16, 40), (32, 48)])
+def test_recover_only_vs_oracle_device(k, m, kb, monkeypatch):
+    """kb: the copy-free decodes' small-batch kernel variants (api.cpp dec_small_kb): default
+    (4-slot batches for k <= 4), "0" (off: 16-slot batches), "8" (also 8-slot for k <= 8)."""
+    from storb_amd.engine import Engine
+
+    if kb != "default":
+        monkeypatch.setenv("SEC_DEC_REC_KB", kb)
+    engine = Engine(0)  # its own plan cache: the knob is read when a plan is built
     rng = random.Random(1000 + k * m)
     sizes = [n for n in (k * k, 4096 * k - 3, 65536, 65536 + 9, 6554 * k - 1, 300007)
              if -(-n // k) * (k - 1) <= n]
@@ -147,6 +155,7 @@ def test_recover_only_vs_oracle_device(engine, k, m):
     want = b"".join(_oracle_recovered(h, k, m, kp) for h, kp in zip(host, keeps))
     assert len(want) == total
     assert out.cpu().numpy()[:total].tobytes() == want
+    engine.close()
 
 
 def test_recover_only_c3_full_size(engine):
