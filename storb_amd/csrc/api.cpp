@@ -255,6 +255,14 @@ int dec_small_kb(int k)
     return e && e[0] == '8' && k <= 8 ? 8 : 0;
 }
 
+// A/B only: SEC_DEC_COPY_KB = 4 or 8 runs the reassembling (copying) decodes of chunks with
+// k <= that through the small-batch variant too (default off: 4-slot batches measured -4 %)
+int dec_copy_kb(int k)
+{
+    const size_t v = env_size("SEC_DEC_COPY_KB", 0);
+    return (v == 4 || v == 8) && (size_t)k <= v ? (int)v : 0;
+}
+
 // Work for one chunk.  `valid` = positions where every block is fully readable and
 // every output row writable (the last data block's length, clamped to [0, B]).
 // Tiles of 256 lanes x 4 KiB * U cover [0, valid); the ragged rest (and small chunks
@@ -1096,7 +1104,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             sp.out_bytes += nout;
             if (nout > 0 && !(nocopy && e_of[i] == 0))
                 add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true, 0, false,
-                         recover || nocopy ? dec_small_kb(c.k) : 0);
+                         recover || nocopy ? dec_small_kb(c.k) : dec_copy_kb(c.k));
         }
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles, true);
