@@ -16,7 +16,8 @@
 //   rec         recover-only-shaped: 4 blocks read, 2 rows written (2:1, like enc, but the
 //               reads come from two buffers as in a decode)
 //   c4_*        C4-shaped encode traffic (8192 x 64 KiB, 10 blocks of 6554 B read, 4 written),
-//               printed first as its own line; c4_aligned_* with B = 6656 (128 B multiple)
+//               printed as its own line; c4_aligned_* with B = 6656 (128 B multiple);
+//               c4_decode_*: C4 reassembly-shaped (10 slots read, the 64 KiB chunk written)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
@@ -151,6 +152,48 @@ __global__ __launch_bounds__(1024) void k_c4(const u8 *__restrict__ in, u8 *__re
     __builtin_nontemporal_store(e, (u32x4_u *)(d + 3 * PS));
 }
 
+// C4-decode-shaped: slots = data blocks {1,3,4,6,8,9} of the chunk (block 9 short: reads clamp
+// to `valid`) and parity rows 0..3; all 10 output rows of the reassembled 64 KiB written (the
+// 6 copies and 4 "recovered" rows, XOR only), 256-lane tiles of 4 KiB as the product's
+template <u32 L>
+__global__ __launch_bounds__(1024) void k_c4dec(const u8 *__restrict__ in, const u8 *__restrict__ par,
+                                                u8 *__restrict__ out, u32 n)
+{
+    constexpr u32 BB_ = 6554, per = (BB_ + 16 * L - 1) / (16 * L);
+    const u32 valid = n - 9 * BB_;
+    const u32 chunk = blockIdx.x / per;
+    u32 t = (blockIdx.x % per) * 16 * L + threadIdx.x * 16;
+    if (t >= valid + 15)
+        return;
+    t = t + 16 > valid ? valid - 16 : t;
+    const u8 *s = in + (size_t)chunk * n + t;
+    const u8 *p = par + (size_t)chunk * 4 * BB_ + t;
+    u8 *o = out + (size_t)chunk * n + t;
+    constexpr int keep[6] = {1, 3, 4, 6, 8, 9};
+    u32x4 x[10];
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+        x[j] = __builtin_nontemporal_load((const u32x4_u *)(s + keep[j] * BB_));
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        x[6 + r] = __builtin_nontemporal_load((const u32x4_u *)(p + r * BB_));
+    u32x4 a = x[6], b = x[7], c = x[8], e = x[9];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        a ^= x[j];
+        b ^= x[j] << 1;
+        c ^= x[j] << 2;
+        e ^= x[j] << 3;
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+        __builtin_nontemporal_store(x[j], (u32x4_u *)(o + keep[j] * BB_));
+    __builtin_nontemporal_store(a, (u32x4_u *)(o + 0 * BB_));
+    __builtin_nontemporal_store(b, (u32x4_u *)(o + 2 * BB_));
+    __builtin_nontemporal_store(c, (u32x4_u *)(o + 5 * BB_));
+    __builtin_nontemporal_store(e, (u32x4_u *)(o + 7 * BB_));
+}
+
 template <class F>
 double time_ms(F launch)
 {
@@ -219,6 +262,15 @@ int main()
     const double c4p_256 = c4(k_c4<6554, 256, 6656>, 6554, 256, 65536);  // parity stride 6656: aligned writes
     const double c4p_448 = c4(k_c4<6554, 448, 6656>, 6554, 448, 65536);
     const double c4r_256 = c4(k_c4<6656, 256, 6554>, 6656, 256, 66560);  // aligned reads, unaligned writes
+    // C4 decode-shaped: 10 slots of B read + n written per chunk (the product's algorithmic bytes)
+    auto c4d = [&](auto kern, u32 L) {
+        const u32 per = (6554 + 16 * L - 1) / (16 * L);
+        return rate((double)NC4 * (10.0 * 6554 + 65536),
+                    time_ms([&] { hipLaunchKernelGGL(kern, dim3(NC4 * per), dim3(L), 0, 0, a, b, c, 65536u); }));
+    };
+    const double c4d_256 = c4d(k_c4dec<256>, 256);
+    const double c4d_448 = c4d(k_c4dec<448>, 448);
+    printf("{\"c4_decode_lanes256\": %.1f, \"c4_decode_lanes448\": %.1f}\n", c4d_256, c4d_448);
     printf("{\"c4_lanes256\": %.1f, \"c4_lanes448\": %.1f, \"c4_lanes64\": %.1f, \"c4_aligned_lanes256\": %.1f, "
            "\"c4_aligned_lanes448\": %.1f, \"c4_pstride6656_lanes256\": %.1f, \"c4_pstride6656_lanes448\": %.1f, "
            "\"c4_aligned_reads_only_lanes256\": %.1f}\n",
