@@ -323,8 +323,10 @@ hipError_t launch_bs(int lanes, const u8 *in, u8 *par, const sec::EncDesc *d, co
     return hipGetLastError();
 }
 
-// Shapes: (k, m, rows per launch).  Ring depths from the register budget: 8 NR accumulators
-// + 8 D ring dwords per lane; SEC_BS_RING (build knob, A/B) sets one depth for every shape.
+// Shapes: (k, m, rows per launch).  Ring depths from the register budget (8 NR accumulators
+// + 8 D ring dwords per lane) and A/Bs: zfec(16,24) keeps 10 of its 16 blocks in flight
+// (182 VGPRs; +2-8 % over 4 on 1 and 16 MiB chunks), C4 5 (10: -2 %), the 16-row groups 2;
+// SEC_BS_RING (build knob, A/B) sets one depth for every shape.
 #ifdef SEC_BS_RING
 #define RING_K(k, d) (SEC_BS_RING < (k) ? SEC_BS_RING : (k))
 #else
@@ -365,7 +367,7 @@ int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uin
     switch (shape * 4 + group + 1) {
     case 1: return launch_bs<10, 14, 0, 4, RING_K(10, 5)>(lanes, in, par, descs, t, ntiles, s);
     case 5: return launch_bs<8, 12, 0, 4, RING_K(8, 4)>(lanes, in, par, descs, t, ntiles, s);
-    case 9: return launch_bs<16, 24, 0, 8, RING_K(16, 4)>(lanes, in, par, descs, t, ntiles, s);
+    case 9: return launch_bs<16, 24, 0, 8, RING_K(16, 10)>(lanes, in, par, descs, t, ntiles, s);
     case 13: return launch_bs<32, 48, 0, 16, RING_K(32, 2)>(lanes, in, par, descs, t, ntiles, s);
     case 16: return launch_bs<64, 96, -1, 16, RING_K(64, 2)>(lanes, in, par, descs, t, ntiles, s);
     case 17: return launch_bs<64, 96, 0, 16, RING_K(64, 2)>(lanes, in, par, descs, t, ntiles, s);

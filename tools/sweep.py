@@ -69,8 +69,11 @@ VARIANTS = {
     # bit-sliced encode (kernels_bs.hip): one ring depth (blocks in flight) for every shape
     "bsr2": {"SEC_BS_RING": 2},
     "bsr3": {"SEC_BS_RING": 3},
+    "bsr6": {"SEC_BS_RING": 6},
     "bsr8": {"SEC_BS_RING": 8},
     "bsr10": {"SEC_BS_RING": 10},
+    "bsr12": {"SEC_BS_RING": 12},
+    "bsr16": {"SEC_BS_RING": 16},
     "bsld": {"SEC_BS_NT_LOAD": 0},  # bit-sliced encode with cached (not streaming) loads
     "bsw3": {"SEC_BS_WAVES": 3},  # bit-sliced encode capped for 3 waves per SIMD
     # decode workgroups per CU capped through padding LDS (160 KiB per CU): 3 or 2 per CU
