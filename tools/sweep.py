@@ -69,6 +69,7 @@ VARIANTS = {
     # bit-sliced encode (kernels_bs.hip): one ring depth (blocks in flight) for every shape
     "bsr2": {"SEC_BS_RING": 2},
     "bsr3": {"SEC_BS_RING": 3},
+    "bsr4": {"SEC_BS_RING": 4},
     "bsr6": {"SEC_BS_RING": 6},
     "bsr8": {"SEC_BS_RING": 8},
     "bsr10": {"SEC_BS_RING": 10},
