@@ -1,9 +1,16 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident RS encode + decode of 1 MiB chunks on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-seconds S] [--workload c2c3|c4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cpu-seconds S] [--workload c2c3|c4|c5]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+Ranks.  One process per GPU.  Under torch.distributed.run the ranks come from RANK /
+LOCAL_RANK / WORLD_SIZE, and WORLD_SIZE must equal --gpus (otherwise exit status 2).  A plain
+`python bench.py --gpus N` (N > 1, WORLD_SIZE unset) launches the N ranks itself, as fresh
+child processes with that environment (MASTER_ADDR 127.0.0.1), before anything touches the
+GPU, and exits with the first failing rank's status.  Every line carries the world size and
+backend the ranks saw.
 
 Workload (per rank; weak scaling — every rank owns its own 1024 chunks, no collective on the
 data path): BASELINE configs[1]+[2] — 1024 x 1 MiB chunks, RS(k=4, m=2) (zfec Encoder(4, 6)):
@@ -14,8 +21,18 @@ ranks / max-over-ranks wall time, in GiB/s (2^30 B).
 
 --workload c4 (BASELINE configs[3]; not the headline line): 65536 x 64 KiB chunks, RS(10,4), split
 over the ranks by storb_amd.dist.partition (8192 per GPU at N = 8; the whole job on one GPU at
-N = 1), strong scaling: value = job bytes encoded per step / max-over-ranks time.  Decode
-(blocks {0,2,5,7} erased, the padded block 9 read in place) is timed after the timed region.
+N = 1), strong scaling: value = job bytes encoded per step / max-over-ranks time.  Parity rows
+are written at a 128-byte-aligned stride (--c4-palign; the ABI's parity_stride, the caller's
+layout choice: storb keeps every piece as its own object).  Decode (blocks {0,2,5,7} erased,
+the padded block 9 read in place) is timed after the timed region.
+
+--workload c5 (BASELINE configs[4]): chunk sizes log-uniform in [4 KiB, 4 MiB] (seed 5) up to
+~1 GiB, RS(8,3) = zfec(8,11), split over the ranks by bytes (strong scaling).  One step =
+encode + decode ({1,3,5} erased, block 7 read in place) of the rank's share END TO END from
+pinned host memory (the kernels read and write the host buffers over PCIe: the product's
+zero-copy path); value = job bytes encoded + decoded per step / max-over-ranks time.  The
+device-resident kernel rates and the staged (pageable -> pinned slabs -> hipMemcpyAsync) rate
+are reported beside it.
 
 Also reported on the headline line:
   roofline      the decode kernel, the dominant one by time: algorithmic bytes per launch
@@ -34,6 +51,11 @@ Also reported on the headline line:
   e2e           host-buffer encode+decode through the C ABI incl. PCIe: pageable buffers
                 (page-locked per call, or staged through pinned slabs) and pinned buffers
                 (zero-copy) — reported beside `value`, never as it
+
+STORB_BENCH_ENGINE=module:Class (tests only) runs the ranks on CPU tensors with that engine
+(tests/bench_stub.py: the oracle behind the Engine interface) over gloo, so the launch, the
+partition and the reductions are tested without a GPU.  STORB_BENCH_DEVICE / STORB_DIST_BACKEND
+(rehearsal only) put every rank on one device over another backend.
 """
 
 from __future__ import annotations
@@ -42,8 +64,12 @@ import argparse
 import ctypes
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
+from types import SimpleNamespace
 
 import numpy as np
 
@@ -58,8 +84,12 @@ CHUNK = 1 << 20
 K, M = 4, 6  # RS(k=4, m=2) == zfec Encoder(4, 6)
 ERASED = (1, 3)
 
+# rocprofv3 kernel names of the headline kernels (api.cpp's plan for C2 / C3)
+ENC_KERNEL_C2 = "sec_encode_kernel<2, 1, false>"
+DEC_KERNEL_C3 = "sec_decode_kernel<2, 1, false, 0>"
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -67,18 +97,127 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--workload", choices=("c2c3", "c4"), default="c2c3",
+    ap.add_argument("--workload", choices=("c2c3", "c4", "c5"), default="c2c3",
                     help="c2c3: the headline line (BASELINE configs[1]+[2], weak scaling); c4: configs[3], "
-                         "65536 x 64 KiB RS(10,4) encode split over the ranks (strong scaling)")
+                         "65536 x 64 KiB RS(10,4) encode split over the ranks (strong scaling); c5: configs[4], "
+                         "mixed 4 KiB-4 MiB RS(8,3) encode + decode end to end from pinned host memory")
+    ap.add_argument("--chunks", type=int, default=N_CHUNKS,
+                    help="c2c3: chunks per rank (default 1024, the BASELINE config; smaller only in tests)")
     ap.add_argument("--c4-chunks", type=int, default=65536, help="c4: chunks in the whole job (default 65536)")
+    ap.add_argument("--c4-palign", type=int, default=128,
+                    help="c4: parity rows start at multiples of this many bytes (1 = packed, B apart)")
+    ap.add_argument("--c5-bytes", type=int, default=1 << 30, help="c5: job size (default ~1 GiB)")
     ap.add_argument("--no-recover", action="store_true",
                     help="skip the recover-only decode measurement (it shares the decode kernel's name, so a "
                          "rocprofv3 --stats run of the headline line wants it off)")
     ap.add_argument("--no-events", action="store_true",
                     help="A/B only: no per-launch HIP events in the timed region (roofline fields then null)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
+# ---------------------------------------------------------------- ranks
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(args, argv=None) -> int | None:
+    """None when this process is a rank; otherwise launch the ranks and return the exit status.
+
+    WORLD_SIZE set (torch.distributed.run, or our own children): it must equal --gpus.  Unset
+    with --gpus N > 1: start N children of this script with RANK = LOCAL_RANK = r, WORLD_SIZE =
+    N, MASTER_ADDR = 127.0.0.1 and a free MASTER_PORT.  This process never touches the GPU (it
+    has imported nothing but numpy), so nothing is re-executed after GPU initialisation."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench: WORLD_SIZE={ws} but --gpus {args.gpus}: refusing to report a {ws}-rank line as "
+                  f"{args.gpus}", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if args.gpus < 1:
+        print("bench: --gpus must be >= 1", file=sys.stderr, flush=True)
+        return 2
+    if args.gpus == 1:
+        return None
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    argv = sys.argv[1:] if argv is None else argv
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), *argv], env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+
+    old = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                c = p.poll()
+                if c is None:
+                    continue
+                pending.remove(p)
+                if c != 0 and rc == 0:  # first failure: stop the others (they would wait in a barrier)
+                    rc = c if c > 0 else 128 - c
+                    stop()
+            time.sleep(0.02)
+    finally:
+        stop()
+        for p in procs:
+            try:
+                p.wait(30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        signal.signal(signal.SIGTERM, old)
+    return rc
+
+
+def rank_context(args) -> SimpleNamespace:
+    """This rank's engine, device, sync and process group."""
+    from storb_amd import dist as D
+
+    rank, local, world = D.rank_env()
+    stub = os.environ.get("STORB_BENCH_ENGINE")
+    if stub:  # tests: the oracle behind the Engine interface, CPU tensors, gloo
+        import importlib
+
+        mod, cls = stub.split(":")
+        eng = getattr(importlib.import_module(mod), cls)()
+        device, sync, dev_idx = "cpu", (lambda: None), None
+        dmod = D.init(os.environ.get("STORB_DIST_BACKEND") or "gloo")
+    else:
+        import torch
+
+        from storb_amd.engine import Engine
+
+        local = int(os.environ.get("STORB_BENCH_DEVICE", local))
+        torch.cuda.set_device(local)
+        dmod = D.init(os.environ.get("STORB_DIST_BACKEND") or None)
+        eng = Engine(local)
+        device, sync, dev_idx = f"cuda:{local}", torch.cuda.synchronize, local
+    seen = dmod.get_world_size() if dmod is not None else 1
+    if seen != args.gpus or seen != world:
+        raise SystemExit(f"bench: rank {rank} sees world size {seen}, --gpus {args.gpus}, WORLD_SIZE {world}")
+    return SimpleNamespace(rank=rank, local=dev_idx, world=world, device=device, sync=sync, dmod=dmod, eng=eng,
+                           backend=dmod.get_backend() if dmod is not None else None)
+
+
+def finish(ctx) -> None:
+    ctx.eng.close()
+    if ctx.dmod is not None:
+        ctx.dmod.destroy_process_group()
+
+
+# ---------------------------------------------------------------- descriptors
 def enc_descs(nchunks, n, k, m, pstride=None):
     """pstride: distance between a chunk's parity blocks (default B, i.e. packed)."""
     from storb_amd._lib import ENC_DTYPE
@@ -125,51 +264,98 @@ def dec_descs(nchunks, n, k, m, B, data_base, par_base, erased, pstride=None, re
     return d, sn, offs, avail
 
 
-def load_traffic(kind: str):
-    """Per-launch HBM bytes of the encode / decode kernel from the committed rocprofv3 PMC summary
-    (profiles/pmc_encode_c2.json: FETCH_SIZE x 2 + WRITE_SIZE on this workload)."""
-    path = os.path.join(ROOT, "profiles", "pmc_encode_c2.json")
+def enc_descs_var(sizes, k, m):
+    """Encode descriptors of chunks of the given sizes packed back to back (parity packed too)."""
+    from storb_amd._lib import ENC_DTYPE
+
+    sizes = np.asarray(sizes, dtype=np.uint64)
+    B = (sizes + k - 1) // k
+    d = np.zeros(len(sizes), dtype=ENC_DTYPE)
+    d["in_off"] = np.concatenate([[0], np.cumsum(sizes)[:-1]]) if len(sizes) else []
+    d["n"] = sizes
+    d["parity_off"] = np.concatenate([[0], np.cumsum(B * (m - k))[:-1]]) if len(sizes) else []
+    d["parity_stride"] = B
+    d["k"], d["m"] = k, m
+    return d, B
+
+
+def dec_descs_var(sizes, k, m, B, data_base, par_base, erased):
+    """enc_descs_var's chunks decoded in place: descriptors, sharenums, block offsets and per-slot
+    avail (an in-place block k-1 has B - padlen bytes)."""
+    from storb_amd._lib import DEC_DTYPE
+
+    keep = [s for s in range(m) if s not in erased][:k]
+    n = len(sizes)
+    sizes = np.asarray(sizes, dtype=np.uint64)
+    in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    par_off = np.concatenate([[0], np.cumsum(B * (m - k))[:-1]]).astype(np.uint64)
+    d = np.zeros(n, dtype=DEC_DTYPE)
+    d["out_off"] = in_off
+    d["B"] = B
+    d["padlen"] = B * k - sizes
+    d["slot0"] = np.arange(n, dtype=np.uint64) * k
+    d["k"], d["m"] = k, m
+    sn = np.tile(np.array(keep, np.int32), n)
+    offs = np.zeros(n * k, np.uint64)
+    avail = np.zeros(n * k, np.uint64)
+    for j, s in enumerate(keep):
+        offs[j::k] = (data_base + in_off + s * B) if s < k else (par_base + par_off + (s - k) * B)
+        avail[j::k] = (sizes - (k - 1) * B) if s == k - 1 else B
+    return d, sn, offs, avail
+
+
+def load_traffic(kind: str, workload: str = "c2", name: str = "pmc_encode_c2.json"):
+    """Per-launch HBM bytes of a bench kernel from a committed rocprofv3 PMC summary
+    (tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE on that workload), else None."""
+    path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as f:
             j = json.load(f)
-        if j.get("workload") == "c2" and j.get(kind, {}).get("hbm_bytes_per_launch"):
+        if j.get("workload") == workload and j.get(kind, {}).get("hbm_bytes_per_launch"):
             return float(j[kind]["hbm_bytes_per_launch"])
     except (OSError, ValueError):
         pass
     return None
 
 
-def _cpu_worker(seconds: float, seed: int) -> tuple[int, float]:
-    """One thread of the CPU baseline: encode + decode loops over its own buffers.  ctypes
-    drops the GIL inside the C calls, so threads run concurrently."""
+# ---------------------------------------------------------------- CPU baseline (oracle)
+def _cpu_worker(seconds: float, seed: int, sizes, k: int, m: int, erased, decode: bool = True) -> tuple[int, int, float]:
+    """One thread of the CPU baseline: encode (+ decode with `erased` lost) of chunks of the given
+    sizes in turn, each from its own buffer.  ctypes drops the GIL inside the C calls, so threads
+    run concurrently.  Returns (chunks, chunk bytes processed, seconds)."""
     from oracle import cfec
 
     lib = cfec.lib()
     u8p = ctypes.POINTER(ctypes.c_uint8)
     rng = np.random.default_rng(seed)
-    nsample = 8
-    chunks = [rng.integers(0, 256, CHUNK, dtype=np.uint8).tobytes() for _ in range(nsample)]
-    B = CHUNK // K
-    blocks = (ctypes.c_uint8 * (M * B))()
-    out = (ctypes.c_uint8 * CHUNK)()
-    keep = [s for s in range(M) if s not in ERASED]
-    sn = (ctypes.c_int * K)(*keep)
-    base = ctypes.addressof(blocks)
-    ptrs = (ctypes.c_char_p * K)(*[ctypes.c_char_p(base + s * B) for s in keep])
-    done = 0
+    keep = [s for s in range(m) if s not in erased][:k]
+    sn = (ctypes.c_int * k)(*keep)
+    cases = []
+    for n in sizes:
+        B = -(-n // k)
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        blocks = (ctypes.c_uint8 * (m * B))()
+        out = (ctypes.c_uint8 * n)()
+        base = ctypes.addressof(blocks)
+        ptrs = (ctypes.c_char_p * k)(*[ctypes.c_char_p(base + s * B) for s in keep])
+        cases.append((n, B, data, blocks, out, ptrs))
+    done = nbytes = 0
     t0 = time.perf_counter()
     while True:
-        c = chunks[done % nsample]
-        if lib.fo_easy_encode(K, M, c, CHUNK, ctypes.cast(blocks, u8p)) != B:
+        n, B, data, blocks, out, ptrs = cases[done % len(cases)]
+        if lib.fo_easy_encode(k, m, data, n, ctypes.cast(blocks, u8p)) != B:
             raise RuntimeError("oracle encode failed")
-        if lib.fo_easy_decode(K, M, ptrs, sn, B, 0, ctypes.cast(out, u8p)):
-            raise RuntimeError("oracle decode failed")
-        if done == 0 and bytes(out) != c:
-            raise RuntimeError("oracle round trip mismatch")
+        nbytes += n
+        if decode:
+            if lib.fo_easy_decode(k, m, ptrs, sn, B, k * B - n, ctypes.cast(out, u8p)):
+                raise RuntimeError("oracle decode failed")
+            if done < len(cases) and bytes(out) != data:
+                raise RuntimeError("oracle round trip mismatch")
+            nbytes += n
         done += 1
         el = time.perf_counter() - t0
         if el >= seconds:
-            return done, el
+            return done, nbytes, el
 
 
 def cpu_threads() -> int:
@@ -182,29 +368,32 @@ def cpu_threads() -> int:
     return max(1, min(16, n))
 
 
-def cpu_baseline(seconds: float) -> dict:
-    """oracle/fec_oracle.c: encode + decode ({1,3} erased) of 1 MiB RS(4,2) chunks, one chunk
-    per task; `seconds` on 1 thread, then `seconds` on cpu_threads() threads."""
+def cpu_baseline(seconds: float, sizes=None, k=K, m=M, erased=ERASED, decode=True, what=None) -> dict:
+    """oracle/fec_oracle.c on a bounded sample: `seconds` on 1 thread, then `seconds` on
+    cpu_threads() threads, each thread cycling over its own copy of `sizes` (default: 8 chunks of
+    1 MiB, RS(4,2), {1,3} erased), one chunk per task."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import cfec
 
+    sizes = list(sizes) if sizes is not None else [CHUNK] * 8
     cfec.lib()  # build / load once before the threads start
-    d1, e1 = _cpu_worker(seconds, 0)
-    single = 2 * d1 * CHUNK / e1 / GIB
+    d1, b1, e1 = _cpu_worker(seconds, 0, sizes, k, m, erased, decode)
     T = cpu_threads()
     with ThreadPoolExecutor(T) as ex:
-        res = list(ex.map(lambda i: _cpu_worker(seconds, i), range(T)))
-    done = sum(d for d, _ in res)
-    el = max(e for _, e in res)
-    multi = 2 * done * CHUNK / el / GIB
-    return {"value": round(multi, 4), "unit": "GiB/s", "cores": T, "kind": "port",
-            "single_thread_value": round(single, 4),
-            "sample": f"{T} threads x {seconds:.0f} s of (encode + decode {{1,3}} erased) of 1 MiB RS(4,2) chunks "
-                      f"({done} chunks), one chunk per task; 1 thread: {d1} chunks in {e1:.1f} s; "
-                      f"oracle/fec_oracle.c (zfec fec.c restatement: 64 KiB LUT, 8 KiB strides)"}
+        res = list(ex.map(lambda i: _cpu_worker(seconds, i, sizes, k, m, erased, decode), range(T)))
+    done = sum(d for d, _, _ in res)
+    nb = sum(b for _, b, _ in res)
+    el = max(e for _, _, e in res)
+    what = what or (f"(encode + decode {{{','.join(map(str, erased))}}} erased) of 1 MiB RS({k},{m - k}) chunks")
+    return {"value": round(nb / el / GIB, 4), "unit": "GiB/s", "cores": T, "kind": "port",
+            "single_thread_value": round(b1 / e1 / GIB, 4),
+            "sample": f"{T} threads x {seconds:.0f} s of {what} ({done} chunks), one chunk per task; 1 thread: "
+                      f"{d1} chunks in {e1:.1f} s; oracle/fec_oracle.c (zfec fec.c restatement: 64 KiB LUT, "
+                      f"8 KiB strides)"}
 
 
+# ---------------------------------------------------------------- timing helpers
 def timed_region(dmod, local, sync, steps, body):
     """The contract's timed region: barrier + device sync on both sides of exactly `steps`
     calls of body(); returns the max over ranks of the elapsed seconds."""
@@ -223,6 +412,10 @@ def timed_region(dmod, local, sync, steps, body):
 def kernel_avg_s(eng, kind):
     ms, n = eng.collect_timing(kind)
     return (ms / 1e3 / n) if n else float("nan"), n
+
+
+def _gbs(nbytes, t):
+    return round(nbytes / t / 1e9, 1) if t == t and t > 0 else None
 
 
 def recover_only_rate(eng, torch, src, par, nchunks, n, k, m, B, reps=10) -> dict:
@@ -246,106 +439,109 @@ def recover_only_rate(eng, torch, src, par, nchunks, n, k, m, B, reps=10) -> dic
     eng.set_timing(False)
     t, nl = kernel_avg_s(eng, "decode")
     alg = nchunks * (k + e) * B
-    return {"achieved": round(alg / t / 1e9, 1), "unit": "GB/s", "algorithmic_bytes_per_launch": alg,
+    return {"achieved": _gbs(alg, t), "unit": "GB/s", "algorithmic_bytes_per_launch": alg,
             "avg_launch_ms": round(t * 1e3, 4), "launches": nl}
 
 
-def main():
-    args = parse()
-    if args.workload == "c4":
-        return main_c4(args)
+# ---------------------------------------------------------------- BASELINE configs[1]+[2] (headline)
+def c2c3_run(ctx, steps, warmup, nchunks=N_CHUNKS, events=True):
+    """This rank's 1024 x 1 MiB RS(4,2) encode + {1,3}-erased decode; returns the rank's numbers
+    and the job's max-over-ranks time, plus the buffers for the after-region measurements."""
     import torch
 
-    from storb_amd import dist as D
-    from storb_amd.engine import Engine
-
-    rank, local, world = D.rank_env()
-    # rehearsal overrides (several ranks on one GPU over gloo); the driver's runs set neither
-    local = int(os.environ.get("STORB_BENCH_DEVICE", local))
-    torch.cuda.set_device(local)
-    dmod = D.init(os.environ.get("STORB_DIST_BACKEND") or None)
-    eng = Engine(local)
-
+    eng = ctx.eng
     n, k, m = CHUNK, K, M
-    g = torch.Generator(device=f"cuda:{local}")
-    g.manual_seed(1000 + rank)
-    src = torch.randint(0, 256, (N_CHUNKS * n,), dtype=torch.uint8, device=f"cuda:{local}", generator=g)
-    ed, B = enc_descs(N_CHUNKS, n, k, m)
-    par = torch.empty(N_CHUNKS * (m - k) * B, dtype=torch.uint8, device=f"cuda:{local}")
+    g = torch.Generator(device=ctx.device)
+    g.manual_seed(1000 + ctx.rank)
+    src = torch.randint(0, 256, (nchunks * n,), dtype=torch.uint8, device=ctx.device, generator=g)
+    ed, B = enc_descs(nchunks, n, k, m)
+    par = torch.empty(nchunks * (m - k) * B, dtype=torch.uint8, device=ctx.device)
     out = torch.empty_like(src)
-    dd, sn, offs, av = dec_descs(N_CHUNKS, n, k, m, B, src.data_ptr(), par.data_ptr(), ERASED)
+    dd, sn, offs, av = dec_descs(nchunks, n, k, m, B, src.data_ptr(), par.data_ptr(), ERASED)
 
     def step():
         eng.encode_batch(ed, src, par, asynchronous=True)
         eng.decode_batch(dd, sn, offs, 0, out, block_avail=av, asynchronous=True)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     eng.sync()
-    if not torch.equal(out, src):
-        raise SystemExit("bench: decode round trip mismatch")
+    if warmup and not torch.equal(out, src):
+        raise SystemExit(f"bench: rank {ctx.rank} decode round trip mismatch")
 
-    eng.set_timing(not args.no_events)
-    el_max = timed_region(dmod, local, torch.cuda.synchronize, args.steps, step)
+    eng.set_timing(events)
+    el_max = timed_region(ctx.dmod, ctx.local, ctx.sync, steps, step)
     eng.set_timing(False)
     enc_avg_s, enc_n = kernel_avg_s(eng, "encode")
     dec_avg_s, dec_n = kernel_avg_s(eng, "decode")
+    from storb_amd import dist as D
 
-    bytes_per_step = 2 * N_CHUNKS * n  # encoded + decoded chunk bytes
-    value = world * args.steps * bytes_per_step / el_max / GIB
+    counts = D.gather_counts(ctx.dmod, nchunks, ctx.rank, ctx.world, ctx.local)
+    return {"el_max": el_max, "B": B, "chunks": nchunks, "per_rank_chunks": counts, "enc_avg_s": enc_avg_s,
+            "enc_launches": enc_n, "dec_avg_s": dec_avg_s, "dec_launches": dec_n, "src": src, "par": par}
 
-    enc_alg = N_CHUNKS * (n + (m - k) * B)  # bytes per encode launch
-    dec_alg = N_CHUNKS * (k * B + n)  # reassemble: k blocks read + n written
-    enc_gbs = enc_alg / enc_avg_s / 1e9
-    dec_gbs = dec_alg / dec_avg_s / 1e9
 
+def main_c2c3(args, ctx):
+    import torch
+
+    r = c2c3_run(ctx, args.steps, args.warmup, args.chunks, events=not args.no_events)
+    nchunks, n, k, m, B = args.chunks, CHUNK, K, M, r["B"]
+    bytes_per_step = 2 * nchunks * n  # encoded + decoded chunk bytes
+    total_chunks = sum(r["per_rank_chunks"])
+    value = args.steps * 2 * total_chunks * n / r["el_max"] / GIB
+
+    enc_alg = nchunks * (n + (m - k) * B)  # bytes per encode launch
+    dec_alg = nchunks * (k * B + n)  # reassemble: k blocks read + n written
+    enc_avg_s, dec_avg_s = r["enc_avg_s"], r["dec_avg_s"]
+    enc_gbs, dec_gbs = _gbs(enc_alg, enc_avg_s), _gbs(dec_alg, dec_avg_s)
     res = None
-    if rank == 0:
+    if ctx.rank == 0:
         res = {
             "metric": "GiB/s device-resident RS encode+decode, 1 MiB chunks, 1/2/4/8 MI355X",
             "value": round(value, 3),
             "unit": "GiB/s",
-            "n_gpus": world,
+            "n_gpus": ctx.world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(el_max / args.steps * 1e3, 4),
+            "ms_per_step": round(r["el_max"] / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (torch.randint uniform bytes, seeded per rank), HBM-resident",
-            "config": {"workload": "1024 x 1 MiB chunks per GPU, RS(k=4,m=2)=zfec(4,6): encode + "
+            "config": {"workload": f"{nchunks} x 1 MiB chunks per GPU, RS(k=4,m=2)=zfec(4,6): encode + "
                                    "decode/reassemble with data shards {1,3} erased",
-                       "chunks_per_gpu": N_CHUNKS, "chunk_bytes": n, "k": k, "m_total": m,
-                       "bytes_per_step_per_gpu": bytes_per_step, "parallelism": f"chunk-partition x{world}"},
+                       "chunks_per_gpu": nchunks, "per_rank_chunks": r["per_rank_chunks"], "chunk_bytes": n,
+                       "k": k, "m_total": m, "bytes_per_step_per_gpu": bytes_per_step, "world_size": ctx.world,
+                       "backend": ctx.backend, "parallelism": f"chunk-partition x{ctx.world}"},
             # the dominant kernel by time is the decode (it moves 2 MiB per chunk to encode's 1.5)
-            "roofline": {"bound": "hbm", "achieved": round(dec_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(dec_gbs / PEAK_HBM_GBS, 4), "traffic": load_traffic("decode"),
-                         "kernel": "sec_decode_kernel<2, 1, false>", "algorithmic_bytes_per_launch": dec_alg,
-                         "avg_launch_ms": round(dec_avg_s * 1e3, 4), "launches": dec_n},
+            "roofline": {"bound": "hbm", "achieved": dec_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(dec_gbs / PEAK_HBM_GBS, 4) if dec_gbs else None,
+                         "traffic": load_traffic("decode"), "kernel": DEC_KERNEL_C3,
+                         "algorithmic_bytes_per_launch": dec_alg,
+                         "avg_launch_ms": round(dec_avg_s * 1e3, 4), "launches": r["dec_launches"]},
             # the north star's target kernel (>= 70 % of HBM roofline on C2 encode)
-            "encode_kernel": {"achieved": round(enc_gbs, 1), "unit": "GB/s", "frac": round(enc_gbs / PEAK_HBM_GBS, 4),
-                              "traffic": load_traffic("encode"), "kernel": "sec_encode_kernel<2, 1, false>",
+            "encode_kernel": {"achieved": enc_gbs, "unit": "GB/s",
+                              "frac": round(enc_gbs / PEAK_HBM_GBS, 4) if enc_gbs else None,
+                              "traffic": load_traffic("encode"), "kernel": ENC_KERNEL_C2,
                               "algorithmic_bytes_per_launch": enc_alg, "avg_launch_ms": round(enc_avg_s * 1e3, 4),
-                              "launches": enc_n},
-            "encode_gibs": round(N_CHUNKS * n / enc_avg_s / GIB, 2),
-            "decode_gibs": round(N_CHUNKS * n / dec_avg_s / GIB, 2),
+                              "launches": r["enc_launches"]},
+            "encode_gibs": round(nchunks * n / enc_avg_s / GIB, 2) if enc_gbs else None,
+            "decode_gibs": round(nchunks * n / dec_avg_s / GIB, 2) if dec_gbs else None,
         }
         if not args.no_events and not args.no_recover:  # after the timed region; not part of `value`
-            res["decode_recover_only_kernel"] = recover_only_rate(eng, torch, src, par, N_CHUNKS, n, k, m, B)
+            res["decode_recover_only_kernel"] = recover_only_rate(ctx.eng, torch, r["src"], r["par"], nchunks, n, k,
+                                                                  m, B)
 
     # host-buffer (PCIe-inclusive) rate: reported, never `value`
-    if rank == 0 and world == 1 and not args.no_e2e:
-        res["e2e"] = e2e_rate(eng)
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_e2e:
+        res["e2e"] = e2e_rate(ctx.eng)
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu:
         res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
-    elif rank == 0:
+    elif ctx.rank == 0:
         res["cpu_baseline"] = None
-    if rank == 0:
+    if ctx.rank == 0:
         print(json.dumps(res), flush=True)
-    eng.close()
-    if dmod is not None:
-        dmod.destroy_process_group()
 
 
 # ---------------------------------------------------------------- BASELINE configs[3] (C4)
@@ -360,26 +556,34 @@ def c4_share(rank: int, world: int, nchunks: int = C4_CHUNKS) -> tuple[int, int]
     return D.partition([C4_CHUNK] * nchunks, world)[rank]
 
 
+def c4_pstride(B: int, palign: int) -> int:
+    """Parity row stride: B rounded up to a multiple of palign (1: packed)."""
+    palign = max(int(palign), 1)
+    return -(-B // palign) * palign
+
+
 def c4_run(eng, dmod, rank, world, local, device, sync, steps, warmup, nchunks=C4_CHUNKS, verify=True,
-           keep=False):
+           keep=False, palign=128):
     """C4 as BASELINE.json writes it: `nchunks` x 64 KiB RS(10,4) chunks split over the ranks
-    (contiguous ranges, no data-path collective); each rank encodes its share on its device.
-    Returns this rank's numbers plus the job's aggregate (max-over-ranks time, summed chunks).
-    `eng` needs encode_batch / decode_batch / sync / set_timing / collect_timing (the product
-    Engine; tests/test_dist.py drives it with a stand-in on CPU tensors)."""
+    (contiguous ranges, no data-path collective); each rank encodes its share on its device,
+    parity rows `palign`-aligned (B rounded up).  Returns this rank's numbers plus the job's
+    aggregate (max-over-ranks time, summed chunks).  `eng` needs encode_batch / decode_batch /
+    sync / set_timing / collect_timing (the product Engine; tests drive it with the oracle)."""
     import torch
 
     from storb_amd import dist as D
 
     lo, hi = c4_share(rank, world, nchunks)
     nch, n, k, m = hi - lo, C4_CHUNK, C4_K, C4_M
+    B = -(-n // k)
+    ps = c4_pstride(B, palign)
     g = torch.Generator(device=device)
     g.manual_seed(4_000_003 + lo)  # seed 4, per share
     src = torch.randint(0, 256, (max(nch * n, 1),), dtype=torch.uint8, device=device, generator=g)
-    ed, B = enc_descs(nch, n, k, m)
-    par = torch.empty(max(nch * (m - k) * B, 1), dtype=torch.uint8, device=device)
+    ed, _ = enc_descs(nch, n, k, m, ps)
+    par = torch.empty(max(nch * (m - k) * ps, 1), dtype=torch.uint8, device=device)
     out = torch.empty_like(src)
-    dd, sn, offs, av = dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), C4_ERASED)
+    dd, sn, offs, av = dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), C4_ERASED, ps)
 
     def step():
         eng.encode_batch(ed, src, par, asynchronous=True)
@@ -402,9 +606,8 @@ def c4_run(eng, dmod, rank, world, local, device, sync, steps, warmup, nchunks=C
     eng.sync()
     eng.set_timing(False)
     dec_avg_s, dec_n = kernel_avg_s(eng, "decode")
-    total_chunks = int(D.sum_over_ranks(dmod, float(nch), local))
-    counts = [int(D.sum_over_ranks(dmod, float(nch if r == rank else 0), local)) for r in range(world)]
-    res = {"lo": lo, "hi": hi, "chunks": nch, "B": B, "el_max": el_max, "total_chunks": total_chunks,
+    counts = D.gather_counts(dmod, nch, rank, world, local)
+    res = {"lo": lo, "hi": hi, "chunks": nch, "B": B, "pstride": ps, "el_max": el_max, "total_chunks": sum(counts),
            "per_rank_chunks": counts, "enc_avg_s": enc_avg_s, "enc_launches": enc_n, "dec_avg_s": dec_avg_s,
            "dec_launches": dec_n}
     if keep:  # the buffers, for tests that compare samples against the oracle
@@ -412,57 +615,201 @@ def c4_run(eng, dmod, rank, world, local, device, sync, steps, warmup, nchunks=C
     return res
 
 
-def main_c4(args):
-    import torch
-
-    from storb_amd import dist as D
-    from storb_amd.engine import Engine
-
-    rank, local, world = D.rank_env()
-    local = int(os.environ.get("STORB_BENCH_DEVICE", local))
-    torch.cuda.set_device(local)
-    dmod = D.init(os.environ.get("STORB_DIST_BACKEND") or None)
-    eng = Engine(local)
-    r = c4_run(eng, dmod, rank, world, local, f"cuda:{local}", torch.cuda.synchronize, args.steps, args.warmup,
-               nchunks=args.c4_chunks)
+def main_c4(args, ctx):
+    r = c4_run(ctx.eng, ctx.dmod, ctx.rank, ctx.world, ctx.local, ctx.device, ctx.sync, args.steps, args.warmup,
+               nchunks=args.c4_chunks, palign=args.c4_palign)
     n, k, m, B = C4_CHUNK, C4_K, C4_M, r["B"]
     job_bytes = r["total_chunks"] * n
     value = args.steps * job_bytes / r["el_max"] / GIB
     enc_alg = r["chunks"] * (n + (m - k) * B)
     dec_alg = r["chunks"] * (k * B + n)
-    if rank == 0:
-        enc_gbs = enc_alg / r["enc_avg_s"] / 1e9
-        res = {
-            "metric": "GiB/s device-resident RS(10,4) encode, 65536 x 64 KiB chunks sharded across N MI355X",
-            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(r["el_max"] / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic (torch.randint uniform bytes, seed 4 per share), HBM-resident",
-            "config": {"workload": f"BASELINE configs[3]: {r['total_chunks']} x 64 KiB chunks, RS(k=10,m=4)="
-                                   "zfec(10,14), B = 6554, padlen 4, encode; chunks split by "
-                                   "storb_amd.dist.partition over the ranks, no data-path collective",
-                       "chunks_total": r["total_chunks"], "per_rank_chunks": r["per_rank_chunks"],
-                       "world_size": world,
-                       "backend": dmod.get_backend() if dmod is not None else None,
-                       "parallelism": f"chunk-partition x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(enc_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(enc_gbs / PEAK_HBM_GBS, 4), "traffic": None,
-                         "kernel": ("sec_encode_kernel<4, 1, false>" if os.environ.get("SEC_BS") == "0"
-                                    else "sec_encode_bs_kernel<10, 14, 0, 4, 5>"),  # api.cpp bs_shape
-                         "algorithmic_bytes_per_launch": enc_alg,
-                         "avg_launch_ms": round(r["enc_avg_s"] * 1e3, 4), "launches": r["enc_launches"]},
-            "decode_kernel": {"achieved": round(dec_alg / r["dec_avg_s"] / 1e9, 1), "unit": "GB/s",
-                              "erased": list(C4_ERASED), "block_9": "read in place, avail = B - padlen",
-                              "algorithmic_bytes_per_launch": dec_alg,
-                              "avg_launch_ms": round(r["dec_avg_s"] * 1e3, 4), "launches": r["dec_launches"]},
-            "cpu_baseline": None,
-        }
-        print(json.dumps(res), flush=True)
-    eng.close()
-    if dmod is not None:
-        dmod.destroy_process_group()
+    if ctx.rank != 0:
+        return
+    enc_gbs = _gbs(enc_alg, r["enc_avg_s"])
+    kernel = ("sec_encode_kernel<4, 1, false>" if os.environ.get("SEC_BS") == "0"
+              else "sec_encode_bs_kernel<10, 14, 0, 4, 5>")  # api.cpp bs_shape
+    # the committed PMC summary applies to the configuration it was taken on (full job, N = 1,
+    # this parity alignment)
+    traffic = None
+    if (ctx.world, args.c4_chunks, r["pstride"]) == (1, C4_CHUNKS, c4_pstride(B, 128)):
+        traffic = load_traffic("encode", "c4", "r03_pmc_c4.json")
+    res = {
+        "metric": "GiB/s device-resident RS(10,4) encode, 65536 x 64 KiB chunks sharded across N MI355X",
+        "value": round(value, 3), "unit": "GiB/s", "n_gpus": ctx.world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(r["el_max"] / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (torch.randint uniform bytes, seed 4 per share), HBM-resident",
+        "config": {"workload": f"BASELINE configs[3]: {r['total_chunks']} x 64 KiB chunks, RS(k=10,m=4)="
+                               "zfec(10,14), B = 6554, padlen 4, encode; chunks split by "
+                               "storb_amd.dist.partition over the ranks, no data-path collective",
+                   "chunks_total": r["total_chunks"], "per_rank_chunks": r["per_rank_chunks"],
+                   "parity_stride": r["pstride"], "world_size": ctx.world, "backend": ctx.backend,
+                   "parallelism": f"chunk-partition x{ctx.world}"},
+        "roofline": {"bound": "hbm", "achieved": enc_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(enc_gbs / PEAK_HBM_GBS, 4) if enc_gbs else None, "traffic": traffic,
+                     "kernel": kernel, "algorithmic_bytes_per_launch": enc_alg,
+                     "avg_launch_ms": round(r["enc_avg_s"] * 1e3, 4), "launches": r["enc_launches"]},
+        "decode_kernel": {"achieved": _gbs(dec_alg, r["dec_avg_s"]), "unit": "GB/s",
+                          "erased": list(C4_ERASED), "block_9": "read in place, avail = B - padlen",
+                          "algorithmic_bytes_per_launch": dec_alg,
+                          "avg_launch_ms": round(r["dec_avg_s"] * 1e3, 4), "launches": r["dec_launches"]},
+        "cpu_baseline": None,
+    }
+    if ctx.world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, [C4_CHUNK] * 16, C4_K, C4_M, C4_ERASED, decode=False,
+                                           what="RS(10,4) encode of 64 KiB chunks (B = 6554, padlen 4)")
+    print(json.dumps(res), flush=True)
 
 
+# ---------------------------------------------------------------- BASELINE configs[4] (C5)
+C5_K, C5_M = 8, 11
+C5_ERASED = (1, 3, 5)  # three data blocks lost; block 7 (zfec's padded one) read in place
+
+
+def c5_sizes(total: int = 1 << 30) -> list[int]:
+    """BASELINE configs[4] chunk sizes: log-uniform integers in [4 KiB, 4 MiB], seed 5, ~`total`."""
+    r5 = np.random.default_rng(5)
+    sizes, tot = [], 0
+    while tot < total:
+        s = int(np.exp(r5.uniform(np.log(4096), np.log(4 << 20))))
+        sizes.append(s)
+        tot += s
+    return sizes
+
+
+def c5_run(ctx, steps, warmup, total=1 << 30, keep=False, staged=True):
+    """C5 on this rank's share (contiguous chunk range balanced by bytes): the timed steps are
+    encode + decode END TO END from pinned host buffers (host=True on Engine.host_empty memory:
+    the kernels read the chunks and write parity / reassembled chunks over PCIe); then, outside
+    the timed region, the same share device-resident (kernel rates from HIP events) and, with
+    `staged`, from pageable buffers through the pinned slabs (SEC_REGISTER_MIN=0: explicit
+    hipMemcpyAsync both ways).  Every path's output is checked against the input."""
+    import torch
+
+    from storb_amd import dist as D
+
+    eng = ctx.eng
+    k, m = C5_K, C5_M
+    sizes_all = c5_sizes(total)
+    lo, hi = D.partition(sizes_all, ctx.world)[ctx.rank]
+    sizes = sizes_all[lo:hi]
+    nbytes = int(np.sum(sizes))
+    ed, B = enc_descs_var(sizes, k, m)
+    npar = int(np.sum(B)) * (m - k)
+    rng = np.random.default_rng(5_000_000 + lo)
+    host = eng.host_empty(nbytes)
+    host[:] = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    hpar, hout = eng.host_empty(max(npar, 1)), eng.host_empty(max(nbytes, 1))
+    dd, sn, offs, av = dec_descs_var(sizes, k, m, B, host.ctypes.data, hpar.ctypes.data, C5_ERASED)
+
+    def step():
+        eng.encode_batch(ed, host, hpar, host=True)
+        eng.decode_batch(dd, sn, offs, 0, hout, block_avail=av, host=True)
+
+    for _ in range(warmup):
+        step()
+    if warmup and not np.array_equal(hout[:nbytes], host):
+        raise SystemExit(f"bench c5: rank {ctx.rank} end-to-end round trip mismatch")
+    el_max = timed_region(ctx.dmod, ctx.local, ctx.sync, steps, step)
+    hout[:] = 0
+    step()  # the last timed step's output, checked (a fast wrong answer is not a result)
+    if not np.array_equal(hout[:nbytes], host):
+        raise SystemExit(f"bench c5: rank {ctx.rank} end-to-end output mismatch")
+
+    # device-resident, after the timed region
+    src = torch.from_numpy(host).to(ctx.device)
+    par = torch.empty(max(npar, 1), dtype=torch.uint8, device=ctx.device)
+    out = torch.empty_like(src)
+    ddd, dsn, doffs, dav = dec_descs_var(sizes, k, m, B, src.data_ptr(), par.data_ptr(), C5_ERASED)
+    eng.encode_batch(ed, src, par)
+    eng.decode_batch(ddd, dsn, doffs, 0, out, block_avail=dav)
+    if not torch.equal(out, src):
+        raise SystemExit(f"bench c5: rank {ctx.rank} device round trip mismatch")
+    reps = max(steps, 5)
+    eng.set_timing(True)
+    for _ in range(reps):
+        eng.encode_batch(ed, src, par, asynchronous=True)
+    for _ in range(reps):
+        eng.decode_batch(ddd, dsn, doffs, 0, out, block_avail=dav, asynchronous=True)
+    eng.sync()
+    eng.set_timing(False)
+    enc_avg_s, enc_n = kernel_avg_s(eng, "encode")
+    dec_avg_s, dec_n = kernel_avg_s(eng, "decode")
+    res = {"lo": lo, "hi": hi, "sizes": sizes, "bytes": nbytes, "el_max": el_max, "enc_avg_s": enc_avg_s,
+           "enc_launches": enc_n, "dec_avg_s": dec_avg_s, "dec_launches": dec_n,
+           "enc_alg": nbytes + npar, "dec_alg": int(np.sum(B)) * k + nbytes,
+           "job_bytes": int(D.sum_over_ranks(ctx.dmod, float(nbytes), ctx.local)),
+           "per_rank_chunks": D.gather_counts(ctx.dmod, hi - lo, ctx.rank, ctx.world, ctx.local)}
+    if staged:  # pageable buffers staged through the pinned slabs: explicit hipMemcpyAsync both ways
+        pg = np.array(host)
+        ppar, pout = np.empty(max(npar, 1), np.uint8), np.empty_like(pg)
+        sdd, ssn, soffs, sav = dec_descs_var(sizes, k, m, B, pg.ctypes.data, ppar.ctypes.data, C5_ERASED)
+        os.environ["SEC_REGISTER_MIN"] = "0"
+        try:
+            eng.encode_batch(ed, pg, ppar, host=True)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                eng.encode_batch(ed, pg, ppar, host=True)
+            t1 = time.perf_counter()
+            for _ in range(3):
+                eng.decode_batch(sdd, ssn, soffs, 0, pout, block_avail=sav, host=True)
+            t2 = time.perf_counter()
+        finally:
+            os.environ.pop("SEC_REGISTER_MIN")
+        if not np.array_equal(pout, pg):
+            raise SystemExit(f"bench c5: rank {ctx.rank} staged round trip mismatch")
+        res["staged_encode_gibs"] = round(3 * nbytes / (t1 - t0) / GIB, 2)
+        res["staged_decode_gibs"] = round(3 * nbytes / (t2 - t1) / GIB, 2)
+    if keep:
+        res.update(src=src, par=par, host=host, hpar=hpar)
+    return res
+
+
+def main_c5(args, ctx):
+    r = c5_run(ctx, args.steps, args.warmup, total=args.c5_bytes, staged=not args.no_e2e)
+    value = args.steps * 2 * r["job_bytes"] / r["el_max"] / GIB
+    if ctx.rank != 0:
+        return
+    enc_gbs, dec_gbs = _gbs(r["enc_alg"], r["enc_avg_s"]), _gbs(r["dec_alg"], r["dec_avg_s"])
+    dom_dec = r["dec_avg_s"] >= r["enc_avg_s"]
+    res = {
+        "metric": "GiB/s end-to-end RS(8,3) encode+decode of mixed 4 KiB-4 MiB chunks from pinned host memory, "
+                  "N MI355X",
+        "value": round(value, 3), "unit": "GiB/s", "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(r["el_max"] / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (numpy uniform bytes, seed 5 per share) in pinned host memory",
+        "config": {"workload": f"BASELINE configs[4]: {sum(r['per_rank_chunks'])} chunks, sizes log-uniform in "
+                               f"[4 KiB, 4 MiB] (seed 5), {r['job_bytes']} B, RS(k=8,m=3)=zfec(8,11): encode + "
+                               "decode with data blocks {1,3,5} erased (block 7 read in place), host buffers "
+                               "(pinned, zero-copy kernels over PCIe) in and out",
+                   "job_bytes": r["job_bytes"], "per_rank_chunks": r["per_rank_chunks"], "world_size": ctx.world,
+                   "backend": ctx.backend, "parallelism": f"chunk-partition x{ctx.world}"},
+        # the kernels on HBM-resident copies of the same share (after the timed region)
+        "roofline": {"bound": "hbm", "achieved": dec_gbs if dom_dec else enc_gbs, "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s",
+                     "frac": (round((dec_gbs if dom_dec else enc_gbs) / PEAK_HBM_GBS, 4)
+                              if (dec_gbs if dom_dec else enc_gbs) else None),
+                     "traffic": None, "kernel": "decode (reassemble)" if dom_dec else "encode",
+                     "algorithmic_bytes_per_launch": r["dec_alg"] if dom_dec else r["enc_alg"],
+                     "avg_launch_ms": round((r["dec_avg_s"] if dom_dec else r["enc_avg_s"]) * 1e3, 4)},
+        "device_resident": {"encode_GBs": enc_gbs, "encode_gibs": round(r["bytes"] / r["enc_avg_s"] / GIB, 2),
+                            "decode_GBs": dec_gbs, "decode_gibs": round(r["bytes"] / r["dec_avg_s"] / GIB, 2),
+                            "encode_ms": round(r["enc_avg_s"] * 1e3, 4), "decode_ms": round(r["dec_avg_s"] * 1e3, 4)},
+        "staged": ({"encode_gibs": r["staged_encode_gibs"], "decode_gibs": r["staged_decode_gibs"],
+                    "path": "pageable numpy buffers staged through the library's pinned slabs (hipMemcpyAsync)"}
+                   if "staged_encode_gibs" in r else None),
+        "cpu_baseline": None,
+    }
+    if ctx.world == 1 and not args.no_cpu:
+        sample = c5_sizes()[:64]
+        res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, sample, C5_K, C5_M, C5_ERASED,
+                                           what=f"(encode + decode {{1,3,5}} erased) of the first 64 C5 chunks "
+                                                f"({sum(sample)} B), RS(8,3)")
+    print(json.dumps(res), flush=True)
+
+
+# ---------------------------------------------------------------- host-buffer rates (headline line)
 def _e2e_pass(eng, host, par, out, nchunks, steps):
     ed, B = enc_descs(nchunks, CHUNK, K, M)
     dd, sn, offs, _ = dec_descs(nchunks, CHUNK, K, M, B, host.ctypes.data, par.ctypes.data, ERASED)
@@ -512,6 +859,18 @@ def e2e_rate(eng, nchunks=1024, steps=3) -> dict:
             "sample": f"{nchunks} x 1 MiB RS(4,2), {steps} calls each; *_gibs: pageable numpy buffers, page-locked "
                       f"by the library per call; staged_*: the same, staged through pinned slabs; pinned_*: "
                       f"Engine.host_empty buffers; the kernels read / write locked or pinned host memory over PCIe"}
+
+
+def main(argv=None):
+    args = parse(argv)
+    rc = spawn_ranks(args, argv)
+    if rc is not None:
+        sys.exit(rc)
+    ctx = rank_context(args)
+    try:
+        {"c2c3": main_c2c3, "c4": main_c4, "c5": main_c5}[args.workload](args, ctx)
+    finally:
+        finish(ctx)
 
 
 if __name__ == "__main__":

@@ -150,7 +150,12 @@ int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
  * out + out_off.  Present primaries are copied, missing ones recovered.
  * `blocks` may be NULL, in which case block_offs are absolute addresses.
  * Every block must have B readable bytes here; sec_decode_batch_ex lifts that.
- * SEC_F_RECOVER: recover-only output instead (see the flag). */
+ * SEC_F_RECOVER: recover-only output instead (see the flag).
+ * Aliasing: a chunk's output range must not overlap any block of any chunk in
+ * the call (no in-place reassembly).  The kernels read blocks while other
+ * workgroups write `out`, and a SEC_F_HOST call joins present primaries on the
+ * host while the device writes the recovered rows, so an overlap gives
+ * unspecified bytes.  The library does not check this. */
 int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
                      const int32_t *sharenums, const uint64_t *block_offs,
                      const uint8_t *blocks, uint8_t *out, unsigned flags);

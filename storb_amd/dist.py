@@ -90,3 +90,16 @@ def sum_over_ranks(dist_mod, value: float, device=None) -> float:
                      device=f"cuda:{device}" if (device is not None and dist_mod.get_backend() == "nccl") else "cpu")
     dist_mod.all_reduce(t, op=dist_mod.ReduceOp.SUM)
     return float(t.item())
+
+
+def gather_counts(dist_mod, count: int, rank: int, world: int, device=None) -> list[int]:
+    """Every rank's `count`, in rank order (one all-reduce of a one-hot vector)."""
+    if dist_mod is None:
+        return [int(count)]
+    import torch
+
+    t = torch.zeros(world, dtype=torch.float64,
+                    device=f"cuda:{device}" if (device is not None and dist_mod.get_backend() == "nccl") else "cpu")
+    t[rank] = float(count)
+    dist_mod.all_reduce(t, op=dist_mod.ReduceOp.SUM)
+    return [int(x) for x in t.tolist()]

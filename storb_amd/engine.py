@@ -311,23 +311,10 @@ class Engine:
         buffers whose concatenation is the output."""
         n = len(items)
         gpu = []  # indices of chunks with a missing primary
-        for i, (k, m, blocks, sharenums, padlen) in enumerate(items):
-            if len(blocks) != k or len(sharenums) != k:
-                raise Error(_lib.strerror(_lib.SEC_ENBLOCKS))
-            B = len(blocks[0])
-            for b in blocks:
-                if len(b) != B:
-                    raise Error(_lib.strerror(_lib.SEC_EBLOCKLEN))
-            sn = [int(x) for x in sharenums]
-            if not (1 <= k <= m <= 256):
-                raise Error(_lib.strerror(_lib.SEC_EKM))
-            if any(x < 0 or x >= m for x in sn):
-                raise Error(_lib.strerror(_lib.SEC_ESHARENUM))
-            if len(set(sn)) != k:
-                raise Error(_lib.strerror(_lib.SEC_EDUPSHARE))
-            if not (0 <= padlen <= k * B):
-                raise Error(_lib.strerror(_lib.SEC_EPADLEN))
-            if any(x >= k for x in sn):
+        for i, item in enumerate(items):
+            check_decode_item(*item)
+            k, sharenums = item[0], item[3]
+            if any(int(x) >= k for x in sharenums):
                 gpu.append(i)
         # The GPU only recovers (SEC_F_RECOVER: zfec fec_decode's own output, the e missing
         # primaries, B bytes each, in primary order); the chunk is then the join of its present
@@ -380,6 +367,27 @@ class Engine:
             else:
                 parts.extend(views)
         return parts
+
+
+def check_decode_item(k: int, m: int, blocks, sharenums, padlen: int) -> None:
+    """zfec's decode preconditions for one chunk (the library's own checks, raised before any
+    GPU work): exactly k blocks and sharenums, equal lengths, 1 <= k <= m <= 256, sharenums in
+    [0, m) and distinct, 0 <= padlen <= k*B.  Raises Error."""
+    if len(blocks) != k or len(sharenums) != k:
+        raise Error(_lib.strerror(_lib.SEC_ENBLOCKS))
+    B = len(blocks[0]) if blocks else 0
+    for b in blocks:
+        if len(b) != B:
+            raise Error(_lib.strerror(_lib.SEC_EBLOCKLEN))
+    sn = [int(x) for x in sharenums]
+    if not (1 <= k <= m <= 256):
+        raise Error(_lib.strerror(_lib.SEC_EKM))
+    if any(x < 0 or x >= m for x in sn):
+        raise Error(_lib.strerror(_lib.SEC_ESHARENUM))
+    if len(set(sn)) != k:
+        raise Error(_lib.strerror(_lib.SEC_EDUPSHARE))
+    if not (0 <= padlen <= k * B):
+        raise Error(_lib.strerror(_lib.SEC_EPADLEN))
 
 
 # -- matrices (host arithmetic; no device needed) ------------------------------

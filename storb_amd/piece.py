@@ -33,6 +33,7 @@ import hashlib
 import logging
 import math
 import os
+import platform
 import threading
 import typing
 from collections import OrderedDict
@@ -45,7 +46,7 @@ from pydantic import BaseModel, ConfigDict, Field
 
 from .constants import MAX_PIECE_SIZE, MIN_PIECE_SIZE, PIECE_LENGTH_OFFSET, PIECE_LENGTH_SCALING
 from .easyfec import Decoder, Encoder, Error
-from .engine import get_engine
+from .engine import check_decode_item, get_engine
 
 logger = logging.getLogger(__name__)
 
@@ -76,6 +77,7 @@ STREAM_WINDOW_BYTES = 64 << 20  # chunk bytes per GPU call in the *_stream pipel
 # 256 / 512 MiB windows against 3.2-5.3 hashing on the host (profiles/r02_stream_rate.json).
 GPU_PIECE_IDS = True
 STREAM_WINDOW_IDS_BYTES = 256 << 20
+STREAM_WORKERS = 4  # worker threads (one engine each) shared by the *_stream pipelines
 
 
 class PieceType(IntEnum):  # piece.py:21-23
@@ -115,12 +117,14 @@ _pools_lock = threading.Lock()
 
 
 def _pool(name: str) -> ThreadPoolExecutor:
-    """Module thread pools: "hash" (hashlib SHA-1, which releases the GIL) and "stream" (one
-    worker that runs the *_stream pipelines' GPU calls on its own engine)."""
+    """Module thread pools: "hash" (hashlib SHA-1, which releases the GIL) and "stream"
+    (STREAM_WORKERS workers that run the *_stream pipelines' GPU calls, each on its own engine:
+    concurrent streams, e.g. downloads served on several request threads, do not queue behind
+    one another, and one stream keeps at most two windows in flight)."""
     with _pools_lock:
         p = _pools.get(name)
         if p is None:
-            n = 1 if name == "stream" else max(1, min(8, (os.cpu_count() or 2) - 1))
+            n = STREAM_WORKERS if name == "stream" else max(1, min(8, (os.cpu_count() or 2) - 1))
             p = _pools[name] = ThreadPoolExecutor(n, thread_name_prefix=f"storb_amd_{name}")
         return p
 
@@ -132,21 +136,70 @@ def _sha1_hex(b) -> str:
 class _PieceIdMemo:
     """Digests encode_chunk started for its pieces, keyed by the piece's bytes object.  A hit
     requires the very object (``is``), which the memo keeps alive while it holds it, so an id
-    cannot be reused under it; entries leave on first use or oldest-first past `max_bytes`."""
+    cannot be reused under it.
 
-    def __init__(self, max_bytes: int = 1 << 30):
+    Retention is bounded (the validator hashes a chunk's pieces right after its encode_chunk,
+    validator.py:1380 -> 1081, so nothing older is ever asked for): entries leave on first use,
+    when they belong to an encode_chunk call more than `keep_calls` calls ago, or oldest-first
+    past `max_bytes`.  A call whose pieces alone exceed `max_bytes` is not prefetched.  When
+    `idle_calls` calls in a row were evicted with none of their ids asked for (a caller that
+    does not hash, or hashes copies), prefetching pauses, except for one probe call in every
+    `probe_every`, so a caller that does not use the ids costs almost no hashing."""
+
+    def __init__(self, max_bytes: int = 128 << 20, keep_calls: int = 2, idle_calls: int = 4, probe_every: int = 64):
         self.max_bytes = max_bytes
-        self._d: OrderedDict = OrderedDict()
+        self.keep_calls = keep_calls
+        self.idle_calls = idle_calls
+        self.probe_every = probe_every
+        self._d: OrderedDict = OrderedDict()  # id -> (obj, future, call number)
         self._bytes = 0
+        self._call = 0
+        self._calls: dict[int, list[int]] = {}  # call number -> [entries held, ids taken]
+        self._idle = 0  # consecutive evicted calls with no id taken
         self._lock = threading.Lock()
 
-    def put(self, obj: bytes, fut: Future) -> None:
+    def _drop(self, c: int, taken: bool) -> None:
+        st = self._calls.get(c)
+        if st is None:
+            return
+        st[0] -= 1
+        st[1] += taken
+        if st[0] <= 0:  # that call's last entry
+            del self._calls[c]
+            self._idle = 0 if st[1] else self._idle + 1
+
+    def _evict_oldest(self) -> None:
+        _, (o, f, c) = self._d.popitem(last=False)
+        self._bytes -= len(o)
+        f.cancel()  # not started yet: no hashing for an id nobody will ask for
+        self._drop(c, False)
+
+    def begin(self, nbytes: int) -> int | None:
+        """Start an encode_chunk call's prefetch of `nbytes` of pieces: its call number, or None
+        when it should not prefetch."""
         with self._lock:
-            self._d[id(obj)] = (obj, fut)
+            self._call += 1
+            c = self._call
+            if nbytes > self.max_bytes:
+                return None
+            if self._idle >= self.idle_calls and c % self.probe_every:
+                return None
+            while self._d and (next(iter(self._d.values()))[2] <= c - self.keep_calls
+                               or self._bytes + nbytes > self.max_bytes):
+                self._evict_oldest()
+            return c
+
+    def put(self, obj: bytes, fut: Future, call: int) -> None:
+        with self._lock:
+            old = self._d.pop(id(obj), None)
+            if old is not None:  # the same object twice: counted once
+                self._bytes -= len(old[0])
+                self._drop(old[2], False)
+            self._d[id(obj)] = (obj, fut, call)
             self._bytes += len(obj)
+            self._calls.setdefault(call, [0, 0])[0] += 1
             while self._bytes > self.max_bytes and self._d:
-                _, (o, _f) = self._d.popitem(last=False)
-                self._bytes -= len(o)
+                self._evict_oldest()
 
     def take(self, obj):
         with self._lock:
@@ -155,7 +208,16 @@ class _PieceIdMemo:
                 return None
             del self._d[id(obj)]
             self._bytes -= len(obj)
-        return e[1].result()
+            self._idle = 0
+            self._drop(e[2], True)
+        try:
+            return e[1].result()
+        except Exception:  # noqa: BLE001 - cancelled or failed: hash here instead
+            return None
+
+    def held_bytes(self) -> int:
+        with self._lock:
+            return self._bytes
 
 
 _memo = _PieceIdMemo()
@@ -209,18 +271,59 @@ def _split(chunk, k: int, B: int) -> list[bytes]:
 # with PyBytes_FromStringAndSize(NULL, n).  The fills are numpy copies, which release the GIL,
 # so the pieces of a chunk are copied on the thread pool in parallel (and beside the GPU call)
 # instead of one after another by the caller's thread.
-_PyBytes_New = ctypes.pythonapi.PyBytes_FromStringAndSize
-_PyBytes_New.restype = ctypes.py_object
-_PyBytes_New.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
-_BYTES_DATA = bytes.__basicsize__ - 1  # offsetof(PyBytesObject, ob_sval)
+#
+# This relies on CPython's PyBytesObject layout (the buffer at offsetof(ob_sval) =
+# bytes.__basicsize__ - 1) and on id() being the object's address.  It is used only on CPython
+# and only after a self-test at import time confirms both (a pattern written through the view
+# reads back through the bytes object); anywhere else the pieces are filled into a bytearray and
+# converted with one copy (_FILL_IN_PLACE False).
+def _bytes_view_self_test() -> bool:
+    if platform.python_implementation() != "CPython":
+        return False
+    try:
+        new = ctypes.pythonapi.PyBytes_FromStringAndSize
+        new.restype = ctypes.py_object
+        new.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+        off = bytes.__basicsize__ - 1  # offsetof(PyBytesObject, ob_sval)
+        pat = bytes(range(251)) * 3
+        b = new(None, len(pat))
+        if not isinstance(b, bytes) or len(b) != len(pat):
+            return False
+        ctypes.memmove(id(b) + off, pat, len(pat))
+        return b == pat and b[len(pat):len(pat) + 1] == b""
+    except Exception:  # noqa: BLE001 - any surprise: use the portable path
+        return False
+
+
+_FILL_IN_PLACE = _bytes_view_self_test()
+if _FILL_IN_PLACE:
+    _PyBytes_New = ctypes.pythonapi.PyBytes_FromStringAndSize
+    _BYTES_DATA = bytes.__basicsize__ - 1
+
+
+class _PendingBytes:
+    """Portable stand-in: a bytearray filled by the pool, turned into bytes by finalize()."""
+
+    __slots__ = ("buf",)
+
+    def __init__(self, n: int):
+        self.buf = bytearray(n)
 
 
 def _new_bytes(n: int):
-    """(a new unshared bytes object of n bytes, a writable uint8 view of its buffer)."""
+    """(a new unshared bytes object of n bytes, or a _PendingBytes off CPython; a writable uint8
+    view of its buffer)."""
+    if not _FILL_IN_PLACE:
+        p = _PendingBytes(n)
+        return p, np.frombuffer(p.buf, dtype=np.uint8) if n else np.empty(0, np.uint8)
     b = _PyBytes_New(None, n)
     if n == 0:
         return b, np.empty(0, np.uint8)
     return b, np.frombuffer((ctypes.c_char * n).from_address(id(b) + _BYTES_DATA), dtype=np.uint8)
+
+
+def _finalize(piece):
+    return bytes(piece.buf) if type(piece) is _PendingBytes else piece
 
 
 def _fill(dst: np.ndarray, src: np.ndarray) -> None:
@@ -261,6 +364,8 @@ def _pieces_parallel(chunks: list, shapes: list, digests: bool = False):
             f += m
     for f in jobs:  # the pieces must be complete before anyone sees them (and buf is reused)
         f.result()
+    if not _FILL_IN_PLACE:
+        out = [[_finalize(p) for p in ps] for ps in out]
     return (out, ids) if digests else out
 
 
@@ -281,7 +386,8 @@ def encode_chunk(chunk: bytes, chunk_idx: int) -> EncodedChunk:
     logger.debug("[encode_chunk] chunk %d: %d bytes, piece_size = %d", chunk_idx, chunk_size, piece_size)
     k, m, B, padlen = chunk_shape(chunk_size)
     enc_ = Encoder(k, m)
-    if not PREFETCH_PIECE_IDS or chunk_size < PREFETCH_MIN_CHUNK:
+    call = _memo.begin(m * B) if PREFETCH_PIECE_IDS and chunk_size >= PREFETCH_MIN_CHUNK else None
+    if call is None:
         encoded_pieces = enc_.encode(chunk)
     else:  # piece ids hashed on the pool: data pieces beside the GPU call, parity right after
         hp = _pool("hash")
@@ -295,7 +401,7 @@ def encode_chunk(chunk: bytes, chunk_idx: int) -> EncodedChunk:
             futs += [hp.submit(_sha1_hex, b) for b in parity]
             encoded_pieces = prim + parity
         for b, f in zip(encoded_pieces, futs):
-            _memo.put(b, f)
+            _memo.put(b, f, call)
     enc = _build(chunk_idx, k, m, B, padlen, chunk_size, encoded_pieces)
     logger.debug("[encode_chunk] chunk %d: k=%d, m=%d, encoded %d blocks", chunk_idx, k, m, len(enc.pieces))
     return enc
@@ -414,22 +520,28 @@ def _decode_window(window: list, by_chunk: dict):
     those with a missing primary); that chunk's error is returned, to be raised in order."""
     items, err = [], None
     for chunk in window:
-        relevant = sorted(by_chunk.get(chunk.chunk_idx, []), key=lambda p: p.piece_idx)
-        if len(relevant) < chunk.k:
-            err = ValueError(f"Not enough pieces to reconstruct chunk {chunk.chunk_idx}")
+        try:
+            relevant = sorted(by_chunk.get(chunk.chunk_idx, []), key=lambda p: p.piece_idx)
+            if len(relevant) < chunk.k:
+                raise ValueError(f"Not enough pieces to reconstruct chunk {chunk.chunk_idx}")
+            chunk.pieces = relevant
+            blocks, sharenums = _sharenums(chunk, False)
+            B = len(blocks[0]) if blocks else 0
+            if not (1 <= chunk.k <= chunk.m <= 256) or not (0 <= chunk.padlen <= chunk.k * B):
+                # easyfec's own slicing semantics: the per-chunk path, decoded here
+                items.append(("bytes", decode_chunk(chunk)))
+                continue
+            item = (chunk.k, chunk.m, blocks, sharenums, chunk.padlen)
+            check_decode_item(*item)  # zfec's preconditions, before any chunk of the window decodes
+        except Exception as e:  # noqa: BLE001 - re-raised on the caller's thread after the chunks before it
+            err = e
             break
-        chunk.pieces = relevant
-        blocks, sharenums = _sharenums(chunk, False)
-        B = len(blocks[0]) if blocks else 0
-        if not (1 <= chunk.k <= chunk.m <= 256) or not (0 <= chunk.padlen <= chunk.k * B):
-            items.append(None)  # easyfec's own slicing semantics: the per-chunk path
-            continue
-        items.append((chunk.k, chunk.m, blocks, sharenums, chunk.padlen))
+        items.append(item)
     try:
-        batch = [it for it in items if it is not None]
+        batch = [it for it in items if it[0] != "bytes"]
         outs = iter(get_engine().decode_host_chunks(batch) if batch else [])
-        res = [next(outs) if it is not None else decode_chunk(ch) for it, ch in zip(items, window)]
-    except Exception as e:  # noqa: BLE001 - re-raised on the caller's thread, in order
+        res = [it[1] if it[0] == "bytes" else next(outs) for it in items]
+    except Exception as e:  # noqa: BLE001 - a device failure: nothing of the window is trusted
         return [], e
     return res, err
 
@@ -451,34 +563,58 @@ def reconstruct_data_stream(pieces: list[Piece], chunks: list[EncodedChunk], *,
     pool = _pool("stream")
     nxt = next(wins, None)
     fut = pool.submit(_decode_window, nxt, by_chunk) if nxt is not None else None
-    while fut is not None:
-        nxt = next(wins, None)
-        ahead = pool.submit(_decode_window, nxt, by_chunk) if nxt is not None else None
-        outs, err = fut.result()
-        yield from outs
-        if err is not None:
-            if ahead is not None:
-                ahead.cancel()
-            raise err
-        fut = ahead
+    ahead = None
+    try:
+        while fut is not None:
+            nxt = next(wins, None)
+            ahead = pool.submit(_decode_window, nxt, by_chunk) if nxt is not None else None
+            outs, err = fut.result()
+            yield from outs
+            if err is not None:
+                raise err
+            fut, ahead = ahead, None
+    finally:  # an error, or the consumer closed the stream early: drop the look-ahead window
+        for f in (fut, ahead):
+            if f is not None:
+                f.cancel()
+
+
+def _window_shapes(window: list):
+    """(shapes of the window's chunks up to the first one encode_chunk would reject, that
+    chunk's error or None): piece_length's ValueError for an empty chunk, easyfec's short middle
+    slice (zfec Error)."""
+    shapes = []
+    for c in window:
+        try:
+            n = len(c)
+            piece_length(n)
+            k, m, B, padlen = chunk_shape(n)
+            if k > 1 and (k - 1) * B > n:
+                raise Error("Precondition violation: Input blocks are required to be all the same length.")
+        except Exception as e:  # noqa: BLE001 - raised on the caller's thread after the chunks before it
+            return shapes, e
+        shapes.append((k, m, B, padlen))
+    return shapes, None
 
 
 def _encode_window(window: list, first_idx: int, piece_ids: bool):
     """Worker side of encode_chunks_stream: one batched GPU encode for the window (+ SHA-1 piece
-    ids on the hash pool: data pieces start before the GPU call, parity pieces after it)."""
-    if not piece_ids:
-        return [(c, None) for c in encode_chunks(window, first_idx)], None
+    ids: on the GPU for large pieces, else on the hash pool, data pieces starting before the GPU
+    call and parity pieces after it).  Returns (results, error): a chunk encode_chunk would
+    reject ends the window there, and the chunks before it are still encoded and returned."""
+    shapes, err = _window_shapes(window)
+    window = window[:len(shapes)]
+    if not window:
+        return [], err
     try:
-        shapes = []
-        for c in window:
-            piece_length(len(c))
-            shapes.append(chunk_shape(len(c)))
+        if not piece_ids:
+            return [(c, None) for c in encode_chunks(window, first_idx)], err
         hp = _pool("hash")
         if GPU_PIECE_IDS and min(B for (_, _, B, _) in shapes) >= PARALLEL_COPY_MIN:
             pieces, ids = _pieces_parallel(window, shapes, digests=True)
             out = [_build(first_idx + i, k, m, B, padlen, len(c), ps)
                    for i, (c, (k, m, B, padlen), ps) in enumerate(zip(window, shapes, pieces))]
-            return list(zip(out, ids)), None
+            return list(zip(out, ids)), err
         if min(B for (_, _, B, _) in shapes) >= PARALLEL_COPY_MIN:
             pieces = _pieces_parallel(window, shapes)
             futs = [[hp.submit(_sha1_hex, b) for b in ps] for ps in pieces]
@@ -491,8 +627,8 @@ def _encode_window(window: list, first_idx: int, piece_ids: bool):
                 fs.extend(hp.submit(_sha1_hex, b) for b in par)
         out = [_build(first_idx + i, k, m, B, padlen, len(c), ps)
                for i, (c, (k, m, B, padlen), ps) in enumerate(zip(window, shapes, pieces))]
-        return [(ec, [f.result() for f in fs]) for ec, fs in zip(out, futs)], None
-    except Exception as e:  # noqa: BLE001 - re-raised on the caller's thread
+        return [(ec, [f.result() for f in fs]) for ec, fs in zip(out, futs)], err
+    except Exception as e:  # noqa: BLE001 - a device failure: nothing of the window is trusted
         return [], e
 
 
@@ -513,15 +649,21 @@ def encode_chunks_stream(chunks: Iterable[bytes], first_chunk_idx: int = 0, *, p
         wb = STREAM_WINDOW_IDS_BYTES if piece_ids and GPU_PIECE_IDS else STREAM_WINDOW_BYTES
     pool = _pool("stream")
     idx = first_chunk_idx
-    pending = None
-    for win in _windows(chunks, wb, lambda c: max(len(c), 1)):
-        fut = pool.submit(_encode_window, win, idx, piece_ids)
-        idx += len(win)
+    pending = fut = None
+    try:
+        for win in _windows(chunks, wb, lambda c: max(len(c), 1)):
+            fut = pool.submit(_encode_window, win, idx, piece_ids)
+            idx += len(win)
+            if pending is not None:
+                yield from _emit(pending, piece_ids)
+            pending, fut = fut, None
         if pending is not None:
-            yield from _emit(pending, piece_ids)
-        pending = fut
-    if pending is not None:
-        yield from _emit(pending, piece_ids)
+            p, pending = pending, None
+            yield from _emit(p, piece_ids)
+    finally:  # an error, or the consumer closed the stream early: drop windows not yet started
+        for f in (pending, fut):
+            if f is not None:
+                f.cancel()
 
 
 def _emit(fut: Future, piece_ids: bool):

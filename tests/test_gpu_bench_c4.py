@@ -24,11 +24,11 @@ def test_bench_c4_share_and_full_job(world, rank):
         r = bench.c4_run(eng, None, rank, world, 0, "cuda:0", torch.cuda.synchronize, steps=2, warmup=1, keep=True)
         assert r["chunks"] == 65536 // world and r["lo"] == rank * (65536 // world)
         assert r["total_chunks"] == r["chunks"] and r["enc_launches"] == 2
-        n, k, m, B = bench.C4_CHUNK, bench.C4_K, bench.C4_M, r["B"]
-        assert B == 6554
+        n, k, m, B, ps = bench.C4_CHUNK, bench.C4_K, bench.C4_M, r["B"], r["pstride"]
+        assert B == 6554 and ps == 6656  # parity rows 128-byte aligned
         for ci in (0, 1, r["chunks"] // 2, r["chunks"] - 1):
             data = r["src"][ci * n:(ci + 1) * n].cpu().numpy().tobytes()
-            par = r["par"][ci * (m - k) * B:(ci + 1) * (m - k) * B].cpu().numpy().tobytes()
-            assert par == b"".join(cfec.easy_encode(data, k, m)[k:]), ci
+            par = r["par"][ci * (m - k) * ps:(ci + 1) * (m - k) * ps].cpu().numpy().reshape(m - k, ps)[:, :B]
+            assert par.tobytes() == b"".join(cfec.easy_encode(data, k, m)[k:]), ci
     finally:
         eng.close()

@@ -161,3 +161,135 @@ def test_encode_stream_piece_ids_large_pieces(gpu_ids, monkeypatch):
         assert min(len(b) for b in blocks) >= piece.PARALLEL_COPY_MIN
         assert [p.data for p in ec.pieces] == blocks
         assert ids == [hashlib.sha1(b).hexdigest() for b in blocks]
+
+
+def test_validator_bytearray_chunks():
+    """The validator hands encode_chunk a bytearray: `copy.copy(buffer[:chunk_size])` of its
+    read buffer (/root/reference/storb/validator/validator.py:1356-1380).  The same objects
+    through encode_chunk, encode_chunks and encode_chunks_stream (with and without ids), small
+    and large pieces: pieces against the oracle, ids against hashlib."""
+    import copy
+
+    rng = random.Random(1356)
+    buffer = bytearray(rng.randbytes(12 << 20))
+    sizes = [4096 + 3, 256 << 10, 700_000, 1 << 20, 3 << 20, (5 << 20) + 17]
+    chunks, off = [], 0
+    for n in sizes:
+        chunks.append(copy.copy(buffer[off:off + n]))
+        off += n
+    assert all(type(c) is bytearray for c in chunks)
+    want = []
+    for c in chunks:
+        k, m, _, _ = piece.chunk_shape(len(c))
+        want.append(cfec.easy_encode(bytes(c), k, m))
+    for i, c in enumerate(chunks):
+        ec = piece.encode_chunk(c, i)
+        assert [p.data for p in ec.pieces] == want[i], i
+        assert all(type(p.data) is bytes for p in ec.pieces)
+        assert [piece.piece_hash(p.data) for p in ec.pieces] == [hashlib.sha1(b).hexdigest() for b in want[i]]
+    for i, ec in enumerate(piece.encode_chunks(chunks)):
+        assert ec.chunk_idx == i and [p.data for p in ec.pieces] == want[i], i
+    for i, ec in enumerate(piece.encode_chunks_stream(iter(chunks), window_bytes=4 << 20)):
+        assert [p.data for p in ec.pieces] == want[i], i
+    got = list(piece.encode_chunks_stream(iter(chunks), piece_ids=True, window_bytes=6 << 20))
+    for i, (ec, ids) in enumerate(got):
+        assert [p.data for p in ec.pieces] == want[i], i
+        assert ids == [hashlib.sha1(b).hexdigest() for b in want[i]], i
+    # decoding the bytearray-born pieces with data pieces lost gives the bytearray's bytes back
+    ecs = piece.encode_chunks(chunks)
+    pieces = [p for ec in ecs for p in ec.pieces if p.piece_idx != 0 or ec.k == 1]
+    metas = [ec.model_copy(update={"pieces": None}) for ec in ecs]
+    assert piece.reconstruct_data(pieces, metas) == b"".join(bytes(c) for c in chunks)
+
+
+def _stream_fixture(seed, n_chunks=10, size=600_000):
+    rng = random.Random(seed)
+    objs = [rng.randbytes(size + 97 * i) for i in range(n_chunks)]
+    encoded = [piece.encode_chunk(o, i) for i, o in enumerate(objs)]
+    chunks = [e.model_copy(update={"pieces": None}) for e in encoded]
+    return objs, encoded, chunks
+
+
+@pytest.mark.parametrize("fault", ["duplicate_idx", "truncated_piece", "bad_sharenum"])
+def test_reconstruct_stream_precondition_error_after_prefix(fault):
+    """A zfec precondition failure in the middle of a window: every chunk before
+    the bad one is still yielded, then the error is raised, as the reference's per-chunk loop
+    does (piece.py:246-263)."""
+    objs, encoded, chunks = _stream_fixture(11)
+    bad = 6
+    pieces = []
+    for e in encoded:
+        ps = [p for p in e.pieces if p.piece_idx != 0]  # data piece 0 lost: GPU recovery everywhere
+        if e.chunk_idx == bad:
+            if fault == "duplicate_idx":
+                ps = [ps[0].model_copy(), *ps[:e.k - 1]]  # k pieces, two with the same piece_idx
+            elif fault == "truncated_piece":
+                ps[1] = ps[1].model_copy(update={"data": ps[1].data[:-1]})
+            else:
+                ps[1] = ps[1].model_copy(update={"piece_idx": e.m + 5})
+        pieces.extend(ps)
+    got = []
+    with pytest.raises((piece.Error, ValueError)):
+        for b in piece.reconstruct_data_stream(pieces, chunks, window_bytes=64 << 20):  # one window
+            got.append(b)
+    assert got == objs[:bad]
+
+
+def test_encode_stream_error_after_prefix():
+    rng = random.Random(12)
+    objs = [rng.randbytes(300_000 + i) for i in range(7)]
+    objs[4] = b""  # piece_length(0): the reference's ValueError (math domain error)
+    got = []
+    with pytest.raises(ValueError):
+        for ec in piece.encode_chunks_stream(iter(objs), window_bytes=64 << 20):
+            got.append(ec)
+    assert [len(ec.pieces) for ec in got] == [piece.chunk_shape(len(o))[1] for o in objs[:4]]
+    for ec, o in zip(got, objs):
+        assert [p.data for p in ec.pieces] == cfec.easy_encode(o, ec.k, ec.m)
+
+
+def test_streams_closed_early_and_concurrent():
+    """Consumers that stop early (client disconnect) do not hold up other streams, and several
+    streams on request threads run side by side."""
+    import threading
+
+    objs, encoded, chunks = _stream_fixture(13, n_chunks=24, size=1 << 20)
+    pieces = [p for e in encoded for p in e.pieces if p.piece_idx != 1]
+    for _ in range(3):
+        it = piece.reconstruct_data_stream(pieces, chunks, window_bytes=2 << 20)
+        assert next(it) == objs[0]
+        it.close()
+        it2 = piece.encode_chunks_stream(iter(objs), window_bytes=2 << 20)
+        assert next(it2).model_dump() == encoded[0].model_dump()
+        it2.close()
+    results, errs = {}, []
+
+    def run(t):
+        try:
+            results[t] = b"".join(piece.reconstruct_data_stream(pieces, chunks, window_bytes=3 << 20))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(t,)) for t in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not errs and len(results) == 4
+    assert all(v == b"".join(objs) for v in results.values())
+
+
+def test_piece_id_memo_bounded_without_piece_hash():
+    """A caller that never asks for piece ids (ADVICE / VERDICT r02): encode_chunk keeps at most
+    the memo's cap (and its last `keep_calls` calls) of piece bytes alive, and stops prefetching
+    once whole calls go unused; the ids are right again as soon as the caller hashes."""
+    memo = piece._memo
+    chunk_objs = [random.Random(40 + i).randbytes(1 << 20) for i in range(3)]
+    per_call = sum(len(p.data) for p in piece.encode_chunk(chunk_objs[0], 0).pieces)
+    for i in range(40):
+        piece.encode_chunk(chunk_objs[i % 3], i)
+        held = memo.held_bytes()
+        assert held <= memo.max_bytes and held <= memo.keep_calls * per_call, (i, held)
+    assert memo._idle >= memo.idle_calls  # prefetch paused
+    info = piece.encode_chunk(chunk_objs[0], 0)
+    assert [piece.piece_hash(p.data) for p in info.pieces] == [hashlib.sha1(p.data).hexdigest() for p in info.pieces]
