@@ -226,7 +226,7 @@ def test_reconstruct_stream_precondition_error_after_prefix(fault):
             elif fault == "truncated_piece":
                 ps[1] = ps[1].model_copy(update={"data": ps[1].data[:-1]})
             else:
-                ps[1] = ps[1].model_copy(update={"piece_idx": e.m + 5})
+                ps[1] = ps[1].model_copy(update={"piece_idx": -1})  # sorts first: sharenum -1
         pieces.extend(ps)
     got = []
     with pytest.raises((piece.Error, ValueError)):
