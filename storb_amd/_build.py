@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libstorbec.so")
 INCLUDE = os.path.join(ROOT, "include")
-SOURCES = ["kernels.hip", "kernels_mfma.hip", "kernels_xb.hip", "kernels_bs.hip", "bignum.hip", "api.cpp"]
+SOURCES = ["kernels.hip", "kernels_bs.hip", "bignum.hip", "api.cpp"]
 HEADERS = ["kernels.hpp", "bignum.hpp", "gf_host.hpp", "gf_const.hpp", "copy_pool.hpp"]
 ARCH = os.environ.get("STORB_EC_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

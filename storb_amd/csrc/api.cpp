@@ -129,9 +129,8 @@ size_t env_size(const char *name, size_t dflt)
 struct Group {
     int rows, U, lanes, wide;  // wide: k > kBatchVecs / U, blocks loaded in several batches
     uint32_t first, count;
-    int mfma = 0;              // 1: sec_encode_mfma_kernel<G = U, TILES = rows> (encode, k = 32 * G);
-                               // 2: sec_encode_xb_kernel of shape `rows`, W = U (encode)
-                               // 3: sec_encode_bs_kernel of shape `rows`, row group U (encode)
+    int mfma = 0;              // bin kind.  Encode: 3 = sec_encode_bs_kernel of shape `rows`, row group U;
+                               // decode: the small-batch variant's batch (dec_small_kb), or 0
 };
 
 // One launch unit: all chunks (device mode) or one slab of chunks (host mode).
@@ -139,7 +138,6 @@ struct SubPlan {
     int64_t c0 = 0, c1 = 0;  // chunk range
     std::vector<Group> groups;
     size_t off_desc = 0, off_tiles = 0, off_tail = 0, off_soff = 0, off_srow = 0, off_mrow = 0, off_savail = 0;
-    size_t off_mtab = 0;  // encode: MFMA bit-matrix tables (shared by every sub-plan)
     uint32_t ntail = 0;
     uint64_t in_bytes = 0, out_bytes = 0;  // dense slab sizes (host mode)
     size_t off_msgs = 0;                   // messages of this unit (SHA-1, bignum)
@@ -344,64 +342,14 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
     }
 }
 
-// Bit-sliced MFMA encode (kernels_mfma.hip) for k = 32 or 64: whole 128-position groups below
-// `valid` in tiles of sec::kMfmaTile positions, one tile per row group of mfma_group_rows(G)
-// parity rows; add_mfma_work returns where the MFMA range ends (the VALU tiles start there).
-// Off unless SEC_MFMA=1: in-process A/Bs measured it below the v_perm kernels on every wide
-// shape (zfec(32,48) 1.75-2.32 against 2.25-2.60 TB/s, zfec(64,96) 0.76-1.07 against 1.24-1.33;
-// profiles/r02_mfma_ab.jsonl).
-bool mfma_eligible(int k, int m)
-{
-    const char *e = getenv("SEC_MFMA");
-    if (!e || e[0] != '1')
-        return false;
-    return m > k && (k == 32 || k == 64);
-}
-
-uint64_t add_mfma_work(Bins &bins, uint32_t chunk, int64_t valid, int k, int m)
-{
-    const uint64_t vm = valid > 0 ? (uint64_t)valid / sec::kMfmaGroup * sec::kMfmaGroup : 0;
-    if (vm == 0)
-        return 0;
-    const int G = k / 32, p = m - k, RGR = sec::mfma_group_rows(G);
-    for (int r0 = 0; r0 < p; r0 += RGR) {
-        const int tiles = (std::min(RGR, p - r0) + 3) / 4;
-        auto &bin = bins[{1, tiles, G, 256, 0}];
-        for (uint64_t t0 = 0; t0 < vm; t0 += sec::kMfmaTile)
-            bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
-    }
-    return vm;
-}
-
-// Compile-time-matrix encode (kernels_xb.hip) for the shapes it is built for ((64,96), (32,48)):
-// positions [0, sec_xb_end(valid)) in 256-lane tiles of 1024 * W positions, all parity rows
-// per tile; add_xb_work returns where its range ends (sec_encode_kernel's tiles start there,
-// as after add_mfma_work).  Dwords per lane: 2 for (32,48), 1 for (64,96), whose 32
-// accumulators per dword leave no registers for a second (profiles/r02_xb_ab.jsonl: the other
-// width measured -1.5 % / -5 %).  SEC_XB=0 turns it off, SEC_XB_W (1 or 2) forces the width;
-// both read per plan build.
-int xb_shape(int k, int m)
-{
-    const char *e = getenv("SEC_XB");
-    if (e && e[0] == '0')
-        return -1;
-    return sec_xb_shape(k, m);
-}
-
-int xb_width(int shape)
-{
-    const size_t w = env_size("SEC_XB_W", 0);
-    return w == 1 || w == 2 ? (int)w : shape == 1 ? 2 : 1;
-}
-
 // Bit-sliced compile-time-matrix encode (kernels_bs.hip) for the shapes it is built for
 // (C4's zfec(10,14), C5's (8,11), the policy's (8,12), (16,24), (32,48), (64,96)): every
 // position [0, B) of a chunk with B >= 16, ragged end included, so such a chunk gets no
 // sec_encode_kernel tile.  Tiles of SEC_BS_LANES lanes (default 256 = 8 KiB of each block).
 // A shape of several row groups ((64,96): 2 x 16 rows) runs them in one launch, a run of 8
 // tiles of each group in turn, so the tiles that read the same blocks share an XCD's L2
-// (SEC_BS_SPLIT=1: one launch per group instead).  SEC_BS=0 turns the kernel off (then xb /
-// v_perm as before), SEC_BS=1 uses it for every shape it has; SEC_BS_R8=1 takes (32,48) in two
+// (SEC_BS_SPLIT=1: one launch per group instead).  SEC_BS=0 turns the kernel off (then the
+// v_perm rows), SEC_BS=1 uses it for every shape it has; SEC_BS_R8=1 takes (32,48) in two
 // groups of 8 rows.  All read per plan build.
 constexpr int kBsAllGroups = 99;  // Group::U of an interleaved launch of every row group
 
@@ -454,16 +402,6 @@ void bs_interleave(int shape, const std::vector<sec::Tile> &pos, std::vector<sec
     }
 }
 
-uint64_t add_xb_work(Bins &bins, uint32_t chunk, int64_t valid, int shape)
-{
-    const uint64_t vx = valid > 0 ? sec_xb_end((uint32_t)valid) : 0;
-    const int W = xb_width(shape);
-    auto &bin = bins[{2, shape, W, 256, 0}];
-    for (uint64_t t0 = 0; t0 < vx; t0 += (uint64_t)sec::kLanes * 4 * W)
-        bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
-    return vx;
-}
-
 // XCD order.  Workgroup b of a launch is dispatched to XCD b % 8, so with the tiles in chunk
 // order the eight XCDs interleave over the same region.  In XCD order each XCD instead walks
 // one contiguous eighth of the group's tiles: tile(b) = start(b % 8) + b / 8 (bijective for
@@ -478,7 +416,7 @@ uint64_t add_xb_work(Bins &bins, uint32_t chunk, int64_t valid, int shape)
 
 bool use_xcd_order(bool decode, const Group &g)
 {
-    if (g.mfma)
+    if (g.mfma == 3)
         return false;
     if (SEC_XCD_ORDER >= 0)
         return SEC_XCD_ORDER == 1;
@@ -829,18 +767,6 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
     }
     Image img;
     plan.subs.clear();
-    // bit-matrix tables of the MFMA encode, one per (k, m) shape it serves
-    std::map<std::pair<int, int>, uint32_t> mtab_of;  // -> offset in 16 B units
-    std::vector<uint8_t> mblob;
-    for (int64_t i = 0; i < nchunks; ++i) {
-        const int k = chunks[i].k, m = chunks[i].m;
-        if (mfma_eligible(k, m) && !mtab_of.count({k, m})) {
-            const std::vector<uint8_t> t = sec::mfma_table(k, m);
-            mtab_of[{k, m}] = (uint32_t)(mblob.size() / 16);
-            mblob.insert(mblob.end(), t.begin(), t.end());
-        }
-    }
-    const size_t off_mtab = mblob.empty() ? 0 : img.put(mblob.data(), mblob.size());
     bool narrow = true;  // every block of the batch >= 64 KiB: one-wave encode tiles (full_lanes)
     for (int64_t i = 0; i < nchunks && narrow; ++i)
         if (chunks[i].m > chunks[i].k && enc_B(chunks[i]) < ((uint64_t)64 << 10))
@@ -848,7 +774,6 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
     uint64_t dig = 0;
     for (auto [c0, c1] : ranges) {
         SubPlan sp;
-        sp.off_mtab = off_mtab;
         sp.c0 = c0;
         sp.c1 = c1;
         sp.dig_first = dig;
@@ -870,8 +795,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             d.p = (uint32_t)p;
             d.tab = tab_of[i];
             d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)B));
-            auto mt = mtab_of.find({c.k, c.m});
-            d.pad = mt != mtab_of.end() ? mt->second : 0;
+            d.pad = 0;
             if (digest) {  // data blocks from the input (padding synthesised), then parity
                 for (int j = 0; j < c.k; ++j) {
                     const int64_t av = (int64_t)c.n - (int64_t)j * (int64_t)B;
@@ -885,16 +809,11 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             }
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
-            const int bs = p > 0 && mt == mtab_of.end() ? bs_shape(c.k, c.m, B) : -1;
-            if (bs >= 0) {
+            const int bs = p > 0 ? bs_shape(c.k, c.m, B) : -1;
+            if (bs >= 0)
                 add_bs_work(bins, (uint32_t)(i - c0), B, bs);
-            } else if (p > 0) {
-                const int xs = mt == mtab_of.end() ? xb_shape(c.k, c.m) : -1;
-                const uint64_t start = mt != mtab_of.end() ? add_mfma_work(bins, (uint32_t)(i - c0), valid, c.k, c.m)
-                                       : xs >= 0             ? add_xb_work(bins, (uint32_t)(i - c0), valid, xs)
-                                                             : 0;
-                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, start, narrow);
-            }
+            else if (p > 0)
+                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, 0, narrow);
         }
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles, false);
@@ -922,17 +841,11 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
     for (const Group &g : sp.groups) {
-        int e = g.mfma == 1 ? sec_launch_encode_mfma(g.U, g.rows, in, par, dd, dt + g.first, g.count,
-                                                     plan.meta.as<uint8_t>(sp.off_mtab), s)
-                : g.mfma == 2 ? sec_launch_encode_xb(g.rows, g.U, in, par, dd, dt + g.first, g.count, s)
-                : g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsAllGroups ? -1 : g.U, g.lanes, in, par, dd,
-                                                     dt + g.first, g.count, s)
-                              : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
+        int e = g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsAllGroups ? -1 : g.U, g.lanes, in, par, dd,
+                                                   dt + g.first, g.count, s)
+                            : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
         if (e)
-            return hip_fail((hipError_t)e, g.mfma == 1   ? "sec_encode_mfma_kernel"
-                                           : g.mfma == 2 ? "sec_encode_xb_kernel"
-                                           : g.mfma == 3 ? "sec_encode_bs_kernel"
-                                                         : "sec_encode_kernel");
+            return hip_fail((hipError_t)e, g.mfma == 3 ? "sec_encode_bs_kernel" : "sec_encode_kernel");
     }
     if (sp.ntail) {
         int e = sec_launch_encode_tail(in, par, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs, s);

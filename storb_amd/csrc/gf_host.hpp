@@ -104,41 +104,6 @@ inline std::vector<uint8_t> encode_matrix(int k, int m)
     return enc;
 }
 
-// A operands of the bit-sliced integer-MFMA encode (kernels_mfma.hip) for k = 32 * G.
-// The GF(2^8) products are GF(2)-linear: bit b of sum_j c_rj * x_j is the XOR over (j, s) of
-// x_j's bit s times bit b of c_rj * 2^s.  That is one 0/1 matrix of 8p x 8k bits, and the XOR
-// is the parity of an integer sum, which v_mfma_i32_32x32x32_i8 computes.  Layout
-// [row group][tile (kMfmaTiles(G))][K-step st = 8g + s][lane 0..63][16 bytes]: lane
-// (r = l & 31, h = l >> 5) holds A[row r][k = 16h + j] (j = 0..15, the gfx950 i8 map, checked
-// by tools/mfma_i8_probe.hip), i.e. block 32g + 16h + j, bit s.  Tile-local row r carries
-// bit b = 4((r >> 3) & 1) + (r & 3) of parity row 4t + 2((r >> 2) & 1) + (r >> 4) of the row
-// group, so the 16 accumulator registers of a lane hold two whole parity bytes.
-constexpr int mfma_tiles(int G) { return G == 1 ? 4 : 2; }  // 32-row tiles per row group
-constexpr int mfma_group_rows(int G) { return 4 * mfma_tiles(G); }
-
-inline std::vector<uint8_t> mfma_table(int k, int m)
-{
-    const Gf &g = gf();
-    const std::vector<uint8_t> enc = encode_matrix(k, m);
-    const int G = k / 32, p = m - k, T = mfma_tiles(G), RGR = mfma_group_rows(G), S = 8 * G;
-    const int ngroups = (p + RGR - 1) / RGR;
-    std::vector<uint8_t> tab((size_t)ngroups * T * S * 64 * 16, 0);
-    size_t o = 0;
-    for (int rg = 0; rg < ngroups; ++rg)
-        for (int t = 0; t < T; ++t)
-            for (int st = 0; st < S; ++st)
-                for (int l = 0; l < 64; ++l)
-                    for (int j = 0; j < 16; ++j, ++o) {
-                        const int r = l & 31, h = l >> 5, gb = st / 8, s = st % 8;
-                        const int b = 4 * ((r >> 3) & 1) + (r & 3);
-                        const int rho = rg * RGR + 4 * t + 2 * ((r >> 2) & 1) + (r >> 4);
-                        const int blk = 32 * gb + 16 * h + j;
-                        if (rho < p && blk < k)
-                            tab[o] = (g.mul(enc[(size_t)(k + rho) * k + blk], (uint8_t)(1u << s)) >> b) & 1;
-                    }
-    return tab;
-}
-
 // zfec _fecmodule.c normalisation: each primary moved into its own slot.
 // perm[i] = caller's position of the block now in slot i.
 inline void normalise_slots(int k, std::vector<int> &idx, std::vector<int> &perm)

@@ -31,12 +31,6 @@ constexpr int kBatchVecs = 16;      // 16 B vectors a lane loads per batch (SEC_
 #endif
 constexpr int max_lanes(int rows, int U) { return U != 1 ? kLanes : (rows > 4 ? SEC_LB_WIDE_ROWS : 1024); }
 
-// Bit-sliced MFMA encode (kernels_mfma.hip, k = 32 * G): one wave covers groups of this many
-// positions, kMfmaGroupsPerWave of them per tile (4 waves), so a tile spans kMfmaTile.
-constexpr int kMfmaGroup = 128;
-constexpr int kMfmaGroupsPerWave = 16;
-constexpr int kMfmaTile = kMfmaGroup * 4 * kMfmaGroupsPerWave;  // 8192 positions
-
 // One encode chunk, device copy (48 B).
 struct EncDesc {
     uint64_t in_off;      // chunk start in `in`
@@ -47,7 +41,7 @@ struct EncDesc {
     uint32_t p;           // parity blocks (m - k)
     uint32_t tab;         // dword offset of this chunk's tables, layout [j][r][5]
     uint32_t valid;       // n - (k-1)*B: bytes of the last (zero-padded) data block
-    uint32_t pad;         // MFMA encode: offset (16 B units) of the chunk's bit-matrix tables
+    uint32_t pad;
 };
 
 // One decode chunk, device copy (40 B).
@@ -112,16 +106,6 @@ int sec_launch_expand(const uint8_t *coef, uint32_t ncoef, uint32_t *tabs, void 
 int sec_launch_encode(int rows, int U, int wide, int lanes, const uint8_t *in, uint8_t *par,
                       const sec::EncDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
                       void *stream);
-// k = 32 * G (G = 1, 2), `tiles` 32-row accumulator tiles per row group (G = 1: 1..4, G = 2: 1..2)
-int sec_launch_encode_mfma(int G, int tiles, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
-                           const sec::Tile *t, uint32_t ntiles, const void *mtabs, void *stream);
-// Compile-time-matrix encode (kernels_xb.hip) for the shapes sec_xb_shape knows (else -1):
-// positions [0, sec_xb_end(valid)) of each chunk, all parity rows per tile, W = 1 or 2 dwords
-// per lane, 256-lane tiles of 1024 * W positions
-int sec_xb_shape(int k, int m);
-uint32_t sec_xb_end(uint32_t valid);
-int sec_launch_encode_xb(int shape, int W, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
-                         const sec::Tile *t, uint32_t ntiles, void *stream);
 // Bit-sliced compile-time-matrix encode (kernels_bs.hip) for the shapes sec_bs_shape knows
 // (else -1; rows = 0: the first kernel of that (k, m), else the one of `rows` rows per group):
 // all of [0, B) of chunks with B >= 16, row group `group` of sec_bs_groups(shape) (-1: every

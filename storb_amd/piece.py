@@ -667,8 +667,9 @@ def encode_chunks_stream(chunks: Iterable[bytes], first_chunk_idx: int = 0, *, p
 
 
 def _emit(fut: Future, piece_ids: bool):
+    """A window's results in order, then its error (raised after the chunks before it)."""
     outs, err = fut.result()
-    if err is not None:
-        raise err
     for ec, ids in outs:
         yield (ec, ids) if piece_ids else ec
+    if err is not None:
+        raise err

@@ -554,19 +554,16 @@ def test_largest_block_size(engine):
         engine.encode_batch(d2, 1, 1)  # rejected before any address is touched
 
 
-@pytest.mark.parametrize("xb_w", ["1", "2", "off"])
-def test_encode_compile_time_matrix_shapes(xb_w, monkeypatch):
-    """(64,96) and (32,48) encode through kernels_xb.hip (compile-time zfec matrix, SEC_XB_W
-    dwords per lane) for [0, valid rounded down to 16) and sec_encode_kernel for the rest,
-    against the oracle: ragged tails, padded last blocks, chunks too small for any XB tile,
-    unaligned B, mixed with other shapes in one batch; "off" (SEC_XB=0) is the v_perm path."""
+@pytest.mark.parametrize("bs", ["default", "off"])
+def test_encode_wide_policy_shapes(bs, monkeypatch):
+    """The policy's wide shapes (64,96), (32,48), (16,24) (files of 1 GiB to 1 TiB, SURVEY
+    Appendix B) through the default plan (the bit-sliced compile-time-matrix kernel) and with it
+    off (SEC_BS=0: the v_perm rows), against the oracle: ragged tails, padded last blocks, tiny
+    and unaligned B, mixed with other shapes in one batch."""
     from storb_amd.engine import Engine
 
-    monkeypatch.setenv("SEC_BS", "0")  # the bit-sliced kernel would take these shapes first
-    if xb_w == "off":
-        monkeypatch.setenv("SEC_XB", "0")
-    else:
-        monkeypatch.setenv("SEC_XB_W", xb_w)
+    if bs == "off":
+        monkeypatch.setenv("SEC_BS", "0")
     eng = Engine(0)  # its own plan cache: the knobs are read when a plan is built
     rng = random.Random(96)
     chunks, km = [], []
@@ -578,5 +575,5 @@ def test_encode_compile_time_matrix_shapes(xb_w, monkeypatch):
             km.append((k, m))
     par = eng.encode_host(chunks, km)
     for c, (k, m), p in zip(chunks, km, par):
-        assert p == oracle_parity(c, k, m), (xb_w, k, m, len(c))
+        assert p == oracle_parity(c, k, m), (bs, k, m, len(c))
     eng.close()

@@ -59,8 +59,6 @@ VARIANTS = {
     "sha1d4": {"SEC_SHA1_DEPTH": 4},
     "lb256p8": {"SEC_LB_WIDE_ROWS": 256, "SEC_PAIR_ROWS": 8},
     "lb512p8": {"SEC_LB_WIDE_ROWS": 512, "SEC_PAIR_ROWS": 8},
-    # bit-sliced MFMA encode (kernels_mfma.hip): one wave per SIMD with the q steps unrolled
-    "mfw1": {"SEC_MFMA_WAVES": 1, "SEC_MFMA_QU": 4},
     # table dwords 1 and 3 from a per-wave LDS copy instead of v_mov from SGPRs (SEC_LDS_TAB)
     # (default 2: encode kernels of 8-row groups only; 1: every tile kernel; 0: none)
     "ldstab": {"SEC_LDS_TAB": 1},
