@@ -262,6 +262,12 @@ int sec_host_unregister(sec_ctx *ctx, void *hptr);
 /* SEC_F_HOST encode / decode calls so far on this context: zero-copy on the caller's pinned
  * buffers, zero-copy on pages the call locked itself, and staged. */
 int sec_ctx_host_paths(sec_ctx *ctx, int64_t *zero_copy, int64_t *registered, int64_t *staged);
+/* Chunks with a lost data block decoded so far on this context, by method: `syndrome` (the
+ * wide-decode path: bit-sliced syndromes of the present parity rows, then the e x e solve) and
+ * `direct` (the decode matrix rows over all k blocks).  Which one a chunk takes is the library's
+ * choice (cost estimate; SEC_SYN=0 / 1 in the environment turns the syndrome path off / forces
+ * it where it applies); the bytes are the same. */
+int sec_ctx_decode_paths(sec_ctx *ctx, int64_t *syndrome, int64_t *direct);
 /* kind: 0 host->device, 1 device->host, 2 device->device; synchronous on the ctx stream */
 int sec_memcpy(sec_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
 int sec_memset(sec_ctx *ctx, void *dptr, int value, size_t bytes);

@@ -147,6 +147,13 @@ struct SubPlan {
     uint32_t nsegs = 0, max_seg = 0;       // segment count; most segments of one message
     uint64_t dig_first = 0;                // first digest slot of this unit
     uint64_t dig_off = 0;                  // host mode: digests' offset in the slab output
+    // syndrome decodes (decode): phase 1 launches (bit-sliced syndromes, one per shape), phase 2
+    // groups (sec_decode_kernel over the syndrome rows) and their tail items
+    std::vector<std::pair<int, std::pair<uint32_t, uint32_t>>> syn1;  // (shape, (first, count)) in syn tiles
+    std::vector<Group> groups2;
+    size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_tiles2 = 0, off_tail2 = 0;
+    uint32_t ntail2 = 0;
+    uint64_t syn_bytes = 0;  // syndrome scratch of this unit
 };
 
 struct Plan {
@@ -155,6 +162,7 @@ struct Plan {
     std::vector<SubPlan> subs;
     DevBuf meta;  // device copy of the metadata image of every sub-plan
     bool valid = false;
+    int64_t nsyn = 0, ndirect = 0;  // decode: chunks with a lost primary, by method
 };
 
 // Device-resident GF coefficient tables (5 dwords per coefficient), keyed by
@@ -259,6 +267,44 @@ int dec_copy_kb(int k)
 {
     const size_t v = env_size("SEC_DEC_COPY_KB", 0);
     return (v == 4 || v == 8) && (size_t)k <= v ? (int)v : 0;
+}
+
+// Syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel, then sec_decode_kernel on the e
+// syndrome rows) for a chunk that lost e data blocks, when its shape has a bit-sliced kernel.
+// VALU estimate per 4 byte positions: the direct decode runs ceil(e / 8) v_perm row groups over
+// all k slots (5 selector ops + 4.5 per row and slot); the syndrome path runs the bit-sliced rows
+// of every NR-row parity group that holds a present row over the k - e present data blocks
+// (6 transpose + 2.75 subset + NR row ops), transposes the e syndromes back (6) and solves with
+// v_perm rows over the e syndromes.  It is used when it needs under SEC_SYN_RATIO (default 0.75)
+// of the direct path's VALU (it also moves 2 e B more bytes).  SEC_SYN=0 / 1 turns it off /
+// forces it wherever it applies; both read per plan build.
+double vperm_ops(int rows, int slots)
+{
+    double v = 0;
+    for (int r = 0; r < rows; r += sec::kMaxRows)
+        v += 5 + 4.5 * std::min(sec::kMaxRows, rows - r);
+    return v * slots;
+}
+
+int syn_choice(const sec_dec_chunk &c, const int *idx, int e)
+{
+    const char *env = getenv("SEC_SYN");
+    if (env && env[0] == '0')
+        return -1;
+    const int sh = sec_syn_shape(c.k, c.m);
+    if (sh < 0 || e < 1 || c.B < 16 || c.B > 0xFFFFFFFFull - 8192 || c.padlen >= c.B)
+        return -1;
+    if (env && env[0] == '1')
+        return sh;
+    const int k = c.k, NR = sec_bs_rows(sh);
+    uint64_t touched = 0;  // parity row groups that hold a present row
+    for (int s = 0; s < k; ++s)
+        if (idx[s] >= k)
+            touched |= 1ull << ((idx[s] - k) / NR);
+    const double syn = __builtin_popcountll(touched) * (k - e) * (8.75 + NR) + 6.0 * e + vperm_ops(e, e);
+    const char *ratio = getenv("SEC_SYN_RATIO");
+    const double lim = ratio && *ratio ? atof(ratio) : 0.75;
+    return syn < lim * vperm_ops(e, k) ? sh : -1;
 }
 
 // Work for one chunk.  `valid` = positions where every block is fully readable and
@@ -480,7 +526,7 @@ std::vector<std::pair<int64_t, int64_t>> slabs_of(const std::vector<uint64_t> &i
 // ---- host pipeline slots ----------------------------------------------------
 struct Slot {
     PinBuf in, out;
-    DevBuf din, dout;
+    DevBuf din, dout, dsyn;
     hipStream_t s = nullptr;
     hipEvent_t done = nullptr;
     bool busy = false;
@@ -505,11 +551,13 @@ struct sec_ctx {
     Plan enc_plan, dec_plan, sha_plan, bn_plan;
     DevBuf bn_scratch;  // host-mode staging of sec_bn_modexp / mulmod operands
     DevBuf bn_part;     // partial residues of segmented reductions (one region per slot)
+    DevBuf syn;         // syndrome rows of device-mode syndrome decodes
     size_t bn_part_stride = 0;
     Slot slots[kSlots];
     std::unique_ptr<sec::CopyPool> pool;
     // SEC_F_HOST encode / decode calls by path (sec_ctx_host_paths)
     int64_t zero_copy_calls = 0, registered_calls = 0, staged_calls = 0;
+    int64_t syn_chunks = 0, direct_chunks = 0;  // decodes by method (sec_ctx_decode_paths)
 
     hipStream_t stream() const { return ext ? ext : own; }
     hipEvent_t ev()
@@ -912,6 +960,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
     TableCache &tc = ctx->dec_tabs;
     std::vector<PendingExpand> pending;
     std::vector<uint32_t> tab_of((size_t)nchunks, 0), e_of((size_t)nchunks, 0);
+    std::vector<int> syn_of((size_t)nchunks, -1);  // syndrome-decode shape, or -1 (syn_choice)
     for (int attempt = 0;; ++attempt) {
         pending.clear();
         size_t need = 0;
@@ -927,7 +976,14 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             e_of[i] = (uint32_t)miss.size();
             if (miss.empty())
                 continue;
-            std::string key = std::to_string(k) + "/" + std::to_string(c.m) + ":";
+            // the syndrome kernel reads every slot but data block k-1 whole (that one may be short:
+            // zfec's padded block read in place)
+            bool whole = true;
+            for (int s = 0; s < k && whole && !host; ++s)
+                whole = idx[s] == k - 1 || slot_avail(c, block_avail, L.perm[L.first[i] + s]) >= c.B;
+            const int sh = syn_of[i] = whole ? syn_choice(c, idx, (int)miss.size()) : -1;
+            // the syndrome path's table is A^-1 (e x e), the direct path's the decode matrix rows
+            std::string key = (sh >= 0 ? "S" : "") + std::to_string(k) + "/" + std::to_string(c.m) + ":";
             for (int s = 0; s < k; ++s)
                 key += std::to_string(idx[s]) + ",";
             auto it = tc.index.find(key);
@@ -935,15 +991,37 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 tab_of[i] = it->second;
                 continue;
             }
-            std::vector<int> iv(idx, idx + k);
-            std::vector<uint8_t> minv;
-            if (!sec::decode_matrix(k, c.m, iv, minv))
-                return SEC_ESINGULAR;
             const int e = (int)miss.size();
-            std::vector<uint8_t> coef((size_t)k * e);
-            for (int s = 0; s < k; ++s)
-                for (int r = 0; r < e; ++r)
-                    coef[(size_t)s * e + r] = minv[(size_t)miss[r] * k + s];
+            std::vector<uint8_t> coef;
+            if (sh >= 0) {
+                // syndrome q belongs to the q-th present parity row (ascending); lost primary r
+                // = A^-1 s with A[q][r] = enc[k + that row][miss[r]]
+                std::vector<int> prow;
+                for (int s = 0; s < k; ++s)
+                    if (idx[s] >= k)
+                        prow.push_back(idx[s]);
+                std::sort(prow.begin(), prow.end());
+                const std::vector<uint8_t> enc = sec::encode_matrix(k, c.m);
+                std::vector<uint8_t> a((size_t)e * e);
+                for (int q = 0; q < e; ++q)
+                    for (int r = 0; r < e; ++r)
+                        a[(size_t)q * e + r] = enc[(size_t)prow[q] * k + miss[r]];
+                if (!sec::gf_invert(a, e))
+                    return SEC_ESINGULAR;
+                coef.resize((size_t)e * e);
+                for (int q = 0; q < e; ++q)  // layout [slot q][missing r]
+                    for (int r = 0; r < e; ++r)
+                        coef[(size_t)q * e + r] = a[(size_t)r * e + q];
+            } else {
+                std::vector<int> iv(idx, idx + k);
+                std::vector<uint8_t> minv;
+                if (!sec::decode_matrix(k, c.m, iv, minv))
+                    return SEC_ESINGULAR;
+                coef.resize((size_t)k * e);
+                for (int s = 0; s < k; ++s)
+                    for (int r = 0; r < e; ++r)
+                        coef[(size_t)s * e + r] = minv[(size_t)miss[r] * k + s];
+            }
             need += coef.size() * sec::kTabDwords;
             uint32_t off = 0;
             if (table_ensure(tc, key, std::move(coef), pending, &off)) {
@@ -959,6 +1037,10 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         RC(table_reset(ctx, tc, need * 2 + ((size_t)1 << 18)));
     }
 
+    plan.nsyn = plan.ndirect = 0;
+    for (int64_t i = 0; i < nchunks; ++i)
+        if (e_of[i])
+            ++(syn_of[i] >= 0 ? plan.nsyn : plan.ndirect);
     std::vector<std::pair<int64_t, int64_t>> ranges;
     if (host) {
         std::vector<uint64_t> ib((size_t)nchunks);
@@ -979,6 +1061,16 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         std::vector<uint32_t> srow, mrow, savail;
         Bins bins;
         std::vector<sec::TailItem> tail;
+        // syndrome decodes: phase-1 descriptors, slots and tiles (per shape); phase-2
+        // descriptors (appended to descs), tiles and tail items
+        std::vector<sec::SynDesc> sdescs;
+        std::vector<uint64_t> ssoff;
+        std::vector<uint32_t> ssavail;
+        std::map<int, std::vector<sec::Tile>> stiles;
+        std::vector<sec::DecDesc> descs2;
+        Bins bins2;
+        std::vector<sec::TailItem> tail2;
+        const int syn_lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
         for (int64_t i = c0; i < c1; ++i) {
             const sec_dec_chunk &c = chunks[i];
             const uint64_t base = L.first[i];
@@ -1015,12 +1107,73 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)c.B));
             sp.in_bytes += (uint64_t)c.k * c.B;
             sp.out_bytes += nout;
-            if (nout > 0 && !(nocopy && e_of[i] == 0))
+            const int sh = syn_of[i];
+            if (sh >= 0 && nout > 0) {
+                // phase 1: every present block in place, syndromes to the scratch
+                const int k = c.k, p = c.m - c.k, e = (int)e_of[i], NR = sec_bs_rows(sh);
+                const bool copies = !recover && !nocopy;
+                sec::SynDesc sd{};
+                sd.out_off = d.out_off;
+                sd.syn_off = sp.syn_bytes;
+                sd.B = (uint32_t)c.B;
+                sd.last = copies ? (uint32_t)(nout - (uint64_t)(k - 1) * c.B) : 0;
+                sd.slot0 = (uint32_t)ssoff.size();
+                ssoff.resize(ssoff.size() + (size_t)(k + p), 0);
+                ssavail.resize(ssavail.size() + (size_t)(k + p), 0);
+                for (int s = 0; s < k; ++s) {
+                    const size_t j = sd.slot0 + (idx[s] < k ? (size_t)s : (size_t)idx[s]);
+                    (idx[s] < k ? sd.dmask : sd.pmask) |= 1ull << (idx[s] < k ? s : idx[s] - k);
+                    ssoff[j] = soff[slot0 + s];
+                    ssavail[j] = savail[slot0 + s];
+                }
+                sp.syn_bytes += (uint64_t)e * c.B;
+                std::vector<int> gs;  // touched row groups, ascending
+                for (int g = 0; g * NR < p; ++g)
+                    if ((sd.pmask >> (g * NR)) & ((NR >= 64 ? ~0ull : (1ull << NR) - 1)))
+                        gs.push_back(g);
+                const uint32_t si = (uint32_t)sdescs.size();
+                sdescs.push_back(sd);
+                const uint64_t step = (uint64_t)sec_bs_span() * (syn_lanes / 64);
+                auto &st = stiles[sh];
+                for (uint64_t t0 = 0; t0 < c.B; t0 += 8 * step)  // runs of 8 positions per group: one XCD
+                    for (int g : gs)
+                        for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
+                            st.push_back(sec::Tile{si, (uint32_t)t, (uint32_t)(g * NR), copies && g == gs[0] ? 1u : 0u});
+                // phase 2: the e syndrome rows are the slots of a plain decode whose matrix is A^-1
+                sec::DecDesc d2 = d;
+                d2.k = (uint32_t)e;
+                d2.slot0 = (uint32_t)soff.size();
+                const int64_t valid2 = recover ? (int64_t)c.B : (int64_t)nout - (int64_t)(k - 1) * (int64_t)c.B;
+                d2.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid2, (int64_t)c.B));
+                for (int q = 0; q < e; ++q) {
+                    soff.push_back(sd.syn_off + (uint64_t)q * c.B);
+                    srow.push_back(0xFFFFFFFFu);
+                    savail.push_back((uint32_t)c.B);
+                    mrow.push_back(mr[q]);
+                }
+                const uint32_t di = (uint32_t)((c1 - c0) + descs2.size());
+                descs2.push_back(d2);
+                add_work(bins2, tail2, di, c.B, valid2, e, e, true, 0, false, dec_small_kb(e));
+            } else if (nout > 0 && !(nocopy && e_of[i] == 0)) {
                 add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true, 0, false,
                          recover || nocopy ? dec_small_kb(c.k) : dec_copy_kb(c.k));
+            }
         }
-        std::vector<sec::Tile> tiles;
+        descs.insert(descs.end(), descs2.begin(), descs2.end());
+        std::vector<sec::Tile> tiles, tiles2, stl;
         flatten(bins, sp.groups, tiles, true);
+        flatten(bins2, sp.groups2, tiles2, true);
+        for (auto &kv : stiles) {
+            sp.syn1.push_back({kv.first, {(uint32_t)stl.size(), (uint32_t)kv.second.size()}});
+            stl.insert(stl.end(), kv.second.begin(), kv.second.end());
+        }
+        sp.ntail2 = (uint32_t)tail2.size();
+        sp.off_sdesc = img.put(sdescs.data(), sdescs.size() * sizeof(sec::SynDesc));
+        sp.off_stiles = img.put(stl.data(), stl.size() * sizeof(sec::Tile));
+        sp.off_ssoff = img.put(ssoff.data(), ssoff.size() * 8);
+        sp.off_ssavail = img.put(ssavail.data(), ssavail.size() * 4);
+        sp.off_tiles2 = img.put(tiles2.data(), tiles2.size() * sizeof(sec::Tile));
+        sp.off_tail2 = img.put(tail2.data(), tail2.size() * sizeof(sec::TailItem));
         sp.ntail = (uint32_t)tail.size();
         sp.off_desc = img.put(descs.data(), descs.size() * sizeof(sec::DecDesc));
         sp.off_tiles = img.put(tiles.data(), tiles.size() * sizeof(sec::Tile));
@@ -1038,7 +1191,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
 }
 
 int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const uint8_t *blocks, uint8_t *out,
-                      hipStream_t s)
+                      hipStream_t s, uint8_t *syn = nullptr)
 {
     const sec::DecDesc *dd = plan.meta.as<sec::DecDesc>(sp.off_desc);
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
@@ -1054,6 +1207,35 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     if (sp.ntail) {
         int e = sec_launch_decode_tail(blocks, out, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs,
                                        sl, s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_decode_tail");
+    }
+    if (sp.syn1.empty())
+        return SEC_OK;
+    if (!syn)
+        return SEC_EINVAL;
+    // syndrome decodes: phase 1 (syndromes + present primaries' copies), then phase 2 on the
+    // syndrome rows (blocks = the scratch), in stream order
+    const sec::SynDesc *sd = plan.meta.as<sec::SynDesc>(sp.off_sdesc);
+    const sec::Tile *st = plan.meta.as<sec::Tile>(sp.off_stiles);
+    const sec::SynSlots ss{plan.meta.as<uint64_t>(sp.off_ssoff), plan.meta.as<uint32_t>(sp.off_ssavail)};
+    const int lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
+    for (auto &g : sp.syn1) {
+        int e = sec_launch_syndrome_bs(g.first, lanes, blocks, out, syn, sd, st + g.second.first, g.second.second, ss,
+                                       s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_syndrome_bs_kernel");
+    }
+    const sec::Tile *dt2 = plan.meta.as<sec::Tile>(sp.off_tiles2);
+    for (const Group &g : sp.groups2) {
+        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, syn, out, dd, dt2 + g.first, g.count, tabs, sl, s,
+                                  g.mfma);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_decode_kernel");
+    }
+    if (sp.ntail2) {
+        int e = sec_launch_decode_tail(syn, out, dd, plan.meta.as<sec::TailItem>(sp.off_tail2), sp.ntail2, tabs, sl,
+                                       s);
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_tail");
     }
@@ -1422,6 +1604,7 @@ void sec_ctx_destroy(sec_ctx *ctx)
         s.out.release();
         s.din.release();
         s.dout.release();
+        s.dsyn.release();
         if (s.done)
             (void)hipEventDestroy(s.done);
         if (s.s)
@@ -1437,6 +1620,7 @@ void sec_ctx_destroy(sec_ctx *ctx)
     ctx->bn_plan.meta.release();
     ctx->bn_scratch.release();
     ctx->bn_part.release();
+    ctx->syn.release();
     if (ctx->own)
         (void)hipStreamDestroy(ctx->own);
     delete ctx;
@@ -2252,11 +2436,14 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
         plan.key.swap(key);
         plan.valid = true;
     }
+    ctx->syn_chunks += plan.nsyn;
+    ctx->direct_chunks += plan.ndirect;
 
     if (!host) {
         hipEvent_t t0 = nullptr;
+        RC(ctx->syn.ensure(plan.subs[0].syn_bytes));
         RC(timing_begin(ctx, &t0, ctx->stream()));
-        RC(launch_decode_sub(ctx, plan, plan.subs[0], blocks, out, ctx->stream()));
+        RC(launch_decode_sub(ctx, plan, plan.subs[0], blocks, out, ctx->stream(), ctx->syn.as<uint8_t>()));
         RC(timing_end(ctx, t0, 1, ctx->stream()));
         if (nocopy)  // the present primaries, host to host, while the kernels run
             pool(ctx).run(joins);
@@ -2301,7 +2488,14 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
         }
     };
     auto launch = [&](const SubPlan &sp, uint8_t *din, uint8_t *dout, hipStream_t s) {
-        return launch_decode_sub(ctx, plan, sp, din, dout, s);
+        uint8_t *syn = nullptr;
+        if (sp.syn_bytes)
+            for (Slot &slot : ctx->slots)  // the unit's slot: its own syndrome scratch
+                if (slot.s == s) {
+                    RC(slot.dsyn.ensure(sp.syn_bytes));
+                    syn = slot.dsyn.as<uint8_t>();
+                }
+        return launch_decode_sub(ctx, plan, sp, din, dout, s, syn);
     };
     RC(run_pipeline(ctx, plan, gather, scatter, launch, true));
     if (join)  // the present primaries, host to host
@@ -2361,6 +2555,17 @@ int sec_host_unregister(sec_ctx *ctx, void *hptr)  // ctx unused: may be NULL
     if (!hptr)
         return SEC_EINVAL;
     CK(hipHostUnregister(hptr));
+    return SEC_OK;
+}
+
+int sec_ctx_decode_paths(sec_ctx *ctx, int64_t *syndrome, int64_t *direct)
+{
+    if (!ctx)
+        return SEC_EINVAL;
+    if (syndrome)
+        *syndrome = ctx->syn_chunks;
+    if (direct)
+        *direct = ctx->direct_chunks;
     return SEC_OK;
 }
 

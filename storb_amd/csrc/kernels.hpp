@@ -66,6 +66,25 @@ struct DecSlots {
     const uint32_t *avail;  // bytes of the block that exist in memory; the rest read as zero
 };
 
+// One chunk of a syndrome decode, phase 1 (kernels_bs.hip sec_syndrome_bs_kernel; 48 B).
+// Block j of the chunk (data j < k, parity row r at j = k + r) is at blocks + off[slot0 + j]
+// with avail[slot0 + j] readable bytes, when its bit in dmask / pmask is set.
+struct SynDesc {
+    uint64_t out_off;  // reassembled chunk in `out`: present primaries are copied there (tile flag)
+    uint64_t syn_off;  // syndrome q (the q-th present parity row) at syn + syn_off + q * B
+    uint64_t dmask;    // bit j: data block j present (k <= 64)
+    uint64_t pmask;    // bit r: parity row r present (m - k <= 64)
+    uint32_t B;
+    uint32_t last;     // bytes of output row k-1 (n - (k-1)*B): its copy stops there
+    uint32_t slot0;
+    uint32_t pad;
+};
+
+struct SynSlots {
+    const uint64_t *off;
+    const uint32_t *avail;
+};
+
 struct Tile {
     uint32_t chunk;  // descriptor index
     uint32_t t0;     // first byte position within the block
@@ -117,6 +136,13 @@ int sec_bs_rows(int shape);
 uint32_t sec_bs_span();
 int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
                          const sec::Tile *t, uint32_t ntiles, void *stream);
+// Syndrome decode, phase 1, for the shapes sec_syn_shape knows (else -1): tiles as the bit-sliced
+// encode's (r0 = the row group's first parity row; ntail bit 0 = this tile also copies the
+// present primaries to `out`)
+int sec_syn_shape(int k, int m);
+int sec_launch_syndrome_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, uint8_t *syn,
+                           const sec::SynDesc *descs, const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl,
+                           void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
                            uint32_t nitems, const uint32_t *tabs, void *stream);
 // kb (4 or 8): the kernel variant whose load batch is kb slots (every chunk of the group has

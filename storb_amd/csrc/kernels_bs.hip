@@ -308,6 +308,183 @@ __global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs2_kernel(c
         bs_span<K, M, NR, NR, D, false>(in, par, d, s);
 }
 
+// ---- decode, phase 1: syndromes of the present parity rows (wide decodes) -------------------
+// A decode that lost e data blocks and holds e parity rows S instead: for a parity row r in S,
+//     s_r = p_r ^ XOR_{present j} c[r][j] * d_j  =  XOR_{lost j} c[r][j] * d_j,
+// so the lost blocks are A^-1 s with A = c[S][lost] (e x e).  Phase 1 is this kernel: the
+// bit-sliced encode of the PRESENT data blocks (the matrix c at compile time, a block the chunk
+// lacks skipped by a wave-uniform branch), XORed with the present parity rows and stored as e
+// syndrome rows.  While it has each present data block in registers it also stores it to its
+// output row (the copy half of a reassembly).  Phase 2 applies the run-time e x e inverse with
+// sec_decode_kernel (api.cpp).  Per input dword this costs the bit-sliced rows (6 + 2.75 + NR +
+// 6 NR / 64 VALU) instead of ceil(e / 8) v_perm row groups over all k blocks (5 + 36 VALU each),
+// and reads the k blocks once instead of once per 8-row group.
+//
+// Items 0..K-1 of a chunk are its data blocks, K..K+NR-1 the parity rows R0.. of this tile's
+// group; one ring of D items in flight serves both.  Results are zfec's fec_decode (restated in
+// oracle/fec_oracle.c; /root/reference/storb/util/piece.py:196-197).
+
+// The lane's two 16-byte pieces of an item.  Only data block K-1 may be short (avail < B: zfec's
+// padded last block read in place; the plan sends chunks whose other slots are shorter to the
+// direct decode), so only that item carries the byte path.
+template <bool SHORT>
+__device__ __forceinline__ void load_item(u32 (&x)[8], const u8 *blk, u32 pa, u32 pb, u32 avail)
+{
+    u32x4 a, b;
+    if (!SHORT || pb + 16 <= avail) {  // pb >= pa: the whole lane is inside
+        a = ld16<true>(blk + pa);
+        b = ld16<true>(blk + pb);
+    } else {
+        a = ld16_avail<true>(blk, pa, avail);
+        b = ld16_avail<true>(blk, pb, avail);
+    }
+    x[0] = a.x;
+    x[1] = a.y;
+    x[2] = a.z;
+    x[3] = a.w;
+    x[4] = b.x;
+    x[5] = b.y;
+    x[6] = b.z;
+    x[7] = b.w;
+}
+
+// 16 bytes to o + off, only those below `lim`
+__device__ __forceinline__ void st16_clamped(u8 *o, u32 off, u32 lim, u32 a, u32 b, u32 c, u32 d)
+{
+    if (off + 16 <= lim) {
+        st16(o + off, a, b, c, d);
+        return;
+    }
+    const u32 w[4] = {a, b, c, d};
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (off + i < lim)
+            o[off + i] = (u8)(w[i >> 2] >> (8 * (i & 3)));
+}
+
+struct SynCtx {
+    const u8 *blocks;
+    const uint64_t *off;
+    const uint32_t *avail;
+    u32 slot0, pa, pb;
+    uint64_t dmask, pmask;
+};
+
+template <int K, int NR, int R0>
+__device__ __forceinline__ bool item_present(const SynCtx &c, int J)
+{
+    return J < K ? ((c.dmask >> J) & 1) : ((c.pmask >> (R0 + J - K)) & 1);
+}
+
+template <int K, int NR, int R0, int J>
+__device__ __forceinline__ void load_syn_item(u32 (&x)[8], const SynCtx &c)
+{
+    constexpr u32 slot = J < K ? (u32)J : (u32)(K + R0 + J - K);
+    load_item<J == K - 1>(x, c.blocks + c.off[c.slot0 + slot], c.pa, c.pb, J == K - 1 ? c.avail[c.slot0 + slot] : 0u);
+}
+
+template <int K, int NR, int R0, int... Js>
+__device__ __forceinline__ void load_syn_first(std::integer_sequence<int, Js...>, u32 (&ring)[sizeof...(Js)][8],
+                                               const SynCtx &c)
+{
+    ((item_present<K, NR, R0>(c, Js) ? load_syn_item<K, NR, R0, Js>(ring[Js], c) : void()), ...);
+}
+
+template <int K, int M, int R0, int NR, int D, int J>
+__device__ __forceinline__ void syn_item(u32 (&acc)[NR * 8], u32 (&ring)[D][8], const SynCtx &c, u8 *orow0, u32 B,
+                                         u32 last, bool copies, u8 *syn, u32 &q)
+{
+    constexpr int NI = K + NR;
+    const bool here = item_present<K, NR, R0>(c, J);
+    u32 x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        x[i] = ring[J % D][i];
+    if constexpr (J + D < NI)
+        if (item_present<K, NR, R0>(c, J + D))
+            load_syn_item<K, NR, R0, J + D>(ring[J % D], c);
+    if (!here)
+        return;
+    if constexpr (J < K) {
+        if (copies) {  // the present primary's bytes to its output row (row K-1 clamps to `last`)
+            u8 *o = orow0 + (u64)J * B;
+            if constexpr (J == K - 1) {
+                st16_clamped(o, c.pa, last, x[0], x[1], x[2], x[3]);
+                st16_clamped(o, c.pb, last, x[4], x[5], x[6], x[7]);
+            } else {
+                st16(o + c.pa, x[0], x[1], x[2], x[3]);
+                st16(o + c.pb, x[4], x[5], x[6], x[7]);
+            }
+        }
+        transpose8(x);
+        u32 lo[16], hi[16];
+        subsets(x[0], x[1], x[2], x[3], lo);
+        subsets(x[4], x[5], x[6], x[7], hi);
+        block_rows<K, M, R0, J, false>(std::make_integer_sequence<int, NR * 8>{}, acc, lo, hi);
+    } else {  // parity row R0 + r: syndrome = its bytes ^ the present blocks' contribution
+        constexpr int r = J - K;
+        u32 y[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            y[i] = acc[r * 8 + i];
+        transpose8(y);
+        u8 *o = syn + (u64)q * B;
+        st16(o + c.pa, y[0] ^ x[0], y[1] ^ x[1], y[2] ^ x[2], y[3] ^ x[3]);
+        st16(o + c.pb, y[4] ^ x[4], y[5] ^ x[5], y[6] ^ x[6], y[7] ^ x[7]);
+        ++q;
+    }
+}
+
+template <int K, int M, int R0, int NR, int D, int... Js>
+__device__ __forceinline__ void syn_items(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], u32 (&ring)[D][8],
+                                          const SynCtx &c, u8 *orow0, u32 B, u32 last, bool copies, u8 *syn, u32 &q)
+{
+    (syn_item<K, M, R0, NR, D, Js>(acc, ring, c, orow0, B, last, copies, syn, q), ...);
+}
+
+template <int K, int M, int R0, int NR, int D>
+__device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__restrict__ out, u8 *__restrict__ syn,
+                                         const sec::SynDesc &d, const sec::SynSlots &sl, u32 s, bool copies)
+{
+    const u32 B = d.B;
+    const u32 lane = (threadIdx.x & 63) * 16;
+    SynCtx c{blocks, sl.off, sl.avail, d.slot0, min(s + lane, B - 16), min(s + 1024 + lane, B - 16), d.dmask, d.pmask};
+    u32 ring[D][8];
+    load_syn_first<K, NR, R0>(std::make_integer_sequence<int, D>{}, ring, c);
+    u32 acc[NR * 8];
+#pragma unroll
+    for (int i = 0; i < NR * 8; ++i)
+        acc[i] = 0;
+    // syndrome row of this group's first present parity row: the present rows below R0
+    u32 q = (u32)__builtin_popcountll(d.pmask & ((1ull << R0) - 1ull));
+    syn_items<K, M, R0, NR, D>(std::make_integer_sequence<int, K + NR>{}, acc, ring, c, out + d.out_off, B, d.last,
+                               copies, syn + d.syn_off, q);
+}
+
+template <int K, int M, int NR, int D>
+__global__ __launch_bounds__(256) void sec_syndrome_bs_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+                                                              u8 *__restrict__ syn,
+                                                              const sec::SynDesc *__restrict__ descs,
+                                                              const sec::Tile *__restrict__ tiles,
+                                                              const sec::SynSlots sl)
+{
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::SynDesc d = descs[tl.chunk];
+    const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
+    if (s >= d.B)
+        return;
+    const bool copies = tl.ntail & 1;  // the chunk's first touched row group copies the primaries
+    if constexpr (M - K <= NR) {
+        syn_span<K, M, 0, NR, D>(blocks, out, syn, d, sl, s, copies);
+    } else {
+        static_assert(M - K == 2 * NR, "two row groups");
+        if (tl.r0 == 0)
+            syn_span<K, M, 0, NR, D>(blocks, out, syn, d, sl, s, copies);
+        else
+            syn_span<K, M, NR, NR, D>(blocks, out, syn, d, sl, s, copies);
+    }
+}
+
 template <int K, int M, int R0, int NR, int D>
 hipError_t launch_bs(int lanes, const u8 *in, u8 *par, const sec::EncDesc *d, const sec::Tile *t, u32 nt,
                      hipStream_t s)
@@ -376,6 +553,45 @@ int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uin
     case 24: return launch_bs<32, 48, -1, 8, RING_K(32, 4)>(lanes, in, par, descs, t, ntiles, s);
     case 25: return launch_bs<32, 48, 0, 8, RING_K(32, 4)>(lanes, in, par, descs, t, ntiles, s);
     case 26: return launch_bs<32, 48, 8, 8, RING_K(32, 4)>(lanes, in, par, descs, t, ntiles, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+namespace {
+template <int K, int M, int NR, int D>
+hipError_t launch_syn(int lanes, const u8 *blocks, u8 *out, u8 *syn, const sec::SynDesc *d, const sec::Tile *t,
+                      u32 nt, sec::SynSlots sl, hipStream_t s)
+{
+    void *a = nullptr, *b = nullptr;
+    sec_next_launch_events(&a, &b);
+    hipExtLaunchKernelGGL((sec_syndrome_bs_kernel<K, M, NR, D>), dim3(nt), dim3(lanes), 0, s, (hipEvent_t)a,
+                          (hipEvent_t)b, 0, blocks, out, syn, d, t, sl);
+    return hipGetLastError();
+}
+}  // namespace
+
+int sec_syn_shape(int k, int m)
+{
+    const int sh = sec_bs_shape(k, m);
+    return sh == 6 ? -1 : sh;  // (32,48) in 8-row groups is an encode A/B only
+}
+
+int sec_launch_syndrome_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, uint8_t *syn,
+                           const sec::SynDesc *descs, const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl,
+                           void *stream)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    if (lanes < 64 || lanes > 256 || lanes % 64)
+        return hipErrorInvalidValue;
+    hipStream_t s = (hipStream_t)stream;
+    switch (shape) {  // ring depths as the encode's (kernels' register budgets are alike)
+    case 0: return launch_syn<10, 14, 4, RING_K(10, 5)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 1: return launch_syn<8, 12, 4, RING_K(8, 4)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 2: return launch_syn<16, 24, 8, RING_K(16, 10)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 3: return launch_syn<32, 48, 16, RING_K(32, 2)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 4: return launch_syn<64, 96, 16, RING_K(64, 2)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 5: return launch_syn<8, 11, 3, RING_K(8, 4)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -199,6 +199,12 @@ class Engine:
         self._check(self.lib.sec_ctx_host_paths(self._ctx, ctypes.byref(z), ctypes.byref(r), ctypes.byref(st)))
         return z.value, r.value, st.value
 
+    def decode_paths(self) -> tuple[int, int]:
+        """(syndrome, direct): chunks with a lost data block decoded so far, by method."""
+        syn, direct = ctypes.c_int64(0), ctypes.c_int64(0)
+        self._check(self.lib.sec_ctx_decode_paths(self._ctx, ctypes.byref(syn), ctypes.byref(direct)))
+        return syn.value, direct.value
+
     _SCRATCH_CAP = 256 << 20  # largest result staged in the reusable pinned scratch
 
     def _out_buffer(self, nbytes: int) -> np.ndarray:

@@ -1,0 +1,234 @@
+"""GPU parity of the syndrome decode (wide decodes with many lost data blocks).
+
+A chunk that lost e data blocks and holds e parity rows instead is decoded in two phases
+(kernels_bs.hip sec_syndrome_bs_kernel: bit-sliced syndromes of the present parity rows and the
+copies of the present primaries; then sec_decode_kernel applies the e x e inverse).  The result
+must be zfec's fec_decode bytes (/root/reference/storb/util/piece.py:196-197 via easyfec),
+checked here against the source chunk (every chunk) and the oracle's padded blocks
+(oracle/fec_oracle.c) for:
+
+* the policy's wide shapes zfec(16,24), (32,48), (64,96) and the kernel's other shapes (C4's
+  (10,14), (8,12), C5's (8,11)), e = 1 .. p lost, parity rows from one or both row groups;
+* B from 16 bytes (one partial wave) to several tiles, unaligned B, padded chunks with block
+  k-1 present and read in place (avail = B - padlen) or lost;
+* reassemble and recover-only; device buffers, staged host buffers and pinned host buffers;
+* syndrome chunks mixed with direct-path chunks and other shapes in one call;
+* the path actually taken (sec_ctx_decode_paths) under SEC_SYN=1 (forced) and the default
+  cost rule, with SEC_SYN=0 (the direct decode) giving the same bytes.
+"""
+
+import random
+
+import numpy as np
+import pytest
+
+from oracle import cfec
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from storb_amd._lib import DEC_DTYPE, ENC_DTYPE  # noqa: E402
+
+SHAPES = [(16, 24), (32, 48), (64, 96), (10, 14), (8, 12), (8, 11)]
+
+
+def _engine(monkeypatch, syn):
+    from storb_amd.engine import Engine
+
+    if syn is None:
+        monkeypatch.delenv("SEC_SYN", raising=False)
+    else:
+        monkeypatch.setenv("SEC_SYN", syn)
+    return Engine(0)  # a fresh context: the knob is read when a plan is built
+
+
+def _cases(rng, k, m, sizes):
+    """(size, keep) pairs: for each size several erasure patterns; keep = the k block numbers
+    the decoder gets (lost data blocks replaced by parity rows)."""
+    p = m - k
+    out = []
+    for n in sizes:
+        for e in sorted({1, min(2, p), p // 2 or 1, p, rng.randint(1, p)}):
+            lost = sorted(rng.sample(range(k), e))
+            par = sorted(rng.sample(range(k, m), e))
+            keep = [j for j in range(k) if j not in lost] + par
+            rng.shuffle(keep)
+            out.append((n, keep))
+    return out
+
+
+def _run(eng, k, m, cases, recover=False, host=None, check_oracle=3):
+    """Encode the chunks on the device, decode them from the kept blocks read in place (or from
+    host copies), compare with the sources (and the oracle for a few)."""
+    sizes = np.array([n for n, _ in cases], dtype=np.uint64)
+    B = (sizes + k - 1) // k
+    in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    par_off = np.concatenate([[0], np.cumsum(B * (m - k))[:-1]]).astype(np.uint64)
+    total = int(sizes.sum())
+    g = torch.Generator(device="cuda")
+    g.manual_seed(int(total) % 100003 + k)
+    src = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda", generator=g)
+    par = torch.empty(max(int((B * (m - k)).sum()), 1), dtype=torch.uint8, device="cuda")
+    ed = np.zeros(len(cases), dtype=ENC_DTYPE)
+    ed["in_off"], ed["n"], ed["parity_off"], ed["parity_stride"], ed["k"], ed["m"] = in_off, sizes, par_off, B, k, m
+    eng.encode_batch(ed, src, par)
+    src_h, par_h = src.cpu().numpy(), par.cpu().numpy()
+    n_ch = len(cases)
+    d = np.zeros(n_ch, dtype=DEC_DTYPE)
+    d["B"], d["padlen"], d["k"], d["m"] = B, B * k - sizes, k, m
+    d["slot0"] = np.arange(n_ch, dtype=np.uint64) * k
+    sn = np.zeros(n_ch * k, np.int32)
+    offs = np.zeros(n_ch * k, np.uint64)
+    avail = np.zeros(n_ch * k, np.uint64)
+    out_off, o, want = np.zeros(n_ch, np.uint64), 0, []
+    hostbuf = bytearray()
+    for i, (n, keep) in enumerate(cases):
+        b = int(B[i])
+        out_off[i] = o
+        chunk = src_h[int(in_off[i]):int(in_off[i]) + n].tobytes()
+        lost = [j for j in range(k) if j not in keep]
+        if recover:
+            padded = chunk + bytes(k * b - n)
+            want.append(b"".join(padded[j * b:(j + 1) * b] for j in lost))
+        else:
+            want.append(chunk)
+        o += len(want[-1])
+        for q, s in enumerate(keep):
+            sn[i * k + q] = s
+            if s < k:
+                a, av = int(in_off[i]) + s * b, min(b, n - s * b)
+                blk = src_h[a:a + av].tobytes() + bytes(b - av)
+                base, dev_av = src.data_ptr(), av
+            else:
+                a = int(par_off[i]) + (s - k) * b
+                blk = par_h[a:a + b].tobytes()
+                base, dev_av = par.data_ptr(), b
+            if host is None:
+                offs[i * k + q], avail[i * k + q] = base + a, dev_av
+            else:
+                offs[i * k + q], avail[i * k + q] = len(hostbuf), b
+                hostbuf += blk
+    d["out_off"] = out_off
+    if host is None:
+        out = torch.zeros(max(o, 1), dtype=torch.uint8, device="cuda")
+        eng.decode_batch(d, sn, offs, 0, out, block_avail=avail, recover_only=recover)
+        got = out.cpu().numpy()
+    else:
+        if host == "pinned":
+            hb = eng.host_empty(len(hostbuf))
+            hb[:] = np.frombuffer(hostbuf, np.uint8)
+            got = eng.host_empty(max(o, 1))
+        else:
+            hb = np.frombuffer(hostbuf, np.uint8).copy()
+            got = np.zeros(max(o, 1), np.uint8)
+        eng.decode_batch(d, sn, offs, hb, got, recover_only=recover, host=True)
+    pos = 0
+    for i, w in enumerate(want):
+        assert got[pos:pos + len(w)].tobytes() == w, (k, m, cases[i][0], cases[i][1], recover, host)
+        pos += len(w)
+    for i in range(min(check_oracle, n_ch)):  # the oracle's decode of the same blocks
+        n, keep = cases[i]
+        b = int(B[i])
+        blocks = cfec.easy_encode(src_h[int(in_off[i]):int(in_off[i]) + n].tobytes(), k, m)
+        dec = cfec.easy_decode([blocks[s] for s in keep], keep, k * b - n, k, m)
+        assert dec == src_h[int(in_off[i]):int(in_off[i]) + n].tobytes()
+
+
+@pytest.mark.parametrize("k,m", SHAPES)
+@pytest.mark.parametrize("recover", [False, True])
+def test_syndrome_decode_forced_device(k, m, recover, monkeypatch):
+    rng = random.Random(k * 1000 + m + recover)
+    sizes = [16 * k, 17 * k - 3, 2048 * k + 5 * k, 6554 * k - 4 if k == 10 else 4099 * k - 1, 65536 * k,
+             rng.randrange(20000, 300000)]
+    sizes = [n for n in sizes if -(-n // k) * (k - 1) < n]  # easyfec: the last block not empty
+    eng = _engine(monkeypatch, "1")
+    try:
+        cases = _cases(rng, k, m, sizes)
+        _run(eng, k, m, cases, recover=recover)
+        syn, direct = eng.decode_paths()
+        assert syn == len(cases) and direct == 0, (syn, direct)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("k,m", [(32, 48), (64, 96), (16, 24)])
+@pytest.mark.parametrize("host", ["staged", "pinned"])
+def test_syndrome_decode_forced_host(k, m, host, monkeypatch):
+    rng = random.Random(7 * k + (host == "pinned"))
+    eng = _engine(monkeypatch, "1")
+    try:
+        cases = _cases(rng, k, m, [4096 * k + 17, 1 << 20, 3 * k * 1024 - 5])
+        _run(eng, k, m, cases, host=host)
+        _run(eng, k, m, cases, host=host, recover=True)
+        assert eng.decode_paths()[0] == 2 * len(cases)
+    finally:
+        eng.close()
+
+
+def test_syndrome_default_rule_and_off_give_same_bytes(monkeypatch):
+    """The default cost rule on the verdict's cases: zfec(64,96) with 16 and 32 data blocks lost,
+    zfec(32,48) with every parity row in use -> syndrome path; one lost block -> direct path.
+    SEC_SYN=0 decodes the same chunks directly, to the same bytes."""
+    cases64 = [(1 << 20, list(range(16, 64)) + list(range(64, 80))),  # 16 lost, parity group 0
+               (1 << 20, list(range(32, 64)) + list(range(64, 96))),  # 32 lost, every parity row
+               (1 << 20, list(range(1, 64)) + [95])]  # one lost
+    cases32 = [(1 << 20, list(range(16, 32)) + list(range(32, 48))), (1 << 20, list(range(1, 32)) + [40])]
+    for syn_env, want in ((None, (3, 2)), ("0", (0, 5))):
+        eng = _engine(monkeypatch, syn_env)
+        try:
+            _run(eng, 64, 96, cases64)
+            _run(eng, 32, 48, cases32)
+            assert eng.decode_paths() == want, (syn_env, eng.decode_paths())
+        finally:
+            eng.close()
+
+
+def test_syndrome_mixed_batch_with_direct_chunks(monkeypatch):
+    """One call: syndrome chunks of two shapes and direct chunks (RS(4,2), and a shape without a
+    bit-sliced kernel), device-resident, reassembled; every chunk against its source."""
+    from storb_amd.engine import Engine
+
+    monkeypatch.delenv("SEC_SYN", raising=False)
+    eng = Engine(0)
+    try:
+        rng = random.Random(5)
+        specs = []  # (k, m, n, keep)
+        for _ in range(6):
+            specs.append((64, 96, rng.randrange(70000, 400000), list(range(20, 64)) + list(range(70, 90))))
+            specs.append((32, 48, rng.randrange(70000, 400000), list(range(12, 32)) + list(range(36, 48))))
+            specs.append((4, 6, rng.randrange(4096, 100000), [0, 2, 4, 5]))
+            specs.append((5, 9, rng.randrange(4096, 100000), [1, 2, 5, 7, 8]))
+        sizes = np.array([n for _, _, n, _ in specs], np.uint64)
+        total = int(sizes.sum())
+        src = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda")
+        in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+        Bs = [-(-int(n) // k) for k, m, n, _ in specs]
+        par_sizes = [(m - k) * b for (k, m, _, _), b in zip(specs, Bs)]
+        par_off = np.concatenate([[0], np.cumsum(par_sizes)[:-1]]).astype(np.uint64)
+        par = torch.empty(int(sum(par_sizes)), dtype=torch.uint8, device="cuda")
+        ed = np.zeros(len(specs), dtype=ENC_DTYPE)
+        for i, ((k, m, n, _), b) in enumerate(zip(specs, Bs)):
+            ed[i] = (in_off[i], n, par_off[i], b, k, m)
+        eng.encode_batch(ed, src, par)
+        d = np.zeros(len(specs), dtype=DEC_DTYPE)
+        sn, offs, av, slot = [], [], [], 0
+        for i, ((k, m, n, keep), b) in enumerate(zip(specs, Bs)):
+            d[i] = (in_off[i], b, b * k - n, slot, k, m)
+            for s in keep:
+                sn.append(s)
+                if s < k:
+                    offs.append(src.data_ptr() + int(in_off[i]) + s * b)
+                    av.append(min(b, n - s * b))
+                else:
+                    offs.append(par.data_ptr() + int(par_off[i]) + (s - k) * b)
+                    av.append(b)
+            slot += k
+        out = torch.zeros_like(src)
+        eng.decode_batch(d, np.array(sn, np.int32), np.array(offs, np.uint64), 0, out,
+                         block_avail=np.array(av, np.uint64))
+        assert torch.equal(out, src)
+        syn, direct = eng.decode_paths()
+        assert syn == 12 and direct == 12, (syn, direct)
+    finally:
+        eng.close()

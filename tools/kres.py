@@ -34,11 +34,12 @@ def main():
     ap.add_argument("defs", nargs="*")
     ap.add_argument("--filter", default=r"encode_kernel|decode_kernel")
     ap.add_argument("--mix", action="store_true")
+    ap.add_argument("--src", default=SRC, help="kernel source (default storb_amd/csrc/kernels.hip)")
     a, extra = ap.parse_known_args()
     a.defs += extra
     with tempfile.TemporaryDirectory() as td:
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", f"-I{ROOT}/include",
-               "--save-temps", "-c", SRC, "-o", os.path.join(td, "k.o"),
+               "--save-temps", "-c", os.path.abspath(a.src), "-o", os.path.join(td, "k.o"),
                "-Rpass-analysis=kernel-resource-usage", *a.defs]
         p = subprocess.run(cmd, cwd=td, capture_output=True, text=True, check=True)
         rows, cur = [], None
@@ -53,7 +54,8 @@ def main():
             elif cur is not None and ":" in t:
                 k, v = t.split(":", 1)
                 cur[k.strip()] = v.strip()
-        asm = open(os.path.join(td, "kernels-hip-amdgcn-amd-amdhsa-gfx950.s")).read()
+        stem = os.path.splitext(os.path.basename(a.src))[0]
+        asm = open(os.path.join(td, f"{stem}-hip-amdgcn-amd-amdhsa-gfx950.s")).read()
     for r in rows:
         nm = demangle(r["name"])
         if not re.search(a.filter, nm):

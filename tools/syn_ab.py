@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""A/B of the syndrome decode against the direct decode on wide shapes (one process, fresh
+engine per variant, rounds interleaved), device-resident, reassemble and recover-only.
+
+    python tools/syn_ab.py [--rounds 3] [--reps 5] > gpurun_out/syn_ab.jsonl
+
+Rates are TB/s of algorithmic bytes: k*B read + n written (reassemble) or k*B + e*B
+(recover-only), per HIP-event kernel time of the whole decode call (both phases).  Every
+variant's output is checked against the source chunks.  Not product code.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# (name, k, m, chunk bytes, chunks, lost data blocks)
+CASES = [
+    ("zfec(64,96) 256MiB x4, 16 lost", 64, 96, 256 << 20, 4, 16),
+    ("zfec(64,96) 1MiB x1024, 16 lost", 64, 96, 1 << 20, 1024, 16),
+    ("zfec(64,96) 1MiB x1024, 32 lost (every parity row)", 64, 96, 1 << 20, 1024, 32),
+    ("zfec(32,48) 1MiB x1024, 16 lost (every parity row)", 32, 48, 1 << 20, 1024, 16),
+    ("zfec(32,48) 32MiB x32, 8 lost", 32, 48, 32 << 20, 32, 8),
+    ("zfec(16,24) 8MiB x128, 8 lost (every parity row)", 16, 24, 8 << 20, 128, 8),
+    ("zfec(16,24) 8MiB x128, 4 lost", 16, 24, 8 << 20, 128, 4),
+    ("C4 zfec(10,14) 64KiB x8192, 4 lost", 10, 14, 65536, 8192, 4),
+]
+
+
+def main():
+    import torch
+
+    import bench
+    from storb_amd.engine import Engine
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", default="direct@SEC_SYN=0,syn@SEC_SYN=1,auto")
+    ap.add_argument("--cases", default="")
+    a = ap.parse_args()
+    variants = []
+    for v in a.variants.split(","):
+        name, _, env = v.partition("@")
+        variants.append((name, dict(kv.split("=") for kv in env.split("+")) if env else {}))
+    sel = [c for c in CASES if not a.cases or any(t in c[0] for t in a.cases.split(","))]
+    for name, k, m, n, nch, e in sel:
+        src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
+        B = -(-n // k)
+        ed, _ = bench.enc_descs(nch, n, k, m)
+        par = torch.empty(nch * (m - k) * B, dtype=torch.uint8, device="cuda")
+        lost = tuple(range(0, 2 * e, 2)) if 2 * e <= k else tuple(range(e))
+        eng0 = Engine(0)
+        eng0.encode_batch(ed, src, par)
+        eng0.close()
+        dd, sn, offs, av = bench.dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), lost)
+        rd, rsn, roffs, rav = bench.dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), lost, recover=True)
+        out = torch.empty_like(src)
+        rec = torch.empty(nch * e * B, dtype=torch.uint8, device="cuda")
+        res = {v[0]: {"reassemble": [], "recover_only": []} for v in variants}
+        paths = {}
+        for _ in range(a.rounds):
+            for vname, env in variants:
+                old = {key: os.environ.get(key) for key in env}
+                os.environ.pop("SEC_SYN", None) if not env else None
+                os.environ.update(env)
+                try:
+                    eng = Engine(0)
+                    for mode, args in (("reassemble", (dd, sn, offs, av, out, False)),
+                                       ("recover_only", (rd, rsn, roffs, rav, rec, True))):
+                        d_, s_, o_, a_, dst, recov = args
+                        dst.zero_()
+                        eng.decode_batch(d_, s_, o_, 0, dst, block_avail=a_, recover_only=recov)
+                        if not recov:
+                            assert torch.equal(out, src), (name, vname)
+                        else:
+                            r3, s3 = rec.view(nch, e, B), src.view(nch, k, B)
+                            for j, blk in enumerate(lost):
+                                assert torch.equal(r3[:, j], s3[:, blk]), (name, vname, blk)
+                        eng.set_timing(True)
+                        for _ in range(a.reps):
+                            eng.decode_batch(d_, s_, o_, 0, dst, block_avail=a_, recover_only=recov, asynchronous=True)
+                        eng.sync()
+                        eng.set_timing(False)
+                        ms, nl = eng.collect_timing("decode")
+                        alg = nch * (k * B + (e * B if recov else n))
+                        res[vname][mode].append(alg / (ms / 1e3 / a.reps) / 1e12)
+                    paths[vname] = eng.decode_paths()
+                    eng.close()
+                finally:
+                    for key, val in old.items():
+                        if val is None:
+                            os.environ.pop(key, None)
+                        else:
+                            os.environ[key] = val
+        row = {"case": name, "k": k, "m": m, "chunk": n, "chunks": nch, "lost": list(lost)}
+        for vname, r in res.items():
+            row[vname] = {mode: round(float(np.median(v)), 3) for mode, v in r.items()}
+            row[vname]["paths(syn,direct)"] = paths.get(vname)
+        print(json.dumps(row), flush=True)
+        del src, par, out, rec
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
