@@ -80,8 +80,9 @@ def main():
                         eng.decode_batch(d_, s_, o_, 0, dst, block_avail=a_, recover_only=recov)
                         if not recov:
                             assert torch.equal(out, src), (name, vname)
-                        else:
-                            r3, s3 = rec.view(nch, e, B), src.view(nch, k, B)
+                        else:  # recovered rows against the (zero-padded) source blocks
+                            r3 = rec.view(nch, e, B)
+                            s3 = torch.nn.functional.pad(src.view(nch, n), (0, k * B - n)).view(nch, k, B)
                             for j, blk in enumerate(lost):
                                 assert torch.equal(r3[:, j], s3[:, blk]), (name, vname, blk)
                         eng.set_timing(True)
