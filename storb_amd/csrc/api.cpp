@@ -154,6 +154,9 @@ struct SubPlan {
     size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_tiles2 = 0, off_tail2 = 0;
     uint32_t ntail2 = 0;
     uint64_t syn_bytes = 0;  // syndrome scratch of this unit
+    // the syndrome chunks in parts (syn_parts): part p's tile ranges per phase-1 launch and per
+    // phase-2 group, so phase 2 of part p can overlap phase 1 of part p + 1 (launch_decode_sub)
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> syn1_parts, syn2_parts;
 };
 
 struct Plan {
@@ -271,13 +274,21 @@ int dec_copy_kb(int k)
 
 // Syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel, then sec_decode_kernel on the e
 // syndrome rows) for a chunk that lost e data blocks, when its shape has a bit-sliced kernel.
-// VALU estimate per 4 byte positions: the direct decode runs ceil(e / 8) v_perm row groups over
-// all k slots (5 selector ops + 4.5 per row and slot); the syndrome path runs the bit-sliced rows
-// of every NR-row parity group that holds a present row over the k - e present data blocks
-// (6 transpose + 2.75 subset + NR row ops), transposes the e syndromes back (6) and solves with
-// v_perm rows over the e syndromes.  It is used when it needs under SEC_SYN_RATIO (default 0.75)
-// of the direct path's VALU (it also moves 2 e B more bytes).  SEC_SYN=0 / 1 turns it off /
-// forces it wherever it applies; both read per plan build.
+// Chosen by a time estimate per 4 byte positions, each kernel taking the longer of its VALU
+// issue time and its HBM time (kVperOp = VALU ops per HBM byte at the measured rates: v_perm
+// rows ~2.8e13 ops/s, mixed traffic ~6 TB/s):
+//   direct:  ceil(e / 8) v_perm row groups (5 selector ops + 4.5 per row) over all k slots;
+//            reads k blocks per row group, writes the chunk (or the e rows);
+//   phase 1: the bit-sliced rows (6 transpose + 2.75 subsets + NR per row group holding a
+//            present parity row) over the k - e present data blocks, 6 per syndrome to transpose
+//            back; reads k blocks, writes the k - e copies (reassembly) and e syndromes;
+//   phase 2: v_perm rows over the e syndromes; reads them per row group, writes e rows.
+// Checked against the in-process A/B on the wide shapes (tools/syn_ab.py,
+// profiles/r03_syn_ab.jsonl): predicted syn / direct 0.70 / 0.95 / 1.16 / 1.40 / 1.25 against
+// measured 0.79 / 1.07 / 1.18 / 1.57 / 1.29 for zfec(64,96) 16 lost, (32,48) 16 and 8 lost,
+// (16,24) 8 and 4 lost; the path is taken when its estimate is under SEC_SYN_RATIO (default
+// 0.85) of the direct one.  SEC_SYN=0 / 1 turns it off / forces it wherever it applies; all
+// read per plan build.
 double vperm_ops(int rows, int slots)
 {
     double v = 0;
@@ -286,7 +297,7 @@ double vperm_ops(int rows, int slots)
     return v * slots;
 }
 
-int syn_choice(const sec_dec_chunk &c, const int *idx, int e)
+int syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies)
 {
     const char *env = getenv("SEC_SYN");
     if (env && env[0] == '0')
@@ -296,15 +307,19 @@ int syn_choice(const sec_dec_chunk &c, const int *idx, int e)
         return -1;
     if (env && env[0] == '1')
         return sh;
-    const int k = c.k, NR = sec_bs_rows(sh);
+    constexpr double kVperOp = 1.0 / 4.63;
+    const int k = c.k, NR = sec_bs_rows(sh), G = (e + sec::kMaxRows - 1) / sec::kMaxRows;
     uint64_t touched = 0;  // parity row groups that hold a present row
     for (int s = 0; s < k; ++s)
         if (idx[s] >= k)
             touched |= 1ull << ((idx[s] - k) / NR);
-    const double syn = __builtin_popcountll(touched) * (k - e) * (8.75 + NR) + 6.0 * e + vperm_ops(e, e);
+    auto t = [&](double ops, double bytes) { return std::max(ops * kVperOp, bytes); };
+    const double direct = t(vperm_ops(e, k), 4.0 * (k * G + (copies ? k : e)));
+    const double p1 = t(__builtin_popcountll(touched) * (k - e) * (8.75 + NR) + 6.0 * e, 4.0 * (k + (copies ? k : e)));
+    const double p2 = t(vperm_ops(e, e), 4.0 * (e * G + e));
     const char *ratio = getenv("SEC_SYN_RATIO");
-    const double lim = ratio && *ratio ? atof(ratio) : 0.75;
-    return syn < lim * vperm_ops(e, k) ? sh : -1;
+    const double lim = ratio && *ratio ? atof(ratio) : 0.85;
+    return p1 + p2 < lim * direct ? sh : -1;
 }
 
 // Work for one chunk.  `valid` = positions where every block is fully readable and
@@ -552,6 +567,8 @@ struct sec_ctx {
     DevBuf bn_scratch;  // host-mode staging of sec_bn_modexp / mulmod operands
     DevBuf bn_part;     // partial residues of segmented reductions (one region per slot)
     DevBuf syn;         // syndrome rows of device-mode syndrome decodes
+    hipStream_t aux = nullptr;                   // phase 2 of syndrome decodes (overlapped)
+    hipEvent_t syn_ev[9] = {};                   // per part + done
     size_t bn_part_stride = 0;
     Slot slots[kSlots];
     std::unique_ptr<sec::CopyPool> pool;
@@ -981,7 +998,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             bool whole = true;
             for (int s = 0; s < k && whole && !host; ++s)
                 whole = idx[s] == k - 1 || slot_avail(c, block_avail, L.perm[L.first[i] + s]) >= c.B;
-            const int sh = syn_of[i] = whole ? syn_choice(c, idx, (int)miss.size()) : -1;
+            const int sh = syn_of[i] = whole ? syn_choice(c, idx, (int)miss.size(), !recover && !nocopy) : -1;
             // the syndrome path's table is A^-1 (e x e), the direct path's the decode matrix rows
             std::string key = (sh >= 0 ? "S" : "") + std::to_string(k) + "/" + std::to_string(c.m) + ":";
             for (int s = 0; s < k; ++s)
@@ -1168,6 +1185,38 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             stl.insert(stl.end(), kv.second.begin(), kv.second.end());
         }
         sp.ntail2 = (uint32_t)tail2.size();
+        // parts of the syndrome chunks (tiles are in chunk order within every launch / group)
+        if (!sdescs.empty()) {
+            const int parts = (int)std::max<size_t>(1, std::min<size_t>(sdescs.size(), env_size("SEC_SYN_PARTS", 4)));
+            const uint32_t nd = (uint32_t)(c1 - c0);
+            auto ranges_of = [&](const sec::Tile *t, uint32_t n, uint32_t base, std::vector<std::pair<uint32_t, uint32_t>> &out,
+                                 size_t slot) {
+                uint32_t lo = 0;
+                for (int q = 0; q < parts; ++q) {
+                    const uint32_t bound = base + (uint32_t)(sdescs.size() * (size_t)(q + 1) / parts);
+                    uint32_t hi = lo;
+                    while (hi < n && t[hi].chunk < bound)
+                        ++hi;
+                    sp.syn1_parts.resize(parts);
+                    sp.syn2_parts.resize(parts);
+                    (void)out;
+                    auto &dst = slot == 0 ? sp.syn1_parts[q] : sp.syn2_parts[q];
+                    dst.push_back({lo, hi - lo});
+                    lo = hi;
+                }
+                return lo == n;  // every tile in one part (chunk order held)
+            };
+            bool ok = true;
+            std::vector<std::pair<uint32_t, uint32_t>> unused;
+            for (auto &g : sp.syn1)
+                ok = ranges_of(stl.data() + g.second.first, g.second.second, 0, unused, 0) && ok;
+            for (auto &g : sp.groups2)
+                ok = ranges_of(tiles2.data() + g.first, g.count, nd, unused, 1) && ok;
+            if (!ok || parts == 1) {
+                sp.syn1_parts.clear();
+                sp.syn2_parts.clear();
+            }
+        }
         sp.off_sdesc = img.put(sdescs.data(), sdescs.size() * sizeof(sec::SynDesc));
         sp.off_stiles = img.put(stl.data(), stl.size() * sizeof(sec::Tile));
         sp.off_ssoff = img.put(ssoff.data(), ssoff.size() * 8);
@@ -1220,18 +1269,47 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::Tile *st = plan.meta.as<sec::Tile>(sp.off_stiles);
     const sec::SynSlots ss{plan.meta.as<uint64_t>(sp.off_ssoff), plan.meta.as<uint32_t>(sp.off_ssavail)};
     const int lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
-    for (auto &g : sp.syn1) {
-        int e = sec_launch_syndrome_bs(g.first, lanes, blocks, out, syn, sd, st + g.second.first, g.second.second, ss,
-                                       s);
-        if (e)
-            return hip_fail((hipError_t)e, "sec_syndrome_bs_kernel");
-    }
     const sec::Tile *dt2 = plan.meta.as<sec::Tile>(sp.off_tiles2);
-    for (const Group &g : sp.groups2) {
-        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, syn, out, dd, dt2 + g.first, g.count, tabs, sl, s,
+    auto phase1 = [&](size_t i, uint32_t first, uint32_t count) {
+        const auto &g = sp.syn1[i];
+        int e = sec_launch_syndrome_bs(g.first, lanes, blocks, out, syn, sd, st + g.second.first + first, count, ss, s);
+        return e ? hip_fail((hipError_t)e, "sec_syndrome_bs_kernel") : SEC_OK;
+    };
+    auto phase2 = [&](size_t i, uint32_t first, uint32_t count, hipStream_t q) {
+        const Group &g = sp.groups2[i];
+        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, syn, out, dd, dt2 + g.first + first, count, tabs, sl, q,
                                   g.mfma);
-        if (e)
-            return hip_fail((hipError_t)e, "sec_decode_kernel");
+        return e ? hip_fail((hipError_t)e, "sec_decode_kernel") : SEC_OK;
+    };
+    const size_t parts = sp.syn1_parts.size();
+    if (parts > 1 && !ctx->aux) {
+        CK(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+        for (hipEvent_t &e : ctx->syn_ev)
+            CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (parts > 1 && parts < 9) {
+        // phase 1 of every part on s; phase 2 of part p on the aux stream once part p's
+        // syndromes are there, so it runs beside phase 1 of the later parts (phase 1 is
+        // memory-bound, phase 2 VALU-bound); s then waits for the aux stream
+        for (size_t p = 0; p < parts; ++p) {
+            for (size_t i = 0; i < sp.syn1.size(); ++i)
+                if (sp.syn1_parts[p][i].second)
+                    RC(phase1(i, sp.syn1_parts[p][i].first, sp.syn1_parts[p][i].second));
+            CK(hipEventRecord(ctx->syn_ev[p], s));
+        }
+        for (size_t p = 0; p < parts; ++p) {
+            CK(hipStreamWaitEvent(ctx->aux, ctx->syn_ev[p], 0));
+            for (size_t i = 0; i < sp.groups2.size(); ++i)
+                if (sp.syn2_parts[p][i].second)
+                    RC(phase2(i, sp.syn2_parts[p][i].first, sp.syn2_parts[p][i].second, ctx->aux));
+        }
+        CK(hipEventRecord(ctx->syn_ev[8], ctx->aux));
+        CK(hipStreamWaitEvent(s, ctx->syn_ev[8], 0));
+    } else {
+        for (size_t i = 0; i < sp.syn1.size(); ++i)
+            RC(phase1(i, 0, sp.syn1[i].second.second));
+        for (size_t i = 0; i < sp.groups2.size(); ++i)
+            RC(phase2(i, 0, sp.groups2[i].count, s));
     }
     if (sp.ntail2) {
         int e = sec_launch_decode_tail(syn, out, dd, plan.meta.as<sec::TailItem>(sp.off_tail2), sp.ntail2, tabs, sl,
@@ -1621,6 +1699,13 @@ void sec_ctx_destroy(sec_ctx *ctx)
     ctx->bn_scratch.release();
     ctx->bn_part.release();
     ctx->syn.release();
+    for (hipEvent_t e : ctx->syn_ev)
+        if (e)
+            (void)hipEventDestroy(e);
+    if (ctx->aux) {
+        (void)hipStreamSynchronize(ctx->aux);
+        (void)hipStreamDestroy(ctx->aux);
+    }
     if (ctx->own)
         (void)hipStreamDestroy(ctx->own);
     delete ctx;
