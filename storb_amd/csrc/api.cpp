@@ -151,12 +151,9 @@ struct SubPlan {
     // groups (sec_decode_kernel over the syndrome rows) and their tail items
     std::vector<std::pair<int, std::pair<uint32_t, uint32_t>>> syn1;  // (shape, (first, count)) in syn tiles
     std::vector<Group> groups2;
-    size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_tiles2 = 0, off_tail2 = 0;
+    size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_smrow = 0, off_tiles2 = 0, off_tail2 = 0;
     uint32_t ntail2 = 0;
     uint64_t syn_bytes = 0;  // syndrome scratch of this unit
-    // the syndrome chunks in parts (syn_parts): part p's tile ranges per phase-1 launch and per
-    // phase-2 group, so phase 2 of part p can overlap phase 1 of part p + 1 (launch_decode_sub)
-    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> syn1_parts, syn2_parts;
 };
 
 struct Plan {
@@ -272,23 +269,28 @@ int dec_copy_kb(int k)
     return (v == 4 || v == 8) && (size_t)k <= v ? (int)v : 0;
 }
 
-// Syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel, then sec_decode_kernel on the e
-// syndrome rows) for a chunk that lost e data blocks, when its shape has a bit-sliced kernel.
-// Chosen by a time estimate per 4 byte positions, each kernel taking the longer of its VALU
-// issue time and its HBM time (kVperOp = VALU ops per HBM byte at the measured rates: v_perm
-// rows ~2.8e13 ops/s, mixed traffic ~6 TB/s):
+// Syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel) for a chunk that lost e data blocks,
+// when its shape has a bit-sliced kernel: the syndromes of its e present parity rows, then the
+// e x e solve, either in the same kernel (fused: every present parity row in one row group, the
+// syndromes never leave the registers) or by sec_decode_kernel over the syndrome rows stored to
+// a scratch buffer (two-phase).  Chosen by a time estimate per 4 byte positions, each kernel
+// taking the longer of its VALU issue time and its HBM time (kVperOp = VALU ops per HBM byte
+// at the measured rates: v_perm rows ~2.8e13 ops/s, mixed traffic ~6 TB/s):
 //   direct:  ceil(e / 8) v_perm row groups (5 selector ops + 4.5 per row) over all k slots;
 //            reads k blocks per row group, writes the chunk (or the e rows);
 //   phase 1: the bit-sliced rows (6 transpose + 2.75 subsets + NR per row group holding a
 //            present parity row) over the k - e present data blocks, 6 per syndrome to transpose
 //            back; reads k blocks, writes the k - e copies (reassembly) and e syndromes;
-//   phase 2: v_perm rows over the e syndromes; reads them per row group, writes e rows.
-// Checked against the in-process A/B on the wide shapes (tools/syn_ab.py,
+//   phase 2: v_perm rows over the e syndromes; reads them per row group, writes e rows;
+//   fused:   phase 1 + per pass of 4 output rows the selectors (5) of all NR rows of the group
+//            and 5 per product (absent rows have zero coefficients); reads k, writes the chunk.
+// The two-phase estimate was checked against the in-process A/B (tools/syn_ab.py,
 // profiles/r03_syn_ab.jsonl): predicted syn / direct 0.70 / 0.95 / 1.16 / 1.40 / 1.25 against
 // measured 0.79 / 1.07 / 1.18 / 1.57 / 1.29 for zfec(64,96) 16 lost, (32,48) 16 and 8 lost,
-// (16,24) 8 and 4 lost; the path is taken when its estimate is under SEC_SYN_RATIO (default
-// 0.85) of the direct one.  SEC_SYN=0 / 1 turns it off / forces it wherever it applies; all
-// read per plan build.
+// (16,24) 8 and 4 lost.  A path is taken when its estimate is under SEC_SYN_RATIO (default
+// 0.85) of the direct one.  SEC_SYN=0 turns both off, SEC_SYN=1 forces the syndrome path
+// wherever it applies (fused when it can be), SEC_SYN_FUSED=0 never fuses; all read per plan
+// build.
 double vperm_ops(int rows, int slots)
 {
     double v = 0;
@@ -297,29 +299,43 @@ double vperm_ops(int rows, int slots)
     return v * slots;
 }
 
-int syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies)
+constexpr int kFusedRows = 4;  // output rows per pass of the fused solve (kernels_bs.hip fused_rows)
+
+struct SynPick {
+    int shape = -1;  // bit-sliced shape, or -1: the direct decode
+    bool fused = false;
+};
+
+SynPick syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies)
 {
     const char *env = getenv("SEC_SYN");
     if (env && env[0] == '0')
-        return -1;
+        return {};
     const int sh = sec_syn_shape(c.k, c.m);
     if (sh < 0 || e < 1 || c.B < 16 || c.B > 0xFFFFFFFFull - 8192 || c.padlen >= c.B)
-        return -1;
-    if (env && env[0] == '1')
-        return sh;
-    constexpr double kVperOp = 1.0 / 4.63;
+        return {};
     const int k = c.k, NR = sec_bs_rows(sh), G = (e + sec::kMaxRows - 1) / sec::kMaxRows;
     uint64_t touched = 0;  // parity row groups that hold a present row
     for (int s = 0; s < k; ++s)
         if (idx[s] >= k)
             touched |= 1ull << ((idx[s] - k) / NR);
+    const int T = __builtin_popcountll(touched);
+    const char *fe = getenv("SEC_SYN_FUSED");
+    const bool can_fuse = T == 1 && !(fe && fe[0] == '0');
+    if (env && env[0] == '1')
+        return {sh, can_fuse};
+    constexpr double kVperOp = 1.0 / 4.63;
     auto t = [&](double ops, double bytes) { return std::max(ops * kVperOp, bytes); };
     const double direct = t(vperm_ops(e, k), 4.0 * (k * G + (copies ? k : e)));
-    const double p1 = t(__builtin_popcountll(touched) * (k - e) * (8.75 + NR) + 6.0 * e, 4.0 * (k + (copies ? k : e)));
-    const double p2 = t(vperm_ops(e, e), 4.0 * (e * G + e));
+    const double v1 = T * (k - e) * (8.75 + NR) + 6.0 * e;
+    const double two = t(v1, 4.0 * (k + (copies ? k : e))) + t(vperm_ops(e, e), 4.0 * (e * G + e));
+    const int passes = (e + kFusedRows - 1) / kFusedRows;
+    const double fused = t(v1 + NR * passes * (5.0 + 5.0 * kFusedRows), 4.0 * (k + (copies ? k : e)));
     const char *ratio = getenv("SEC_SYN_RATIO");
-    const double lim = ratio && *ratio ? atof(ratio) : 0.85;
-    return p1 + p2 < lim * direct ? sh : -1;
+    const double lim = (ratio && *ratio ? atof(ratio) : 0.85) * direct;
+    if (can_fuse && fused < lim && fused <= two)
+        return {sh, true};
+    return two < lim ? SynPick{sh, false} : SynPick{};
 }
 
 // Work for one chunk.  `valid` = positions where every block is fully readable and
@@ -567,8 +583,6 @@ struct sec_ctx {
     DevBuf bn_scratch;  // host-mode staging of sec_bn_modexp / mulmod operands
     DevBuf bn_part;     // partial residues of segmented reductions (one region per slot)
     DevBuf syn;         // syndrome rows of device-mode syndrome decodes
-    hipStream_t aux = nullptr;                   // phase 2 of syndrome decodes (overlapped)
-    hipEvent_t syn_ev[9] = {};                   // per part + done
     size_t bn_part_stride = 0;
     Slot slots[kSlots];
     std::unique_ptr<sec::CopyPool> pool;
@@ -977,7 +991,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
     TableCache &tc = ctx->dec_tabs;
     std::vector<PendingExpand> pending;
     std::vector<uint32_t> tab_of((size_t)nchunks, 0), e_of((size_t)nchunks, 0);
-    std::vector<int> syn_of((size_t)nchunks, -1);  // syndrome-decode shape, or -1 (syn_choice)
+    std::vector<SynPick> syn_of((size_t)nchunks);  // syndrome decodes (syn_choice)
     for (int attempt = 0;; ++attempt) {
         pending.clear();
         size_t need = 0;
@@ -998,9 +1012,11 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             bool whole = true;
             for (int s = 0; s < k && whole && !host; ++s)
                 whole = idx[s] == k - 1 || slot_avail(c, block_avail, L.perm[L.first[i] + s]) >= c.B;
-            const int sh = syn_of[i] = whole ? syn_choice(c, idx, (int)miss.size(), !recover && !nocopy) : -1;
-            // the syndrome path's table is A^-1 (e x e), the direct path's the decode matrix rows
-            std::string key = (sh >= 0 ? "S" : "") + std::to_string(k) + "/" + std::to_string(c.m) + ":";
+            const SynPick pick = syn_of[i] = whole ? syn_choice(c, idx, (int)miss.size(), !recover && !nocopy) : SynPick{};
+            const int sh = pick.shape;
+            // the syndrome path's table is A^-1 (e x e; fused: by parity row of the group, e padded),
+            // the direct path's the decode matrix rows
+            std::string key = (sh < 0 ? "" : pick.fused ? "F" : "S") + std::to_string(k) + "/" + std::to_string(c.m) + ":";
             for (int s = 0; s < k; ++s)
                 key += std::to_string(idx[s]) + ",";
             auto it = tc.index.find(key);
@@ -1025,10 +1041,21 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                         a[(size_t)q * e + r] = enc[(size_t)prow[q] * k + miss[r]];
                 if (!sec::gf_invert(a, e))
                     return SEC_ESINGULAR;
-                coef.resize((size_t)e * e);
-                for (int q = 0; q < e; ++q)  // layout [slot q][missing r]
-                    for (int r = 0; r < e; ++r)
-                        coef[(size_t)q * e + r] = a[(size_t)r * e + q];
+                if (pick.fused) {
+                    // layout [parity row r of the group][lost o, padded to whole passes]: the
+                    // kernel runs every row of the group, absent ones with zero coefficients
+                    const int NR = sec_bs_rows(sh), ep = (e + kFusedRows - 1) / kFusedRows * kFusedRows;
+                    const int r0 = (prow[0] - k) / NR * NR;
+                    coef.assign((size_t)NR * ep, 0);
+                    for (int q = 0; q < e; ++q)
+                        for (int o = 0; o < e; ++o)
+                            coef[(size_t)(prow[q] - k - r0) * ep + o] = a[(size_t)o * e + q];
+                } else {
+                    coef.resize((size_t)e * e);
+                    for (int q = 0; q < e; ++q)  // layout [slot q][missing r]
+                        for (int r = 0; r < e; ++r)
+                            coef[(size_t)q * e + r] = a[(size_t)r * e + q];
+                }
             } else {
                 std::vector<int> iv(idx, idx + k);
                 std::vector<uint8_t> minv;
@@ -1057,7 +1084,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
     plan.nsyn = plan.ndirect = 0;
     for (int64_t i = 0; i < nchunks; ++i)
         if (e_of[i])
-            ++(syn_of[i] >= 0 ? plan.nsyn : plan.ndirect);
+            ++(syn_of[i].shape >= 0 ? plan.nsyn : plan.ndirect);
     std::vector<std::pair<int64_t, int64_t>> ranges;
     if (host) {
         std::vector<uint64_t> ib((size_t)nchunks);
@@ -1082,7 +1109,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         // descriptors (appended to descs), tiles and tail items
         std::vector<sec::SynDesc> sdescs;
         std::vector<uint64_t> ssoff;
-        std::vector<uint32_t> ssavail;
+        std::vector<uint32_t> ssavail, smrow;
         std::map<int, std::vector<sec::Tile>> stiles;
         std::vector<sec::DecDesc> descs2;
         Bins bins2;
@@ -1124,7 +1151,8 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)c.B));
             sp.in_bytes += (uint64_t)c.k * c.B;
             sp.out_bytes += nout;
-            const int sh = syn_of[i];
+            const int sh = syn_of[i].shape;
+            const bool fused = syn_of[i].fused;
             if (sh >= 0 && nout > 0) {
                 // phase 1: every present block in place, syndromes to the scratch
                 const int k = c.k, p = c.m - c.k, e = (int)e_of[i], NR = sec_bs_rows(sh);
@@ -1133,7 +1161,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 sd.out_off = d.out_off;
                 sd.syn_off = sp.syn_bytes;
                 sd.B = (uint32_t)c.B;
-                sd.last = copies ? (uint32_t)(nout - (uint64_t)(k - 1) * c.B) : 0;
+                sd.last = recover ? (uint32_t)c.B : (uint32_t)(nout - (uint64_t)(k - 1) * c.B);
                 sd.slot0 = (uint32_t)ssoff.size();
                 ssoff.resize(ssoff.size() + (size_t)(k + p), 0);
                 ssavail.resize(ssavail.size() + (size_t)(k + p), 0);
@@ -1143,7 +1171,14 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                     ssoff[j] = soff[slot0 + s];
                     ssavail[j] = savail[slot0 + s];
                 }
-                sp.syn_bytes += (uint64_t)e * c.B;
+                if (fused) {  // the lost blocks straight to their output rows
+                    sd.tab = tab_of[i];
+                    sd.e = (uint32_t)e;
+                    sd.mrow0 = (uint32_t)smrow.size();
+                    smrow.insert(smrow.end(), mr.begin(), mr.begin() + e);
+                } else {
+                    sp.syn_bytes += (uint64_t)e * c.B;
+                }
                 std::vector<int> gs;  // touched row groups, ascending
                 for (int g = 0; g * NR < p; ++g)
                     if ((sd.pmask >> (g * NR)) & ((NR >= 64 ? ~0ull : (1ull << NR) - 1)))
@@ -1151,11 +1186,13 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 const uint32_t si = (uint32_t)sdescs.size();
                 sdescs.push_back(sd);
                 const uint64_t step = (uint64_t)sec_bs_span() * (syn_lanes / 64);
-                auto &st = stiles[sh];
+                auto &st = stiles[sh * 2 + (fused ? 1 : 0)];
                 for (uint64_t t0 = 0; t0 < c.B; t0 += 8 * step)  // runs of 8 positions per group: one XCD
                     for (int g : gs)
                         for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
                             st.push_back(sec::Tile{si, (uint32_t)t, (uint32_t)(g * NR), copies && g == gs[0] ? 1u : 0u});
+                if (fused)
+                    continue;
                 // phase 2: the e syndrome rows are the slots of a plain decode whose matrix is A^-1
                 sec::DecDesc d2 = d;
                 d2.k = (uint32_t)e;
@@ -1185,42 +1222,11 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             stl.insert(stl.end(), kv.second.begin(), kv.second.end());
         }
         sp.ntail2 = (uint32_t)tail2.size();
-        // parts of the syndrome chunks (tiles are in chunk order within every launch / group)
-        if (!sdescs.empty()) {
-            const int parts = (int)std::max<size_t>(1, std::min<size_t>(sdescs.size(), env_size("SEC_SYN_PARTS", 4)));
-            const uint32_t nd = (uint32_t)(c1 - c0);
-            auto ranges_of = [&](const sec::Tile *t, uint32_t n, uint32_t base, std::vector<std::pair<uint32_t, uint32_t>> &out,
-                                 size_t slot) {
-                uint32_t lo = 0;
-                for (int q = 0; q < parts; ++q) {
-                    const uint32_t bound = base + (uint32_t)(sdescs.size() * (size_t)(q + 1) / parts);
-                    uint32_t hi = lo;
-                    while (hi < n && t[hi].chunk < bound)
-                        ++hi;
-                    sp.syn1_parts.resize(parts);
-                    sp.syn2_parts.resize(parts);
-                    (void)out;
-                    auto &dst = slot == 0 ? sp.syn1_parts[q] : sp.syn2_parts[q];
-                    dst.push_back({lo, hi - lo});
-                    lo = hi;
-                }
-                return lo == n;  // every tile in one part (chunk order held)
-            };
-            bool ok = true;
-            std::vector<std::pair<uint32_t, uint32_t>> unused;
-            for (auto &g : sp.syn1)
-                ok = ranges_of(stl.data() + g.second.first, g.second.second, 0, unused, 0) && ok;
-            for (auto &g : sp.groups2)
-                ok = ranges_of(tiles2.data() + g.first, g.count, nd, unused, 1) && ok;
-            if (!ok || parts == 1) {
-                sp.syn1_parts.clear();
-                sp.syn2_parts.clear();
-            }
-        }
         sp.off_sdesc = img.put(sdescs.data(), sdescs.size() * sizeof(sec::SynDesc));
         sp.off_stiles = img.put(stl.data(), stl.size() * sizeof(sec::Tile));
         sp.off_ssoff = img.put(ssoff.data(), ssoff.size() * 8);
         sp.off_ssavail = img.put(ssavail.data(), ssavail.size() * 4);
+        sp.off_smrow = img.put(smrow.data(), smrow.size() * 4);
         sp.off_tiles2 = img.put(tiles2.data(), tiles2.size() * sizeof(sec::Tile));
         sp.off_tail2 = img.put(tail2.data(), tail2.size() * sizeof(sec::TailItem));
         sp.ntail = (uint32_t)tail.size();
@@ -1261,18 +1267,20 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     }
     if (sp.syn1.empty())
         return SEC_OK;
-    if (!syn)
+    if (!syn && sp.syn_bytes)
         return SEC_EINVAL;
     // syndrome decodes: phase 1 (syndromes + present primaries' copies), then phase 2 on the
     // syndrome rows (blocks = the scratch), in stream order
     const sec::SynDesc *sd = plan.meta.as<sec::SynDesc>(sp.off_sdesc);
     const sec::Tile *st = plan.meta.as<sec::Tile>(sp.off_stiles);
-    const sec::SynSlots ss{plan.meta.as<uint64_t>(sp.off_ssoff), plan.meta.as<uint32_t>(sp.off_ssavail)};
+    const sec::SynSlots ss{plan.meta.as<uint64_t>(sp.off_ssoff), plan.meta.as<uint32_t>(sp.off_ssavail),
+                           plan.meta.as<uint32_t>(sp.off_smrow), tabs};
     const int lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
     const sec::Tile *dt2 = plan.meta.as<sec::Tile>(sp.off_tiles2);
     auto phase1 = [&](size_t i, uint32_t first, uint32_t count) {
         const auto &g = sp.syn1[i];
-        int e = sec_launch_syndrome_bs(g.first, lanes, blocks, out, syn, sd, st + g.second.first + first, count, ss, s);
+        int e = sec_launch_syndrome_bs(g.first / 2, g.first % 2, lanes, blocks, out, syn, sd, st + g.second.first + first,
+                                       count, ss, s);
         return e ? hip_fail((hipError_t)e, "sec_syndrome_bs_kernel") : SEC_OK;
     };
     auto phase2 = [&](size_t i, uint32_t first, uint32_t count, hipStream_t q) {
@@ -1281,36 +1289,10 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
                                   g.mfma);
         return e ? hip_fail((hipError_t)e, "sec_decode_kernel") : SEC_OK;
     };
-    const size_t parts = sp.syn1_parts.size();
-    if (parts > 1 && !ctx->aux) {
-        CK(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
-        for (hipEvent_t &e : ctx->syn_ev)
-            CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    if (parts > 1 && parts < 9) {
-        // phase 1 of every part on s; phase 2 of part p on the aux stream once part p's
-        // syndromes are there, so it runs beside phase 1 of the later parts (phase 1 is
-        // memory-bound, phase 2 VALU-bound); s then waits for the aux stream
-        for (size_t p = 0; p < parts; ++p) {
-            for (size_t i = 0; i < sp.syn1.size(); ++i)
-                if (sp.syn1_parts[p][i].second)
-                    RC(phase1(i, sp.syn1_parts[p][i].first, sp.syn1_parts[p][i].second));
-            CK(hipEventRecord(ctx->syn_ev[p], s));
-        }
-        for (size_t p = 0; p < parts; ++p) {
-            CK(hipStreamWaitEvent(ctx->aux, ctx->syn_ev[p], 0));
-            for (size_t i = 0; i < sp.groups2.size(); ++i)
-                if (sp.syn2_parts[p][i].second)
-                    RC(phase2(i, sp.syn2_parts[p][i].first, sp.syn2_parts[p][i].second, ctx->aux));
-        }
-        CK(hipEventRecord(ctx->syn_ev[8], ctx->aux));
-        CK(hipStreamWaitEvent(s, ctx->syn_ev[8], 0));
-    } else {
-        for (size_t i = 0; i < sp.syn1.size(); ++i)
-            RC(phase1(i, 0, sp.syn1[i].second.second));
-        for (size_t i = 0; i < sp.groups2.size(); ++i)
-            RC(phase2(i, 0, sp.groups2[i].count, s));
-    }
+    for (size_t i = 0; i < sp.syn1.size(); ++i)
+        RC(phase1(i, 0, sp.syn1[i].second.second));
+    for (size_t i = 0; i < sp.groups2.size(); ++i)
+        RC(phase2(i, 0, sp.groups2[i].count, s));
     if (sp.ntail2) {
         int e = sec_launch_decode_tail(syn, out, dd, plan.meta.as<sec::TailItem>(sp.off_tail2), sp.ntail2, tabs, sl,
                                        s);
@@ -1699,13 +1681,6 @@ void sec_ctx_destroy(sec_ctx *ctx)
     ctx->bn_scratch.release();
     ctx->bn_part.release();
     ctx->syn.release();
-    for (hipEvent_t e : ctx->syn_ev)
-        if (e)
-            (void)hipEventDestroy(e);
-    if (ctx->aux) {
-        (void)hipStreamSynchronize(ctx->aux);
-        (void)hipStreamDestroy(ctx->aux);
-    }
     if (ctx->own)
         (void)hipStreamDestroy(ctx->own);
     delete ctx;
