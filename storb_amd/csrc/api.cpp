@@ -143,6 +143,8 @@ struct SubPlan {
     size_t off_msgs = 0;                   // messages of this unit (SHA-1, bignum)
     uint32_t nmsgs = 0;
     bool sha_split = false;  // SHA-1 messages: the two-wave kernel (sha1_split)
+    int flat_shape = -1;     // encode: the unit is one flat bit-sliced launch (FlatEnc) of this shape
+    sec::FlatEnc flat{};
     size_t off_segs = 0, off_seginfo = 0;  // bignum: segments of the messages, per-message (first, count)
     uint32_t nsegs = 0, max_seg = 0;       // segment count; most segments of one message
     uint64_t dig_first = 0;                // first digest slot of this unit
@@ -790,6 +792,52 @@ int check_sharenums(int k, int m, const int32_t *s)
 uint64_t enc_B(const sec_enc_chunk &c) { return (c.n + (uint64_t)c.k - 1) / (uint64_t)c.k; }
 
 // ---- encode plan ------------------------------------------------------------
+// Flat bit-sliced encode (kernels_bs.hip sec_encode_bs_flat_kernel): a unit whose chunks all have
+// the same (k, m, n), a one-group bit-sliced shape and constant input / parity strides runs as
+// one launch whose waves span chunk boundaries, when whole 2048-position wave spans per chunk
+// would waste more than 3 % of the waves (C4: B = 6554 in 4 spans, 20 % fewer waves flat).
+// Host slabs are dense, so their uniform units qualify too.  SEC_BS_FLAT=0 turns it off (read
+// per plan build).  Fills sp.flat / sp.flat_shape; returns whether the unit is flat.
+bool flat_unit(const sec_enc_chunk *chunks, int64_t c0, int64_t c1, bool host, SubPlan &sp)
+{
+    sp.flat_shape = -1;
+    const char *e = getenv("SEC_BS_FLAT");
+    if ((e && e[0] == '0') || c1 <= c0)
+        return false;
+    const sec_enc_chunk &a = chunks[c0];
+    const uint64_t B = enc_B(a);
+    const int shape = a.m > a.k ? bs_shape(a.k, a.m, B) : -1;
+    if (shape < 0 || sec_bs_groups(shape) != 1)
+        return false;
+    const uint64_t span = sec_bs_span(), Bv = (B + 15) / 16 * 16;
+    if ((B + span - 1) / span * span - B <= B * 3 / 100)
+        return false;
+    const uint64_t n = (uint64_t)(c1 - c0);
+    if (n * Bv > 0xFFFFFFFFull)
+        return false;
+    const uint64_t p = (uint64_t)(a.m - a.k);
+    uint64_t in0 = 0, istr = a.n, par0 = 0, pstr = p * B, rstr = B;  // host slabs: dense
+    if (!host) {
+        in0 = a.in_off;
+        par0 = a.parity_off;
+        rstr = a.parity_stride;
+        istr = n > 1 ? chunks[c0 + 1].in_off - a.in_off : a.n;
+        pstr = n > 1 ? chunks[c0 + 1].parity_off - a.parity_off : p * rstr;
+    }
+    for (int64_t i = c0; i < c1; ++i) {
+        const sec_enc_chunk &c = chunks[i];
+        const uint64_t j = (uint64_t)(i - c0);
+        if (c.k != a.k || c.m != a.m || c.n != a.n)
+            return false;
+        if (!host && (c.in_off != in0 + j * istr || c.parity_off != par0 + j * pstr || c.parity_stride != rstr))
+            return false;
+    }
+    sp.flat_shape = shape;
+    sp.flat = sec::FlatEnc{in0, istr, par0, pstr, rstr, n * Bv, (uint32_t)B, (uint32_t)Bv,
+                           (uint32_t)(a.n - (uint64_t)(a.k - 1) * B), 0};
+    return true;
+}
+
 int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, bool host, bool digest)
 {
     Plan &plan = ctx->enc_plan;
@@ -860,6 +908,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
         Bins bins;
         std::vector<sec::TailItem> tail;
         std::vector<sec::MsgDesc> msgs;
+        const bool flat_ok = flat_unit(chunks, c0, c1, host, sp);
         for (int64_t i = c0; i < c1; ++i) {
             const sec_enc_chunk &c = chunks[i];
             const uint64_t B = enc_B(c);
@@ -889,6 +938,8 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
             const int bs = p > 0 ? bs_shape(c.k, c.m, B) : -1;
+            if (bs >= 0 && flat_ok)
+                continue;  // the whole unit is one flat launch (below)
             if (bs >= 0)
                 add_bs_work(bins, (uint32_t)(i - c0), B, bs);
             else if (p > 0)
@@ -919,6 +970,12 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::EncDesc *dd = plan.meta.as<sec::EncDesc>(sp.off_desc);
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
+    if (sp.flat_shape >= 0) {
+        const int lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
+        int e = sec_launch_encode_bs_flat(sp.flat_shape, 0, lanes, in, par, sp.flat, s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_encode_bs_flat_kernel");
+    }
     for (const Group &g : sp.groups) {
         int e = g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsAllGroups ? -1 : g.U, g.lanes, in, par, dd,
                                                    dt + g.first, g.count, s)
