@@ -114,6 +114,14 @@ class EncodedPieces(BaseModel):  # piece.py:50-51
 
 _pools: dict = {}
 _pools_lock = threading.Lock()
+HASH_WORKERS = 16  # at most this many hash-pool threads (piece copies and hashlib SHA-1)
+
+
+def _usable_cpus() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 2
 
 
 def _pool(name: str) -> ThreadPoolExecutor:
@@ -124,7 +132,7 @@ def _pool(name: str) -> ThreadPoolExecutor:
     with _pools_lock:
         p = _pools.get(name)
         if p is None:
-            n = STREAM_WORKERS if name == "stream" else max(1, min(8, (os.cpu_count() or 2) - 1))
+            n = STREAM_WORKERS if name == "stream" else max(1, min(HASH_WORKERS, _usable_cpus() - 1))
             p = _pools[name] = ThreadPoolExecutor(n, thread_name_prefix=f"storb_amd_{name}")
         return p
 
@@ -332,30 +340,46 @@ def _fill(dst: np.ndarray, src: np.ndarray) -> None:
         dst[len(src):] = 0
 
 
-def _pieces_parallel(chunks: list, shapes: list, digests: bool = False):
+def _hash_filled(fill: Future, view: np.ndarray) -> str:
+    """SHA-1 hex of a piece once its fill (an earlier task of the same FIFO pool) is done."""
+    fill.result()
+    return hashlib.sha1(view).hexdigest()
+
+
+def _pieces_parallel(chunks: list, shapes: list, digests: bool = False, hash_ids: bool = False):
     """Every chunk's m pieces as bytes (k zero-padded data slices, then the parity): one GPU
     call for all chunks; the piece copies run on the hash pool, the data slices beside the GPU
     call.  Returns once every piece is filled.  ``digests=True``: (pieces, ids), ids[i] = the
-    piece ids (SHA-1 hex) of chunk i's m pieces, hashed on the GPU after the encode."""
+    piece ids (SHA-1 hex) of chunk i's m pieces, hashed on the GPU after the encode.
+    ``hash_ids=True``: (pieces, futures), futures[i][j] = the hashlib SHA-1 hex of piece j of
+    chunk i, each started as soon as that piece is filled (data pieces beside the GPU call) and
+    still running when this returns."""
     hp = _pool("hash")
-    out, jobs = [], []
+    out, jobs, hfut = [], [], []
     for c, (k, m, B, _) in zip(chunks, shapes):
         if k > 1 and (k - 1) * B > len(c):  # easyfec's short middle slice, as Encoder.encode
             raise Error("Precondition violation: Input blocks are required to be all the same length.")
         src = np.frombuffer(memoryview(c).cast("B"), dtype=np.uint8)
-        ps = []
+        ps, views = [], []
         for j in range(k):
             b, v = _new_bytes(B)
             ps.append(b)
+            views.append(v)
             jobs.append(hp.submit(_fill, v, src[j * B:min((j + 1) * B, len(src))]))
         out.append(ps)
+        if hash_ids:  # queued behind this chunk's data fills (FIFO), so they never wait long
+            hfut.append([hp.submit(_hash_filled, f, v) for f, v in zip(jobs[-k:], views)])
     res = get_engine().encode_host_raw(list(chunks), [(k, m) for (k, m, _, _) in shapes], digests=digests)
     buf, layout = res[0], res[1]
-    for ps, (o, B, p) in zip(out, layout):
+    for i, (ps, (o, B, p)) in enumerate(zip(out, layout)):
+        pj = []
         for r in range(p):
             b, v = _new_bytes(B)
             ps.append(b)
             jobs.append(hp.submit(_fill, v, buf[o + r * B:o + (r + 1) * B]))
+            pj.append((jobs[-1], v))
+        if hash_ids:
+            hfut[i].extend(hp.submit(_hash_filled, f, v) for f, v in pj)
     ids = None
     if digests:
         hx, ids, f = res[2].tobytes().hex(), [], 0
@@ -366,6 +390,8 @@ def _pieces_parallel(chunks: list, shapes: list, digests: bool = False):
         f.result()
     if not _FILL_IN_PLACE:
         out = [[_finalize(p) for p in ps] for ps in out]
+    if hash_ids:
+        return out, hfut
     return (out, ids) if digests else out
 
 
@@ -391,9 +417,9 @@ def encode_chunk(chunk: bytes, chunk_idx: int) -> EncodedChunk:
         encoded_pieces = enc_.encode(chunk)
     else:  # piece ids hashed on the pool: data pieces beside the GPU call, parity right after
         hp = _pool("hash")
-        if B >= PARALLEL_COPY_MIN:  # large pieces: their copies on the pool as well
-            encoded_pieces = _pieces_parallel([chunk], [(k, m, B, padlen)])[0]
-            futs = [hp.submit(_sha1_hex, b) for b in encoded_pieces]
+        if B >= PARALLEL_COPY_MIN:  # large pieces: their copies on the pool as well, each hashed once filled
+            pieces, hf = _pieces_parallel([chunk], [(k, m, B, padlen)], hash_ids=True)
+            encoded_pieces, futs = pieces[0], hf[0]
         else:
             prim = _split(chunk, k, B)
             futs = [hp.submit(_sha1_hex, b) for b in prim]
