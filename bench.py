@@ -626,9 +626,8 @@ def main_c4(args, ctx):
     if ctx.rank != 0:
         return
     enc_gbs = _gbs(enc_alg, r["enc_avg_s"])
-    kernel = ("sec_encode_kernel<4, 1, false>" if os.environ.get("SEC_BS") == "0"  # api.cpp bs_shape / flat_unit
-              else "sec_encode_bs_kernel<10, 14, 0, 4, 5>" if os.environ.get("SEC_BS_FLAT") == "0"
-              else "sec_encode_bs_flat_kernel<10, 14, 0, 4, 5>")
+    kernel = ("sec_encode_kernel<4, 1, false>" if os.environ.get("SEC_BS") == "0"
+              else "sec_encode_bs_kernel<10, 14, 0, 4, 5>")  # api.cpp bs_shape
     # the committed PMC summary applies to the configuration it was taken on (full job, N = 1,
     # this parity alignment)
     traffic = None

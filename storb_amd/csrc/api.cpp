@@ -143,8 +143,6 @@ struct SubPlan {
     size_t off_msgs = 0;                   // messages of this unit (SHA-1, bignum)
     uint32_t nmsgs = 0;
     bool sha_split = false;  // SHA-1 messages: the two-wave kernel (sha1_split)
-    int flat_shape = -1;     // encode: the unit is one flat bit-sliced launch (FlatEnc) of this shape
-    sec::FlatEnc flat{};
     size_t off_segs = 0, off_seginfo = 0;  // bignum: segments of the messages, per-message (first, count)
     uint32_t nsegs = 0, max_seg = 0;       // segment count; most segments of one message
     uint64_t dig_first = 0;                // first digest slot of this unit
@@ -153,7 +151,7 @@ struct SubPlan {
     // groups (sec_decode_kernel over the syndrome rows) and their tail items
     std::vector<std::pair<int, std::pair<uint32_t, uint32_t>>> syn1;  // (shape, (first, count)) in syn tiles
     std::vector<Group> groups2;
-    size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_smrow = 0, off_tiles2 = 0, off_tail2 = 0;
+    size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_tiles2 = 0, off_tail2 = 0;
     uint32_t ntail2 = 0;
     uint64_t syn_bytes = 0;  // syndrome scratch of this unit
 };
@@ -271,28 +269,25 @@ int dec_copy_kb(int k)
     return (v == 4 || v == 8) && (size_t)k <= v ? (int)v : 0;
 }
 
-// Syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel) for a chunk that lost e data blocks,
-// when its shape has a bit-sliced kernel: the syndromes of its e present parity rows, then the
-// e x e solve, either in the same kernel (fused: every present parity row in one row group, the
-// syndromes never leave the registers) or by sec_decode_kernel over the syndrome rows stored to
-// a scratch buffer (two-phase).  Chosen by a time estimate per 4 byte positions, each kernel
-// taking the longer of its VALU issue time and its HBM time (kVperOp = VALU ops per HBM byte
-// at the measured rates: v_perm rows ~2.8e13 ops/s, mixed traffic ~6 TB/s):
+// Syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel, then sec_decode_kernel on the e
+// syndrome rows) for a chunk that lost e data blocks, when its shape has a bit-sliced kernel.
+// Chosen by a time estimate per 4 byte positions, each kernel taking the longer of its VALU
+// issue time and its HBM time (kVperOp = VALU ops per HBM byte at the measured rates: v_perm
+// rows ~2.8e13 ops/s, mixed traffic ~6 TB/s):
 //   direct:  ceil(e / 8) v_perm row groups (5 selector ops + 4.5 per row) over all k slots;
 //            reads k blocks per row group, writes the chunk (or the e rows);
 //   phase 1: the bit-sliced rows (6 transpose + 2.75 subsets + NR per row group holding a
 //            present parity row) over the k - e present data blocks, 6 per syndrome to transpose
 //            back; reads k blocks, writes the k - e copies (reassembly) and e syndromes;
-//   phase 2: v_perm rows over the e syndromes; reads them per row group, writes e rows;
-//   fused:   phase 1 + per pass of 4 output rows the selectors (5) of all NR rows of the group
-//            and 5 per product (absent rows have zero coefficients); reads k, writes the chunk.
-// The two-phase estimate was checked against the in-process A/B (tools/syn_ab.py,
+//   phase 2: v_perm rows over the e syndromes; reads them per row group, writes e rows.
+// Checked against the in-process A/B on the wide shapes (tools/syn_ab.py,
 // profiles/r03_syn_ab.jsonl): predicted syn / direct 0.70 / 0.95 / 1.16 / 1.40 / 1.25 against
 // measured 0.79 / 1.07 / 1.18 / 1.57 / 1.29 for zfec(64,96) 16 lost, (32,48) 16 and 8 lost,
-// (16,24) 8 and 4 lost.  A path is taken when its estimate is under SEC_SYN_RATIO (default
-// 0.85) of the direct one.  SEC_SYN=0 turns both off, SEC_SYN=1 forces the syndrome path
-// wherever it applies (fused when it can be), SEC_SYN_FUSED=0 never fuses; all read per plan
-// build.
+// (16,24) 8 and 4 lost; the path is taken when its estimate is under SEC_SYN_RATIO (default
+// 0.85) of the direct one.  SEC_SYN=0 / 1 turns it off / forces it wherever it applies; all
+// read per plan build.  (Two variants measured and dropped: the solve fused into the phase-1
+// kernel, which needs 256+ VGPRs and ran 0.6x the two-phase rate; phase 2 of a part of the
+// chunks overlapped with phase 1 of the rest on a second stream, -1 to -25 %.)
 double vperm_ops(int rows, int slots)
 {
     double v = 0;
@@ -301,43 +296,29 @@ double vperm_ops(int rows, int slots)
     return v * slots;
 }
 
-constexpr int kFusedRows = 4;  // output rows per pass of the fused solve (kernels_bs.hip fused_rows)
-
-struct SynPick {
-    int shape = -1;  // bit-sliced shape, or -1: the direct decode
-    bool fused = false;
-};
-
-SynPick syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies)
+int syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies)
 {
     const char *env = getenv("SEC_SYN");
     if (env && env[0] == '0')
-        return {};
+        return -1;
     const int sh = sec_syn_shape(c.k, c.m);
     if (sh < 0 || e < 1 || c.B < 16 || c.B > 0xFFFFFFFFull - 8192 || c.padlen >= c.B)
-        return {};
+        return -1;
+    if (env && env[0] == '1')
+        return sh;
+    constexpr double kVperOp = 1.0 / 4.63;
     const int k = c.k, NR = sec_bs_rows(sh), G = (e + sec::kMaxRows - 1) / sec::kMaxRows;
     uint64_t touched = 0;  // parity row groups that hold a present row
     for (int s = 0; s < k; ++s)
         if (idx[s] >= k)
             touched |= 1ull << ((idx[s] - k) / NR);
-    const int T = __builtin_popcountll(touched);
-    const char *fe = getenv("SEC_SYN_FUSED");
-    const bool can_fuse = T == 1 && !(fe && fe[0] == '0');
-    if (env && env[0] == '1')
-        return {sh, can_fuse};
-    constexpr double kVperOp = 1.0 / 4.63;
     auto t = [&](double ops, double bytes) { return std::max(ops * kVperOp, bytes); };
     const double direct = t(vperm_ops(e, k), 4.0 * (k * G + (copies ? k : e)));
-    const double v1 = T * (k - e) * (8.75 + NR) + 6.0 * e;
-    const double two = t(v1, 4.0 * (k + (copies ? k : e))) + t(vperm_ops(e, e), 4.0 * (e * G + e));
-    const int passes = (e + kFusedRows - 1) / kFusedRows;
-    const double fused = t(v1 + NR * passes * (5.0 + 5.0 * kFusedRows), 4.0 * (k + (copies ? k : e)));
+    const double p1 = t(__builtin_popcountll(touched) * (k - e) * (8.75 + NR) + 6.0 * e, 4.0 * (k + (copies ? k : e)));
+    const double p2 = t(vperm_ops(e, e), 4.0 * (e * G + e));
     const char *ratio = getenv("SEC_SYN_RATIO");
-    const double lim = (ratio && *ratio ? atof(ratio) : 0.85) * direct;
-    if (can_fuse && fused < lim && fused <= two)
-        return {sh, true};
-    return two < lim ? SynPick{sh, false} : SynPick{};
+    const double lim = ratio && *ratio ? atof(ratio) : 0.85;
+    return p1 + p2 < lim * direct ? sh : -1;
 }
 
 // Work for one chunk.  `valid` = positions where every block is fully readable and
@@ -792,52 +773,6 @@ int check_sharenums(int k, int m, const int32_t *s)
 uint64_t enc_B(const sec_enc_chunk &c) { return (c.n + (uint64_t)c.k - 1) / (uint64_t)c.k; }
 
 // ---- encode plan ------------------------------------------------------------
-// Flat bit-sliced encode (kernels_bs.hip sec_encode_bs_flat_kernel): a unit whose chunks all have
-// the same (k, m, n), a one-group bit-sliced shape and constant input / parity strides runs as
-// one launch whose waves span chunk boundaries, when whole 2048-position wave spans per chunk
-// would waste more than 3 % of the waves (C4: B = 6554 in 4 spans, 20 % fewer waves flat).
-// Host slabs are dense, so their uniform units qualify too.  SEC_BS_FLAT=0 turns it off (read
-// per plan build).  Fills sp.flat / sp.flat_shape; returns whether the unit is flat.
-bool flat_unit(const sec_enc_chunk *chunks, int64_t c0, int64_t c1, bool host, SubPlan &sp)
-{
-    sp.flat_shape = -1;
-    const char *e = getenv("SEC_BS_FLAT");
-    if ((e && e[0] == '0') || c1 <= c0)
-        return false;
-    const sec_enc_chunk &a = chunks[c0];
-    const uint64_t B = enc_B(a);
-    const int shape = a.m > a.k ? bs_shape(a.k, a.m, B) : -1;
-    if (shape < 0 || sec_bs_groups(shape) != 1)
-        return false;
-    const uint64_t span = sec_bs_span(), Bv = (B + 15) / 16 * 16;
-    if ((B + span - 1) / span * span - B <= B * 3 / 100)
-        return false;
-    const uint64_t n = (uint64_t)(c1 - c0);
-    if (n * Bv > 0xFFFFFFFFull)
-        return false;
-    const uint64_t p = (uint64_t)(a.m - a.k);
-    uint64_t in0 = 0, istr = a.n, par0 = 0, pstr = p * B, rstr = B;  // host slabs: dense
-    if (!host) {
-        in0 = a.in_off;
-        par0 = a.parity_off;
-        rstr = a.parity_stride;
-        istr = n > 1 ? chunks[c0 + 1].in_off - a.in_off : a.n;
-        pstr = n > 1 ? chunks[c0 + 1].parity_off - a.parity_off : p * rstr;
-    }
-    for (int64_t i = c0; i < c1; ++i) {
-        const sec_enc_chunk &c = chunks[i];
-        const uint64_t j = (uint64_t)(i - c0);
-        if (c.k != a.k || c.m != a.m || c.n != a.n)
-            return false;
-        if (!host && (c.in_off != in0 + j * istr || c.parity_off != par0 + j * pstr || c.parity_stride != rstr))
-            return false;
-    }
-    sp.flat_shape = shape;
-    sp.flat = sec::FlatEnc{in0, istr, par0, pstr, rstr, n * Bv, (uint32_t)B, (uint32_t)Bv,
-                           (uint32_t)(a.n - (uint64_t)(a.k - 1) * B), 0};
-    return true;
-}
-
 int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, bool host, bool digest)
 {
     Plan &plan = ctx->enc_plan;
@@ -908,7 +843,6 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
         Bins bins;
         std::vector<sec::TailItem> tail;
         std::vector<sec::MsgDesc> msgs;
-        const bool flat_ok = flat_unit(chunks, c0, c1, host, sp);
         for (int64_t i = c0; i < c1; ++i) {
             const sec_enc_chunk &c = chunks[i];
             const uint64_t B = enc_B(c);
@@ -938,8 +872,6 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
             const int bs = p > 0 ? bs_shape(c.k, c.m, B) : -1;
-            if (bs >= 0 && flat_ok)
-                continue;  // the whole unit is one flat launch (below)
             if (bs >= 0)
                 add_bs_work(bins, (uint32_t)(i - c0), B, bs);
             else if (p > 0)
@@ -970,12 +902,6 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::EncDesc *dd = plan.meta.as<sec::EncDesc>(sp.off_desc);
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
-    if (sp.flat_shape >= 0) {
-        const int lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
-        int e = sec_launch_encode_bs_flat(sp.flat_shape, 0, lanes, in, par, sp.flat, s);
-        if (e)
-            return hip_fail((hipError_t)e, "sec_encode_bs_flat_kernel");
-    }
     for (const Group &g : sp.groups) {
         int e = g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsAllGroups ? -1 : g.U, g.lanes, in, par, dd,
                                                    dt + g.first, g.count, s)
@@ -1048,7 +974,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
     TableCache &tc = ctx->dec_tabs;
     std::vector<PendingExpand> pending;
     std::vector<uint32_t> tab_of((size_t)nchunks, 0), e_of((size_t)nchunks, 0);
-    std::vector<SynPick> syn_of((size_t)nchunks);  // syndrome decodes (syn_choice)
+    std::vector<int> syn_of((size_t)nchunks, -1);  // syndrome-decode shape, or -1 (syn_choice)
     for (int attempt = 0;; ++attempt) {
         pending.clear();
         size_t need = 0;
@@ -1069,11 +995,9 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             bool whole = true;
             for (int s = 0; s < k && whole && !host; ++s)
                 whole = idx[s] == k - 1 || slot_avail(c, block_avail, L.perm[L.first[i] + s]) >= c.B;
-            const SynPick pick = syn_of[i] = whole ? syn_choice(c, idx, (int)miss.size(), !recover && !nocopy) : SynPick{};
-            const int sh = pick.shape;
-            // the syndrome path's table is A^-1 (e x e; fused: by parity row of the group, e padded),
-            // the direct path's the decode matrix rows
-            std::string key = (sh < 0 ? "" : pick.fused ? "F" : "S") + std::to_string(k) + "/" + std::to_string(c.m) + ":";
+            const int sh = syn_of[i] = whole ? syn_choice(c, idx, (int)miss.size(), !recover && !nocopy) : -1;
+            // the syndrome path's table is A^-1 (e x e), the direct path's the decode matrix rows
+            std::string key = (sh >= 0 ? "S" : "") + std::to_string(k) + "/" + std::to_string(c.m) + ":";
             for (int s = 0; s < k; ++s)
                 key += std::to_string(idx[s]) + ",";
             auto it = tc.index.find(key);
@@ -1098,21 +1022,10 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                         a[(size_t)q * e + r] = enc[(size_t)prow[q] * k + miss[r]];
                 if (!sec::gf_invert(a, e))
                     return SEC_ESINGULAR;
-                if (pick.fused) {
-                    // layout [parity row r of the group][lost o, padded to whole passes]: the
-                    // kernel runs every row of the group, absent ones with zero coefficients
-                    const int NR = sec_bs_rows(sh), ep = (e + kFusedRows - 1) / kFusedRows * kFusedRows;
-                    const int r0 = (prow[0] - k) / NR * NR;
-                    coef.assign((size_t)NR * ep, 0);
-                    for (int q = 0; q < e; ++q)
-                        for (int o = 0; o < e; ++o)
-                            coef[(size_t)(prow[q] - k - r0) * ep + o] = a[(size_t)o * e + q];
-                } else {
-                    coef.resize((size_t)e * e);
-                    for (int q = 0; q < e; ++q)  // layout [slot q][missing r]
-                        for (int r = 0; r < e; ++r)
-                            coef[(size_t)q * e + r] = a[(size_t)r * e + q];
-                }
+                coef.resize((size_t)e * e);
+                for (int q = 0; q < e; ++q)  // layout [slot q][missing r]
+                    for (int r = 0; r < e; ++r)
+                        coef[(size_t)q * e + r] = a[(size_t)r * e + q];
             } else {
                 std::vector<int> iv(idx, idx + k);
                 std::vector<uint8_t> minv;
@@ -1141,7 +1054,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
     plan.nsyn = plan.ndirect = 0;
     for (int64_t i = 0; i < nchunks; ++i)
         if (e_of[i])
-            ++(syn_of[i].shape >= 0 ? plan.nsyn : plan.ndirect);
+            ++(syn_of[i] >= 0 ? plan.nsyn : plan.ndirect);
     std::vector<std::pair<int64_t, int64_t>> ranges;
     if (host) {
         std::vector<uint64_t> ib((size_t)nchunks);
@@ -1166,7 +1079,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         // descriptors (appended to descs), tiles and tail items
         std::vector<sec::SynDesc> sdescs;
         std::vector<uint64_t> ssoff;
-        std::vector<uint32_t> ssavail, smrow;
+        std::vector<uint32_t> ssavail;
         std::map<int, std::vector<sec::Tile>> stiles;
         std::vector<sec::DecDesc> descs2;
         Bins bins2;
@@ -1208,8 +1121,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)c.B));
             sp.in_bytes += (uint64_t)c.k * c.B;
             sp.out_bytes += nout;
-            const int sh = syn_of[i].shape;
-            const bool fused = syn_of[i].fused;
+            const int sh = syn_of[i];
             if (sh >= 0 && nout > 0) {
                 // phase 1: every present block in place, syndromes to the scratch
                 const int k = c.k, p = c.m - c.k, e = (int)e_of[i], NR = sec_bs_rows(sh);
@@ -1218,7 +1130,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 sd.out_off = d.out_off;
                 sd.syn_off = sp.syn_bytes;
                 sd.B = (uint32_t)c.B;
-                sd.last = recover ? (uint32_t)c.B : (uint32_t)(nout - (uint64_t)(k - 1) * c.B);
+                sd.last = copies ? (uint32_t)(nout - (uint64_t)(k - 1) * c.B) : 0;
                 sd.slot0 = (uint32_t)ssoff.size();
                 ssoff.resize(ssoff.size() + (size_t)(k + p), 0);
                 ssavail.resize(ssavail.size() + (size_t)(k + p), 0);
@@ -1228,14 +1140,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                     ssoff[j] = soff[slot0 + s];
                     ssavail[j] = savail[slot0 + s];
                 }
-                if (fused) {  // the lost blocks straight to their output rows
-                    sd.tab = tab_of[i];
-                    sd.e = (uint32_t)e;
-                    sd.mrow0 = (uint32_t)smrow.size();
-                    smrow.insert(smrow.end(), mr.begin(), mr.begin() + e);
-                } else {
-                    sp.syn_bytes += (uint64_t)e * c.B;
-                }
+                sp.syn_bytes += (uint64_t)e * c.B;
                 std::vector<int> gs;  // touched row groups, ascending
                 for (int g = 0; g * NR < p; ++g)
                     if ((sd.pmask >> (g * NR)) & ((NR >= 64 ? ~0ull : (1ull << NR) - 1)))
@@ -1243,13 +1148,11 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 const uint32_t si = (uint32_t)sdescs.size();
                 sdescs.push_back(sd);
                 const uint64_t step = (uint64_t)sec_bs_span() * (syn_lanes / 64);
-                auto &st = stiles[sh * 2 + (fused ? 1 : 0)];
+                auto &st = stiles[sh];
                 for (uint64_t t0 = 0; t0 < c.B; t0 += 8 * step)  // runs of 8 positions per group: one XCD
                     for (int g : gs)
                         for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
                             st.push_back(sec::Tile{si, (uint32_t)t, (uint32_t)(g * NR), copies && g == gs[0] ? 1u : 0u});
-                if (fused)
-                    continue;
                 // phase 2: the e syndrome rows are the slots of a plain decode whose matrix is A^-1
                 sec::DecDesc d2 = d;
                 d2.k = (uint32_t)e;
@@ -1283,7 +1186,6 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         sp.off_stiles = img.put(stl.data(), stl.size() * sizeof(sec::Tile));
         sp.off_ssoff = img.put(ssoff.data(), ssoff.size() * 8);
         sp.off_ssavail = img.put(ssavail.data(), ssavail.size() * 4);
-        sp.off_smrow = img.put(smrow.data(), smrow.size() * 4);
         sp.off_tiles2 = img.put(tiles2.data(), tiles2.size() * sizeof(sec::Tile));
         sp.off_tail2 = img.put(tail2.data(), tail2.size() * sizeof(sec::TailItem));
         sp.ntail = (uint32_t)tail.size();
@@ -1324,20 +1226,18 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     }
     if (sp.syn1.empty())
         return SEC_OK;
-    if (!syn && sp.syn_bytes)
+    if (!syn)
         return SEC_EINVAL;
     // syndrome decodes: phase 1 (syndromes + present primaries' copies), then phase 2 on the
     // syndrome rows (blocks = the scratch), in stream order
     const sec::SynDesc *sd = plan.meta.as<sec::SynDesc>(sp.off_sdesc);
     const sec::Tile *st = plan.meta.as<sec::Tile>(sp.off_stiles);
-    const sec::SynSlots ss{plan.meta.as<uint64_t>(sp.off_ssoff), plan.meta.as<uint32_t>(sp.off_ssavail),
-                           plan.meta.as<uint32_t>(sp.off_smrow), tabs};
+    const sec::SynSlots ss{plan.meta.as<uint64_t>(sp.off_ssoff), plan.meta.as<uint32_t>(sp.off_ssavail)};
     const int lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
     const sec::Tile *dt2 = plan.meta.as<sec::Tile>(sp.off_tiles2);
     auto phase1 = [&](size_t i, uint32_t first, uint32_t count) {
         const auto &g = sp.syn1[i];
-        int e = sec_launch_syndrome_bs(g.first / 2, g.first % 2, lanes, blocks, out, syn, sd, st + g.second.first + first,
-                                       count, ss, s);
+        int e = sec_launch_syndrome_bs(g.first, lanes, blocks, out, syn, sd, st + g.second.first + first, count, ss, s);
         return e ? hip_fail((hipError_t)e, "sec_syndrome_bs_kernel") : SEC_OK;
     };
     auto phase2 = [&](size_t i, uint32_t first, uint32_t count, hipStream_t q) {

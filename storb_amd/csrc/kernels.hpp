@@ -66,40 +66,23 @@ struct DecSlots {
     const uint32_t *avail;  // bytes of the block that exist in memory; the rest read as zero
 };
 
-// A batch of equal chunks at constant strides, for the flat bit-sliced encode
-// (sec_encode_bs_flat_kernel): chunk c's block j at in + in0 + c * in_stride + j * B, its
-// parity row r at par + par0 + c * par_cstride + r * par_rstride.
-struct FlatEnc {
-    uint64_t in0, in_stride;
-    uint64_t par0, par_cstride, par_rstride;
-    uint64_t total;   // nchunks * Bv positions (< 2^32)
-    uint32_t B, Bv;   // block bytes; B rounded up to 16
-    uint32_t valid;   // readable bytes of block k-1 (n - (k-1) * B)
-    uint32_t pad;
-};
-
-// One chunk of a syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel; 64 B).  Block j of
+// One chunk of a syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel; 48 B).  Block j of
 // the chunk (data j < k, parity row r at j = k + r) is at blocks + off[slot0 + j] with
 // avail[slot0 + j] readable bytes, when its bit in dmask / pmask is set.
 struct SynDesc {
     uint64_t out_off;  // reassembled chunk in `out`: present primaries are copied there (tile flag)
-    uint64_t syn_off;  // two-phase: syndrome q (of the q-th present parity row) at syn + syn_off + q * B
+    uint64_t syn_off;  // syndrome q (of the q-th present parity row) at syn + syn_off + q * B
     uint64_t dmask;    // bit j: data block j present (k <= 64)
     uint64_t pmask;    // bit r: parity row r present (m - k <= 64)
     uint32_t B;
     uint32_t last;     // bytes of output row k-1 (n - (k-1)*B): its stores stop there
     uint32_t slot0;
-    uint32_t tab;      // fused: dword offset of A^-1's tables, layout [syndrome q][lost o][5]
-    uint32_t e;        // fused: lost data blocks (rows solved in the same kernel)
-    uint32_t mrow0;    // fused: lost block o goes to output row mrow[mrow0 + o]
-    uint32_t pad[2];
+    uint32_t pad;
 };
 
 struct SynSlots {
     const uint64_t *off;
     const uint32_t *avail;
-    const uint32_t *mrow;
-    const uint32_t *tabs;  // the decode coefficient tables (5 dwords per coefficient)
 };
 
 struct Tile {
@@ -153,15 +136,11 @@ int sec_bs_rows(int shape);
 uint32_t sec_bs_span();
 int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
                          const sec::Tile *t, uint32_t ntiles, void *stream);
-// The flat bit-sliced encode of a batch of equal chunks (FlatEnc), row group `group`
-int sec_launch_encode_bs_flat(int shape, int group, int lanes, const uint8_t *in, uint8_t *par, const sec::FlatEnc &f,
-                              void *stream);
 // Syndrome decode, phase 1, for the shapes sec_syn_shape knows (else -1): tiles as the bit-sliced
 // encode's (r0 = the row group's first parity row; ntail bit 0 = this tile also copies the
 // present primaries to `out`)
 int sec_syn_shape(int k, int m);
-// fused: the e x e solve in the same kernel (every present parity row in one row group)
-int sec_launch_syndrome_bs(int shape, int fused, int lanes, const uint8_t *blocks, uint8_t *out, uint8_t *syn,
+int sec_launch_syndrome_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, uint8_t *syn,
                            const sec::SynDesc *descs, const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl,
                            void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,

@@ -308,113 +308,6 @@ __global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs2_kernel(c
         bs_span<K, M, NR, NR, D, false>(in, par, d, s);
 }
 
-// ---- flat layout: a batch of equal chunks at constant strides -------------------------------
-// The per-chunk tiles above give every chunk whole wave spans of 2048 positions, so C4's
-// 6554-byte blocks take 4 waves per chunk, the last covering 410 positions.  Here the waves run
-// over the concatenation of the chunks' blocks (each B rounded up to 16): a lane's two 16-byte
-// pieces may lie in different chunks, which is fine since bit slicing is position-wise and every
-// chunk of the batch has the same matrix.  C4 then needs 20 % fewer waves.  A piece past a
-// chunk's B moves back to end at B, as in bs_span; block K-1's bytes past `valid` read as zero.
-struct FlatLane {
-    const u8 *a, *b;  // block 0 of the lane's two pieces (chunk base + position)
-    u64 oa, ob;       // the pieces' parity offsets (parity base + chunk's first row + position)
-    u32 pa, pb;       // positions in their chunks
-};
-
-__device__ __forceinline__ void flat_piece(const sec::FlatEnc &f, const u8 *in, u64 v, const u8 *&src, u64 &poff,
-                                           u32 &pos)
-{
-    if (v + 16 > f.total)
-        v = f.total - 16;
-    const u32 c = (u32)v / f.Bv;
-    const u32 p = min((u32)v - c * f.Bv, f.B - 16);
-    src = in + f.in0 + (u64)c * f.in_stride + p;
-    poff = f.par0 + (u64)c * f.par_cstride + p;
-    pos = p;
-}
-
-template <bool LAST>
-__device__ __forceinline__ void load_flat(u32 (&x)[8], const FlatLane &l, u64 jB, u32 valid)
-{
-    u32x4 a, b;
-    if (!LAST || l.pa + 16 <= valid)
-        a = ld16<true>(l.a + jB);
-    else
-        a = ld16_avail<true>(l.a + jB - l.pa, l.pa, valid);
-    if (!LAST || l.pb + 16 <= valid)
-        b = ld16<true>(l.b + jB);
-    else
-        b = ld16_avail<true>(l.b + jB - l.pb, l.pb, valid);
-    x[0] = a.x;
-    x[1] = a.y;
-    x[2] = a.z;
-    x[3] = a.w;
-    x[4] = b.x;
-    x[5] = b.y;
-    x[6] = b.z;
-    x[7] = b.w;
-}
-
-template <int K, int M, int R0, int NR, int D, int J>
-__device__ __forceinline__ void flat_block(u32 (&acc)[NR * 8], u32 (&ring)[D][8], const FlatLane &l, u64 B, u32 valid)
-{
-    u32 x[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-        x[i] = ring[J % D][i];
-    if constexpr (J + D < K)
-        load_flat<J + D == K - 1>(ring[J % D], l, (u64)(J + D) * B, valid);
-    transpose8(x);
-    u32 lo[16], hi[16];
-    subsets(x[0], x[1], x[2], x[3], lo);
-    subsets(x[4], x[5], x[6], x[7], hi);
-    block_rows<K, M, R0, J, J == 0>(std::make_integer_sequence<int, NR * 8>{}, acc, lo, hi);
-}
-
-template <int K, int M, int R0, int NR, int D, int... Js>
-__device__ __forceinline__ void flat_blocks(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], u32 (&ring)[D][8],
-                                            const FlatLane &l, u64 B, u32 valid)
-{
-    (flat_block<K, M, R0, NR, D, Js>(acc, ring, l, B, valid), ...);
-}
-
-template <int K, int M, int R0, int NR, int D, int... Js>
-__device__ __forceinline__ void flat_first(std::integer_sequence<int, Js...>, u32 (&ring)[D][8], const FlatLane &l,
-                                           u64 B, u32 valid)
-{
-    (load_flat<Js == K - 1>(ring[Js], l, (u64)Js * B, valid), ...);
-}
-
-template <int K, int M, int R0, int NR, int D>
-__global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs_flat_kernel(const u8 *__restrict__ in,
-                                                                                 u8 *__restrict__ par,
-                                                                                 const sec::FlatEnc f)
-{
-    const u64 s = ((u64)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * kSpan;
-    if (s >= f.total)
-        return;
-    const u32 lane = (threadIdx.x & 63) * 16;
-    FlatLane l;
-    flat_piece(f, in, s + lane, l.a, l.oa, l.pa);
-    flat_piece(f, in, s + 1024 + lane, l.b, l.ob, l.pb);
-    const u64 B = f.B;
-    u32 ring[D][8];
-    flat_first<K, M, R0, NR, D>(std::make_integer_sequence<int, D>{}, ring, l, B, f.valid);
-    u32 acc[NR * 8];
-    flat_blocks<K, M, R0, NR, D>(std::make_integer_sequence<int, K>{}, acc, ring, l, B, f.valid);
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        u32 y[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            y[i] = acc[r * 8 + i];
-        transpose8(y);
-        const u64 ro = (u64)(R0 + r) * f.par_rstride;
-        st16(par + l.oa + ro, y[0], y[1], y[2], y[3]);
-        st16(par + l.ob + ro, y[4], y[5], y[6], y[7]);
-    }
-}
-
 // ---- decode, phase 1: syndromes of the present parity rows (wide decodes) -------------------
 // A decode that lost e data blocks and holds e parity rows S instead: for a parity row r in S,
 //     s_r = p_r ^ XOR_{present j} c[r][j] * d_j  =  XOR_{lost j} c[r][j] * d_j,
@@ -498,11 +391,11 @@ __device__ __forceinline__ void load_syn_first(std::integer_sequence<int, Js...>
     ((item_present<K, NR, R0>(c, Js) ? load_syn_item<K, NR, R0, Js>(ring[Js], c) : void()), ...);
 }
 
-template <int K, int M, int R0, int NR, int D, bool FUSED, int J>
+template <int K, int M, int R0, int NR, int D, int J>
 __device__ __forceinline__ void syn_item(u32 (&acc)[NR * 8], u32 (&ring)[D][8], const SynCtx &c, u8 *orow0, u32 B,
                                          u32 last, bool copies, u8 *syn, u32 &q)
 {
-    constexpr int NI = FUSED ? K : K + NR;  // fused: the parity rows are read after the blocks
+    constexpr int NI = K + NR;
     const bool here = item_present<K, NR, R0>(c, J);
     u32 x[8];
 #pragma unroll
@@ -543,80 +436,14 @@ __device__ __forceinline__ void syn_item(u32 (&acc)[NR * 8], u32 (&ring)[D][8], 
     }
 }
 
-template <int K, int M, int R0, int NR, int D, bool FUSED, int... Js>
+template <int K, int M, int R0, int NR, int D, int... Js>
 __device__ __forceinline__ void syn_items(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], u32 (&ring)[D][8],
                                           const SynCtx &c, u8 *orow0, u32 B, u32 last, bool copies, u8 *syn, u32 &q)
 {
-    (syn_item<K, M, R0, NR, D, FUSED, Js>(acc, ring, c, orow0, B, last, copies, syn, q), ...);
+    (syn_item<K, M, R0, NR, D, Js>(acc, ring, c, orow0, B, last, copies, syn, q), ...);
 }
 
-// Fused solve, step 1: present parity row R0 + r's syndrome, in place of its accumulator, in the
-// byte domain: its planes transposed back, XOR its bytes.  (An absent row's accumulator is left
-// as it is: its coefficients in the solve are zero.)
-template <int K, int NR, int R0, int r>
-__device__ __forceinline__ void syn_in_place(u32 (&acc)[NR * 8], const SynCtx &c)
-{
-    if (!item_present<K, NR, R0>(c, K + r))
-        return;
-    u32 p[8], y[8];
-    load_syn_item<K, NR, R0, K + r>(p, c);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-        y[i] = acc[r * 8 + i];
-    transpose8(y);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-        acc[r * 8 + i] = y[i] ^ p[i];
-}
-
-template <int K, int NR, int R0, int... Rs>
-__device__ __forceinline__ void syn_all_in_place(std::integer_sequence<int, Rs...>, u32 (&acc)[NR * 8], const SynCtx &c)
-{
-    (syn_in_place<K, NR, R0, Rs>(acc, c), ...);
-}
-
-__device__ __forceinline__ u32 perm(u32 hi, u32 lo, u32 sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
-
-// Fused solve, step 2: out[o] ^= coef[r][o0 + o] * s_r for every row r of the group (RO output
-// rows per pass): the v_perm product of kernels.hip (3-bit tables, 5 dwords per coefficient:
-// 3 v_perm + 2 VALU per dword), the syndrome's selectors shared by the RO rows.  The plan's
-// table holds A^-1[o][q] at [r][o] for the q-th present row r and zeros for absent rows, so
-// there is no run-time branch here.
-template <int RO>
-__device__ __forceinline__ void solve_one(u32 (&out)[RO][8], const u32 *v, const u32 *__restrict__ t)
-{
-    // one syndrome at a time: left free, the scheduler hoisted every syndrome's selectors and
-    // products of the pass (all 256 VGPRs and more)
-    __builtin_amdgcn_sched_barrier(0);
-    u32 s0[8], s1[8], s2[8];
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-        s0[w] = v[w] & 0x07070707u;
-        s1[w] = (v[w] >> 3) & 0x07070707u;
-        s2[w] = (v[w] >> 6) & 0x03030303u;
-    }
-#pragma unroll
-    for (int o = 0; o < RO; ++o) {
-        const u32 *cf = t + o * 5;
-        const u32 c0 = cf[0], c1 = cf[1], c2 = cf[2], c3 = cf[3], c4 = cf[4];
-#pragma unroll
-        for (int w = 0; w < 8; ++w)
-            out[o][w] = xor3(out[o][w], perm(c1, c0, s0[w]), perm(c3, c2, s1[w])) ^ perm(c4, c4, s2[w]);
-    }
-}
-
-template <int NR, int RO, int... Rs>
-__device__ __forceinline__ void syn_solve(std::integer_sequence<int, Rs...>, u32 (&out)[RO][8], const u32 (&acc)[NR * 8],
-                                          const u32 *__restrict__ tq, u32 estride, u32 o0)
-{
-    (solve_one<RO>(out, acc + Rs * 8, tq + (Rs * estride + o0) * 5u), ...);
-}
-
-// output rows per pass of the fused solve: 8, or 4 for 16-row groups (registers)
-template <int NR>
-constexpr int fused_rows() { return 4; }
-
-template <int K, int M, int R0, int NR, int D, bool FUSED>
+template <int K, int M, int R0, int NR, int D>
 __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__restrict__ out, u8 *__restrict__ syn,
                                          const sec::SynDesc &d, const sec::SynSlots &sl, u32 s, bool copies)
 {
@@ -631,42 +458,12 @@ __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__re
         acc[i] = 0;
     // syndrome row of this group's first present parity row: the present rows below R0
     u32 q = (u32)__builtin_popcountll(d.pmask & ((1ull << R0) - 1ull));
-    syn_items<K, M, R0, NR, D, FUSED>(std::make_integer_sequence<int, FUSED ? K : K + NR>{}, acc, ring, c,
-                                      out + d.out_off, B, d.last, copies, syn + d.syn_off, q);
-    if constexpr (FUSED) {
-        // the e lost blocks = A^-1 times the e syndromes, RO output rows per pass
-        constexpr int RO = fused_rows<NR>();
-        syn_all_in_place<K, NR, R0>(std::make_integer_sequence<int, NR>{}, acc, c);
-        const u32 *tq = sl.tabs + d.tab;
-        const u32 estride = (d.e + RO - 1) / RO * RO;  // table row length (e padded with zeros)
-        u8 *dst = out + d.out_off;
-#pragma unroll 1
-        for (u32 o0 = 0; o0 < d.e; o0 += RO) {
-            u32 res[RO][8];
-#pragma unroll
-            for (int o = 0; o < RO; ++o)
-#pragma unroll
-                for (int w = 0; w < 8; ++w)
-                    res[o][w] = 0;
-            syn_solve<NR, RO>(std::make_integer_sequence<int, NR>{}, res, acc, tq, estride, o0);
-#pragma unroll
-            for (int o = 0; o < RO; ++o) {
-                if (o0 + o >= d.e)
-                    break;
-                const u32 row = sl.mrow[d.mrow0 + o0 + o];
-                u8 *orow = dst + (u64)row * B;
-                const u32 lim = row == K - 1 ? d.last : B;  // the chunk's last row stops at `last`
-                st16_clamped(orow, c.pa, lim, res[o][0], res[o][1], res[o][2], res[o][3]);
-                st16_clamped(orow, c.pb, lim, res[o][4], res[o][5], res[o][6], res[o][7]);
-            }
-        }
-    }
+    syn_items<K, M, R0, NR, D>(std::make_integer_sequence<int, K + NR>{}, acc, ring, c, out + d.out_off, B, d.last,
+                               copies, syn + d.syn_off, q);
 }
 
-// FUSED: the e x e solve in the same kernel (every present parity row of the chunk lies in the
-// tile's row group): the syndromes stay in registers and the lost blocks are stored directly.
-// Otherwise the syndromes go to `syn` and sec_decode_kernel solves (api.cpp).
-template <int K, int M, int NR, int D, bool FUSED>
+// The syndromes go to `syn`; sec_decode_kernel then solves for the lost blocks (api.cpp).
+template <int K, int M, int NR, int D>
 __global__ __launch_bounds__(256) void sec_syndrome_bs_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                               u8 *__restrict__ syn,
                                                               const sec::SynDesc *__restrict__ descs,
@@ -680,13 +477,13 @@ __global__ __launch_bounds__(256) void sec_syndrome_bs_kernel(const u8 *__restri
         return;
     const bool copies = tl.ntail & 1;  // the chunk's first touched row group copies the primaries
     if constexpr (M - K <= NR) {
-        syn_span<K, M, 0, NR, D, FUSED>(blocks, out, syn, d, sl, s, copies);
+        syn_span<K, M, 0, NR, D>(blocks, out, syn, d, sl, s, copies);
     } else {
         static_assert(M - K == 2 * NR, "two row groups");
         if (tl.r0 == 0)
-            syn_span<K, M, 0, NR, D, FUSED>(blocks, out, syn, d, sl, s, copies);
+            syn_span<K, M, 0, NR, D>(blocks, out, syn, d, sl, s, copies);
         else
-            syn_span<K, M, NR, NR, D, FUSED>(blocks, out, syn, d, sl, s, copies);
+            syn_span<K, M, NR, NR, D>(blocks, out, syn, d, sl, s, copies);
     }
 }
 
@@ -764,17 +561,13 @@ int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uin
 
 namespace {
 template <int K, int M, int NR, int D>
-hipError_t launch_syn(int fused, int lanes, const u8 *blocks, u8 *out, u8 *syn, const sec::SynDesc *d,
-                      const sec::Tile *t, u32 nt, sec::SynSlots sl, hipStream_t s)
+hipError_t launch_syn(int lanes, const u8 *blocks, u8 *out, u8 *syn, const sec::SynDesc *d, const sec::Tile *t, u32 nt,
+                      sec::SynSlots sl, hipStream_t s)
 {
     void *a = nullptr, *b = nullptr;
     sec_next_launch_events(&a, &b);
-    if (fused)
-        hipExtLaunchKernelGGL((sec_syndrome_bs_kernel<K, M, NR, D, true>), dim3(nt), dim3(lanes), 0, s, (hipEvent_t)a,
-                              (hipEvent_t)b, 0, blocks, out, syn, d, t, sl);
-    else
-        hipExtLaunchKernelGGL((sec_syndrome_bs_kernel<K, M, NR, D, false>), dim3(nt), dim3(lanes), 0, s,
-                              (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, syn, d, t, sl);
+    hipExtLaunchKernelGGL((sec_syndrome_bs_kernel<K, M, NR, D>), dim3(nt), dim3(lanes), 0, s, (hipEvent_t)a,
+                          (hipEvent_t)b, 0, blocks, out, syn, d, t, sl);
     return hipGetLastError();
 }
 }  // namespace
@@ -785,7 +578,7 @@ int sec_syn_shape(int k, int m)
     return sh == 6 ? -1 : sh;  // (32,48) in 8-row groups is an encode A/B only
 }
 
-int sec_launch_syndrome_bs(int shape, int fused, int lanes, const uint8_t *blocks, uint8_t *out, uint8_t *syn,
+int sec_launch_syndrome_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, uint8_t *syn,
                            const sec::SynDesc *descs, const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl,
                            void *stream)
 {
@@ -795,46 +588,13 @@ int sec_launch_syndrome_bs(int shape, int fused, int lanes, const uint8_t *block
         return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
     switch (shape) {  // ring depths as the encode's (kernels' register budgets are alike)
-    case 0: return launch_syn<10, 14, 4, RING_K(10, 5)>(fused, lanes, blocks, out, syn, descs, t, ntiles, sl, s);
-    case 1: return launch_syn<8, 12, 4, RING_K(8, 4)>(fused, lanes, blocks, out, syn, descs, t, ntiles, sl, s);
-    case 2: return launch_syn<16, 24, 8, RING_K(16, 10)>(fused, lanes, blocks, out, syn, descs, t, ntiles, sl, s);
-    case 3: return launch_syn<32, 48, 16, RING_K(32, 2)>(fused, lanes, blocks, out, syn, descs, t, ntiles, sl, s);
-    case 4: return launch_syn<64, 96, 16, RING_K(64, 2)>(fused, lanes, blocks, out, syn, descs, t, ntiles, sl, s);
-    case 5: return launch_syn<8, 11, 3, RING_K(8, 4)>(fused, lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 0: return launch_syn<10, 14, 4, RING_K(10, 5)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 1: return launch_syn<8, 12, 4, RING_K(8, 4)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 2: return launch_syn<16, 24, 8, RING_K(16, 10)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 3: return launch_syn<32, 48, 16, RING_K(32, 2)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 4: return launch_syn<64, 96, 16, RING_K(64, 2)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 5: return launch_syn<8, 11, 3, RING_K(8, 4)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
     default: return hipErrorInvalidValue;
     }
 }
 
-namespace {
-template <int K, int M, int R0, int NR, int D>
-hipError_t launch_flat(int lanes, const u8 *in, u8 *par, const sec::FlatEnc &f, hipStream_t s)
-{
-    void *a = nullptr, *b = nullptr;
-    sec_next_launch_events(&a, &b);
-    const u64 waves = (f.total + kSpan - 1) / kSpan, per = (u64)lanes / 64;
-    hipExtLaunchKernelGGL((sec_encode_bs_flat_kernel<K, M, R0, NR, D>), dim3((u32)((waves + per - 1) / per)),
-                          dim3(lanes), 0, s, (hipEvent_t)a, (hipEvent_t)b, 0, in, par, f);
-    return hipGetLastError();
-}
-}  // namespace
-
-int sec_launch_encode_bs_flat(int shape, int group, int lanes, const uint8_t *in, uint8_t *par, const sec::FlatEnc &f,
-                              void *stream)
-{
-    if (f.total == 0)
-        return hipSuccess;
-    if (lanes < 64 || lanes > 256 || lanes % 64 || f.B < 16 || f.total > 0xFFFFFFFFull || f.Bv % 16 ||
-        f.Bv < f.B)
-        return hipErrorInvalidValue;
-    hipStream_t s = (hipStream_t)stream;
-    switch (shape * 4 + group) {
-    case 0: return launch_flat<10, 14, 0, 4, RING_K(10, 5)>(lanes, in, par, f, s);
-    case 4: return launch_flat<8, 12, 0, 4, RING_K(8, 4)>(lanes, in, par, f, s);
-    case 8: return launch_flat<16, 24, 0, 8, RING_K(16, 10)>(lanes, in, par, f, s);
-    case 12: return launch_flat<32, 48, 0, 16, RING_K(32, 2)>(lanes, in, par, f, s);
-    case 16: return launch_flat<64, 96, 0, 16, RING_K(64, 2)>(lanes, in, par, f, s);
-    case 17: return launch_flat<64, 96, 16, 16, RING_K(64, 2)>(lanes, in, par, f, s);
-    case 20: return launch_flat<8, 11, 0, 3, RING_K(8, 4)>(lanes, in, par, f, s);
-    default: return hipErrorInvalidValue;
-    }
-}

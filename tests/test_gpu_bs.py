@@ -112,50 +112,3 @@ def test_encode_bit_sliced_device_padded_stride(k, m, monkeypatch):
     assert (ph[:, :, B:] == 0xA5).all()  # the gaps between parity blocks are untouched
     engine.close()
 
-
-FLAT_SHAPES = [(10, 14), (8, 11), (8, 12), (16, 24), (32, 48)]  # one row group each
-
-
-@pytest.mark.parametrize("k,m", FLAT_SHAPES)
-@pytest.mark.parametrize("flat", ["1", "0"])
-def test_encode_flat_uniform_batches(k, m, flat, monkeypatch):
-    """Uniform batches (same n, constant strides) run as one flat launch whose waves cross
-    chunk boundaries (kernels_bs.hip sec_encode_bs_flat_kernel); SEC_BS_FLAT=0 is the per-chunk
-    tiling.  Device chunks at a stride larger than n with a padded parity stride (gaps untouched)
-    and host (staged, dense) calls; B from 16 to several spans, ragged and padded; one chunk."""
-    from storb_amd.engine import Engine
-
-    monkeypatch.setenv("SEC_BS", "1")
-    monkeypatch.setenv("SEC_BS_FLAT", flat)
-    eng = Engine(0)
-    rng = random.Random(k * 31 + m + int(flat))
-    try:
-        for n, nch in [(16 * k, 7), (17 * k - 1, 5), (6554 * k - 4 if k == 10 else 6554 * k - 3, 300),
-                       (100 * k + 3, 64), (3000 * k + 1, 1), (2048 * k - 5, 33)]:
-            if -(-n // k) * (k - 1) >= n:
-                continue
-            B = -(-n // k)
-            istr, ps = n + 37, B + 16
-            g = torch.Generator(device="cuda")
-            g.manual_seed(n + nch)
-            src = torch.randint(0, 256, (nch * istr,), dtype=torch.uint8, device="cuda", generator=g)
-            d = np.zeros(nch, dtype=ENC_DTYPE)
-            d["in_off"] = np.arange(nch, dtype=np.uint64) * istr
-            d["n"] = n
-            d["parity_off"] = np.arange(nch, dtype=np.uint64) * (m - k) * ps
-            d["parity_stride"] = ps
-            d["k"], d["m"] = k, m
-            par = torch.full((nch * (m - k) * ps,), 0x5A, dtype=torch.uint8, device="cuda")
-            eng.encode_batch(d, src, par)
-            sh = src.cpu().numpy()
-            ph = par.cpu().numpy().reshape(nch, m - k, ps)
-            for ci in sorted({0, nch // 2, nch - 1}):
-                want = oracle_parity(sh[ci * istr:ci * istr + n].tobytes(), k, m)
-                for r in range(m - k):
-                    assert ph[ci, r, :B].tobytes() == want[r], (k, m, n, ci, r, flat)
-            assert (ph[:, :, B:] == 0x5A).all()
-            chunks = [rng.randbytes(n) for _ in range(min(nch, 40))]
-            for c, p in zip(chunks, eng.encode_host(chunks, [(k, m)] * len(chunks))):
-                assert p == oracle_parity(c, k, m), (k, m, n, "host", flat)
-    finally:
-        eng.close()

@@ -33,10 +33,10 @@ from storb_amd._lib import DEC_DTYPE, ENC_DTYPE  # noqa: E402
 SHAPES = [(16, 24), (32, 48), (64, 96), (10, 14), (8, 12), (8, 11)]
 
 
-def _engine(monkeypatch, syn, fused=None):
+def _engine(monkeypatch, syn):
     from storb_amd.engine import Engine
 
-    for var, val in (("SEC_SYN", syn), ("SEC_SYN_FUSED", fused)):
+    for var, val in (("SEC_SYN", syn),):
         if val is None:
             monkeypatch.delenv(var, raising=False)
         else:
@@ -52,7 +52,7 @@ def _cases(rng, k, m, sizes):
     for n in sizes:
         for e in sorted({1, min(2, p), p // 2 or 1, p, rng.randint(1, p)}):
             lost = sorted(rng.sample(range(k), e))
-            if p > 16 and e <= 16 and rng.random() < 0.5:  # (64,96): rows of one 16-row group (fusable)
+            if p > 16 and e <= 16 and rng.random() < 0.5:  # (64,96): rows of one 16-row group
                 g = rng.randrange(p // 16)
                 par = sorted(rng.sample(range(k + 16 * g, k + 16 * g + 16), e))
             else:
@@ -142,15 +142,13 @@ def _run(eng, k, m, cases, recover=False, host=None, check_oracle=3):
 
 @pytest.mark.parametrize("k,m", SHAPES)
 @pytest.mark.parametrize("recover", [False, True])
-@pytest.mark.parametrize("fused", ["1", "0"])
-def test_syndrome_decode_forced_device(k, m, recover, fused, monkeypatch):
-    """SEC_SYN=1: every chunk on the syndrome path, fused (solve in the same kernel) wherever its
-    parity rows lie in one row group, or (SEC_SYN_FUSED=0) always two-phase."""
+def test_syndrome_decode_forced_device(k, m, recover, monkeypatch):
+    """SEC_SYN=1: every chunk on the syndrome path."""
     rng = random.Random(k * 1000 + m + recover)
     sizes = [16 * k, 17 * k - 3, 2048 * k + 5 * k, 6554 * k - 4 if k == 10 else 4099 * k - 1, 65536 * k,
              rng.randrange(20000, 300000)]
     sizes = [n for n in sizes if -(-n // k) * (k - 1) < n]  # easyfec: the last block not empty
-    eng = _engine(monkeypatch, "1", fused)
+    eng = _engine(monkeypatch, "1")
     try:
         cases = _cases(rng, k, m, sizes)
         _run(eng, k, m, cases, recover=recover)
@@ -162,10 +160,9 @@ def test_syndrome_decode_forced_device(k, m, recover, fused, monkeypatch):
 
 @pytest.mark.parametrize("k,m", [(32, 48), (64, 96), (16, 24)])
 @pytest.mark.parametrize("host", ["staged", "pinned"])
-@pytest.mark.parametrize("fused", ["1", "0"])
-def test_syndrome_decode_forced_host(k, m, host, fused, monkeypatch):
+def test_syndrome_decode_forced_host(k, m, host, monkeypatch):
     rng = random.Random(7 * k + (host == "pinned"))
-    eng = _engine(monkeypatch, "1", fused)
+    eng = _engine(monkeypatch, "1")
     try:
         cases = _cases(rng, k, m, [4096 * k + 17, 1 << 20, 3 * k * 1024 - 5])
         _run(eng, k, m, cases, host=host)

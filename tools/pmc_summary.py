@@ -1,11 +1,17 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py into per-launch HBM bytes.
 
-    python tools/pmc_summary.py gpurun_out > profiles/pmc_encode_c2.json
+    python tools/pmc_summary.py gpurun_out [c2|c4] > profiles/pmc_encode_c2.json (or r03_pmc_c4.json)
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of a wide
 coalesced streaming read, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for
 16 B/lane streaming stores (x 1024).  Both counters are in KiB per dispatch.
+
+Workloads (the bench line each summary belongs to; bench.py load_traffic reads it):
+  c2  python3 bench.py: encode (sec_encode_kernel) and decode (sec_decode_kernel) launches over
+      1024 x 1 MiB RS(4,2) chunks
+  c4  python3 bench.py --workload c4: the encode launches (sec_encode_bs*_kernel) over the
+      whole 65536 x 64 KiB RS(10,4) job at N = 1, and the decode launches after the timed region
 """
 
 from __future__ import annotations
@@ -17,11 +23,17 @@ import os
 import sys
 from collections import defaultdict
 
-ENC_ALG = 1024 * ((1 << 20) + 2 * (1 << 18))  # bytes per encode launch (bench workload c2)
-DEC_ALG = 1024 * (4 * (1 << 18) + (1 << 20))  # bytes per decode launch (reassemble)
+WORKLOADS = {
+    "c2": {"encode": ("sec_encode_kernel", 1024 * ((1 << 20) + 2 * (1 << 18))),
+           "decode": ("sec_decode_kernel", 1024 * (4 * (1 << 18) + (1 << 20))),
+           "cmd": "python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e"},
+    "c4": {"encode": ("sec_encode_bs", 65536 * (65536 + 4 * 6554)),
+           "decode": ("sec_decode_kernel", 65536 * (10 * 6554 + 65536)),
+           "cmd": "python3 bench.py --workload c4 --steps 10 --warmup 2 --no-cpu"},
+}
 
 
-def counters(d: str, name: str) -> dict:
+def counters(d: str, name: str, kinds: dict) -> dict:
     vals = defaultdict(list)
     for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         with open(path) as f:
@@ -29,7 +41,7 @@ def counters(d: str, name: str) -> dict:
                 if row.get("Counter_Name") != name:
                     continue
                 k = row.get("Kernel_Name", "")
-                kind = "encode" if "sec_encode_kernel" in k else "decode" if "sec_decode_kernel" in k else None
+                kind = next((kd for kd, (pat, _) in kinds.items() if pat in k), None)
                 if kind:
                     vals[(kind, row.get("Dispatch_Id"))].append(float(row["Counter_Value"]))
     per = defaultdict(list)
@@ -40,16 +52,18 @@ def counters(d: str, name: str) -> dict:
 
 def main():
     d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-    fetch = counters(os.path.join(d, "pmc_fetch"), "FETCH_SIZE")
-    write = counters(os.path.join(d, "pmc_write"), "WRITE_SIZE")
-    out = {"workload": "c2", "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on "
-                                      "python3 bench.py --steps 10 --warmup 2",
+    wl = sys.argv[2] if len(sys.argv) > 2 else "c2"
+    spec = WORKLOADS[wl]
+    kinds = {k: v for k, v in spec.items() if k in ("encode", "decode")}
+    fetch = counters(os.path.join(d, "pmc_fetch"), "FETCH_SIZE", kinds)
+    write = counters(os.path.join(d, "pmc_write"), "WRITE_SIZE", kinds)
+    out = {"workload": wl, "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on {spec['cmd']}",
            "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB"}
-    for kind, alg in (("encode", ENC_ALG), ("decode", DEC_ALG)):
+    for kind, (pat, alg) in kinds.items():
         if kind in fetch and kind in write:
             rd = 2 * fetch[kind] * 1024
             wr = write[kind] * 1024
-            out[kind] = {"fetch_size_kib": fetch[kind], "write_size_kib": write[kind], "read_bytes": rd,
+            out[kind] = {"kernel": pat, "fetch_size_kib": fetch[kind], "write_size_kib": write[kind], "read_bytes": rd,
                          "write_bytes": wr, "hbm_bytes_per_launch": rd + wr, "algorithmic_bytes": alg,
                          "traffic_over_algorithmic": round((rd + wr) / alg, 4)}
     if "encode" in out:
