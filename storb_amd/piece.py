@@ -68,6 +68,7 @@ PREFETCH_MIN_CHUNK = 512 << 10
 # (tools/stream_rate.py); with 128 KiB pieces the hand-offs cost more than the copies (C1's
 # 4 MiB object fell from 1236-1289 to 811 MiB/s per chunk, 1327-1469 to 868 streamed).
 PARALLEL_COPY_MIN = 256 << 10
+HASH_ON_FILL = True  # encode_chunk: each large piece's id hashing starts as soon as that piece is filled
 STREAM_WINDOW_BYTES = 64 << 20  # chunk bytes per GPU call in the *_stream pipelines
 # encode_chunks_stream(piece_ids=True) over windows whose pieces are all >= PARALLEL_COPY_MIN:
 # the ids come from the GPU SHA-1 kernel, fused after the window's encode, instead of hashlib
@@ -417,9 +418,12 @@ def encode_chunk(chunk: bytes, chunk_idx: int) -> EncodedChunk:
         encoded_pieces = enc_.encode(chunk)
     else:  # piece ids hashed on the pool: data pieces beside the GPU call, parity right after
         hp = _pool("hash")
-        if B >= PARALLEL_COPY_MIN:  # large pieces: their copies on the pool as well, each hashed once filled
+        if B >= PARALLEL_COPY_MIN and HASH_ON_FILL:  # large pieces: copies on the pool too, each hashed once filled
             pieces, hf = _pieces_parallel([chunk], [(k, m, B, padlen)], hash_ids=True)
             encoded_pieces, futs = pieces[0], hf[0]
+        elif B >= PARALLEL_COPY_MIN:  # (A/B: every piece hashed after all are filled)
+            encoded_pieces = _pieces_parallel([chunk], [(k, m, B, padlen)])[0]
+            futs = [hp.submit(_sha1_hex, b) for b in encoded_pieces]
         else:
             prim = _split(chunk, k, B)
             futs = [hp.submit(_sha1_hex, b) for b in prim]

@@ -46,7 +46,12 @@ def main():
     ap.add_argument("--mib", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--gpu-ids", action="store_true", help="also: piece ids from the GPU SHA-1, per window")
+    ap.add_argument("--ab", action="store_true",
+                    help="A/B in one process, rounds interleaved: stream pool of 1 vs STREAM_WORKERS workers, "
+                         "and encode_chunk's id hashing on fill vs after all pieces")
     a = ap.parse_args()
+    if a.ab:
+        return ab(a)
     from storb_amd import piece
 
     data = np.random.default_rng(3).integers(0, 256, a.mib << 20, dtype=np.uint8).tobytes()
@@ -117,6 +122,61 @@ def main():
         res[f"download_per_chunk_{label}"] = round(len(data) / best(down_per_chunk, a.reps) / GIB, 3)
         res[f"download_stream_{label}"] = round(len(data) / best(down_stream, a.reps) / GIB, 3)
     print(json.dumps(res, indent=1))
+
+
+def ab(a):
+    """Interleaved A/B of the stream pool size and of HASH_ON_FILL (best of --reps per round,
+    median over 3 rounds)."""
+    from storb_amd import piece
+
+    data = np.random.default_rng(3).integers(0, 256, a.mib << 20, dtype=np.uint8).tobytes()
+    cs = piece.piece_length(len(data))
+    parts = [data[o:o + cs] for o in range(0, len(data), cs)]
+    enc = list(piece.encode_chunks_stream(iter(parts), piece_ids=True))
+    chunks = [ec.model_copy(update={"pieces": None}) for ec, _ in enc]
+    all_p = [p for ec, _ in enc for p in ec.pieces]
+    lost_p = [p for ec, _ in enc for p in ec.pieces if p.piece_idx != 0]
+    workers0 = piece.STREAM_WORKERS
+
+    def set_workers(n):
+        with piece._pools_lock:
+            old = piece._pools.pop("stream", None)
+        if old is not None:
+            old.shutdown(wait=True)
+        piece.STREAM_WORKERS = n
+
+    def up_chunk():
+        for i, c in enumerate(parts):
+            ec = piece.encode_chunk(c, i)
+            [piece.piece_hash(p.data) for p in ec.pieces]
+
+    def up_stream():
+        list(piece.encode_chunks_stream(iter(parts), piece_ids=True))
+
+    def down(pieces):
+        def run():
+            n = 0
+            for b in piece.reconstruct_data_stream(pieces, chunks):
+                n += len(b)
+            assert n == len(data)
+        return run
+
+    res = {}
+    for _ in range(3):
+        for w in (1, workers0):
+            set_workers(w)
+            for name, fn in (("upload_stream", up_stream), ("download_stream_all_present", down(all_p)),
+                             ("download_stream_piece0_lost", down(lost_p))):
+                fn()  # warm the pool's engines
+                res.setdefault(f"{name}_workers{w}", []).append(len(data) / best(fn, a.reps) / GIB)
+        for hof in (True, False):
+            piece.HASH_ON_FILL = hof
+            up_chunk()
+            res.setdefault(f"upload_per_chunk_hash_on_fill_{hof}", []).append(len(data) / best(up_chunk, a.reps) / GIB)
+        piece.HASH_ON_FILL = True
+    set_workers(workers0)
+    print(json.dumps({"object_bytes": len(data), "chunk_bytes": cs, "unit": "GiB/s, median of 3 rounds of best-of-%d" % a.reps,
+                      **{k: round(float(np.median(v)), 3) for k, v in res.items()}}, indent=1))
 
 
 if __name__ == "__main__":
