@@ -78,7 +78,7 @@ STREAM_WINDOW_BYTES = 64 << 20  # chunk bytes per GPU call in the *_stream pipel
 # 256 / 512 MiB windows against 3.2-5.3 hashing on the host (profiles/r02_stream_rate.json).
 GPU_PIECE_IDS = True
 STREAM_WINDOW_IDS_BYTES = 256 << 20
-STREAM_WORKERS = 4  # worker threads (one engine each) shared by the *_stream pipelines
+STREAM_WORKERS = 4  # single-thread workers (one engine each) the *_stream pipelines are spread over
 
 
 class PieceType(IntEnum):  # piece.py:21-23
@@ -126,16 +126,30 @@ def _usable_cpus() -> int:
 
 
 def _pool(name: str) -> ThreadPoolExecutor:
-    """Module thread pools: "hash" (hashlib SHA-1, which releases the GIL) and "stream"
-    (STREAM_WORKERS workers that run the *_stream pipelines' GPU calls, each on its own engine:
-    concurrent streams, e.g. downloads served on several request threads, do not queue behind
-    one another, and one stream keeps at most two windows in flight)."""
+    """Module thread pools: "hash" (piece copies and hashlib SHA-1, which release the GIL) and
+    "stream<i>" (_stream_pool)."""
     with _pools_lock:
         p = _pools.get(name)
         if p is None:
-            n = STREAM_WORKERS if name == "stream" else max(1, min(HASH_WORKERS, _usable_cpus() - 1))
+            n = 1 if name.startswith("stream") else max(1, min(HASH_WORKERS, _usable_cpus() - 1))
             p = _pools[name] = ThreadPoolExecutor(n, thread_name_prefix=f"storb_amd_{name}")
         return p
+
+
+_stream_rr = [0]
+
+
+def _stream_pool() -> ThreadPoolExecutor:
+    """The worker a new *_stream pipeline runs its GPU calls on: one of STREAM_WORKERS
+    single-thread workers (each with its own engine), round robin.  A stream keeps its windows
+    on its one worker (window w + 1 decodes while the caller consumes window w), and concurrent
+    streams (downloads served on several request threads) do not queue behind one another.
+    (All windows of one stream on 4 shared workers measured 2-7 % slower: tools/stream_rate.py
+    --ab, profiles/r03_stream_ab.json.)"""
+    with _pools_lock:
+        i = _stream_rr[0] % max(1, STREAM_WORKERS)
+        _stream_rr[0] += 1
+    return _pool(f"stream{i}")
 
 
 def _sha1_hex(b) -> str:
@@ -590,7 +604,7 @@ def reconstruct_data_stream(pieces: list[Piece], chunks: list[EncodedChunk], *,
         by_chunk.setdefault(p.chunk_idx, []).append(p)
     wb = STREAM_WINDOW_BYTES if window_bytes is None else window_bytes
     wins = _windows(chunks, wb, lambda c: max(c.original_chunk_size, 1))
-    pool = _pool("stream")
+    pool = _stream_pool()
     nxt = next(wins, None)
     fut = pool.submit(_decode_window, nxt, by_chunk) if nxt is not None else None
     ahead = None
@@ -677,7 +691,7 @@ def encode_chunks_stream(chunks: Iterable[bytes], first_chunk_idx: int = 0, *, p
     wb = window_bytes
     if wb is None:
         wb = STREAM_WINDOW_IDS_BYTES if piece_ids and GPU_PIECE_IDS else STREAM_WINDOW_BYTES
-    pool = _pool("stream")
+    pool = _stream_pool()
     idx = first_chunk_idx
     pending = fut = None
     try:

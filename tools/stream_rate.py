@@ -47,8 +47,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--gpu-ids", action="store_true", help="also: piece ids from the GPU SHA-1, per window")
     ap.add_argument("--ab", action="store_true",
-                    help="A/B in one process, rounds interleaved: stream pool of 1 vs STREAM_WORKERS workers, "
-                         "and encode_chunk's id hashing on fill vs after all pieces")
+                    help="A/B in one process, rounds interleaved: STREAM_WORKERS 1 vs the default (a single stream "
+                         "should not care), and encode_chunk's id hashing on fill vs after all pieces")
     a = ap.parse_args()
     if a.ab:
         return ab(a)
@@ -139,10 +139,6 @@ def ab(a):
     workers0 = piece.STREAM_WORKERS
 
     def set_workers(n):
-        with piece._pools_lock:
-            old = piece._pools.pop("stream", None)
-        if old is not None:
-            old.shutdown(wait=True)
         piece.STREAM_WORKERS = n
 
     def up_chunk():

@@ -43,13 +43,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="direct@SEC_SYN=0,syn@SEC_SYN=1,auto")
+    ap.add_argument("--variants", default="direct@SEC_SYN=0,syn@SEC_SYN=1,auto",
+                    help="name@ENV=V+ENV2=V2[/tag]: environment per variant, optionally a prebuilt variant library "
+                         "storb_amd/lib/libstorbec_<tag>.so (storb_amd._build.build(defines=..., tag=...))")
     ap.add_argument("--cases", default="")
     a = ap.parse_args()
-    variants = []
+    variants = []  # (name, env, lib path or None); "name@ENV=V+ENV2=V2/tag": storb_amd/lib/libstorbec_<tag>.so
     for v in a.variants.split(","):
+        v, _, tag = v.partition("/")
         name, _, env = v.partition("@")
-        variants.append((name, dict(kv.split("=") for kv in env.split("+")) if env else {}))
+        lib = os.path.join(ROOT, "storb_amd", "lib", f"libstorbec_{tag}.so") if tag else None
+        variants.append((name, dict(kv.split("=") for kv in env.split("+")) if env else {}, lib))
     sel = [c for c in CASES if not a.cases or any(t in c[0] for t in a.cases.split(","))]
     for name, k, m, n, nch, e in sel:
         src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
@@ -67,12 +71,12 @@ def main():
         res = {v[0]: {"reassemble": [], "recover_only": []} for v in variants}
         paths = {}
         for _ in range(a.rounds):
-            for vname, env in variants:
+            for vname, env, lib in variants:
                 old = {key: os.environ.get(key) for key in env}
                 os.environ.pop("SEC_SYN", None) if not env else None
                 os.environ.update(env)
                 try:
-                    eng = Engine(0)
+                    eng = Engine(0, lib_path=lib)
                     for mode, args in (("reassemble", (dd, sn, offs, av, out, False)),
                                        ("recover_only", (rd, rsn, roffs, rav, rec, True))):
                         d_, s_, o_, a_, dst, recov = args
