@@ -147,12 +147,12 @@ struct SubPlan {
     uint32_t nsegs = 0, max_seg = 0;       // segment count; most segments of one message
     uint64_t dig_first = 0;                // first digest slot of this unit
     uint64_t dig_off = 0;                  // host mode: digests' offset in the slab output
-    // syndrome decodes (decode): phase 1 launches (bit-sliced syndromes, one per shape), phase 2
-    // groups (sec_decode_kernel over the syndrome rows) and their tail items
-    std::vector<std::pair<int, std::pair<uint32_t, uint32_t>>> syn1;  // (shape, (first, count)) in syn tiles
-    std::vector<Group> groups2;
-    size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_tiles2 = 0, off_tail2 = 0;
-    uint32_t ntail2 = 0;
+    // syndrome decodes (decode): phase 1 launches (bit-sliced syndromes) and phase 2 launches
+    // (the Cauchy solve), one each per shape
+    // (shape, (first, count)) in tiles; synf: the fused kernel (both phases in one wave)
+    std::vector<std::pair<int, std::pair<uint32_t, uint32_t>>> syn1, syn2, synf;
+    size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_vdesc = 0, off_vtiles = 0,
+           off_masks = 0, off_ftiles = 0;
     uint64_t syn_bytes = 0;  // syndrome scratch of this unit
 };
 
@@ -269,25 +269,25 @@ int dec_copy_kb(int k)
     return (v == 4 || v == 8) && (size_t)k <= v ? (int)v : 0;
 }
 
-// Syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel, then sec_decode_kernel on the e
-// syndrome rows) for a chunk that lost e data blocks, when its shape has a bit-sliced kernel.
-// Chosen by a time estimate per 4 byte positions, each kernel taking the longer of its VALU
-// issue time and its HBM time (kVperOp = VALU ops per HBM byte at the measured rates: v_perm
-// rows ~2.8e13 ops/s, mixed traffic ~6 TB/s):
-//   direct:  ceil(e / 8) v_perm row groups (5 selector ops + 4.5 per row) over all k slots;
-//            reads k blocks per row group, writes the chunk (or the e rows);
-//   phase 1: the bit-sliced rows (6 transpose + 2.75 subsets + NR per row group holding a
-//            present parity row) over the k - e present data blocks, 6 per syndrome to transpose
-//            back; reads k blocks, writes the k - e copies (reassembly) and e syndromes;
-//   phase 2: v_perm rows over the e syndromes; reads them per row group, writes e rows.
-// Checked against the in-process A/B on the wide shapes (tools/syn_ab.py,
-// profiles/r03_syn_ab.jsonl): predicted syn / direct 0.70 / 0.95 / 1.16 / 1.40 / 1.25 against
-// measured 0.79 / 1.07 / 1.18 / 1.57 / 1.29 for zfec(64,96) 16 lost, (32,48) 16 and 8 lost,
-// (16,24) 8 and 4 lost; the path is taken when its estimate is under SEC_SYN_RATIO (default
-// 0.85) of the direct one.  SEC_SYN=0 / 1 turns it off / forces it wherever it applies; all
-// read per plan build.  (Two variants measured and dropped: the solve fused into the phase-1
-// kernel, which needs 256+ VGPRs and ran 0.6x the two-phase rate; phase 2 of a part of the
-// chunks overlapped with phase 1 of the rest on a second stream, -1 to -25 %.)
+// Syndrome decode (kernels_bs.hip) for a chunk that lost e data blocks, when its shape has the
+// bit-sliced kernels: the one-wave kernel sec_decode_bs_kernel ("fused": e <= 16 and every
+// present parity row in one 16-row group, the syndromes never leave the registers) or the two
+// kernels sec_syndrome_bs_kernel + sec_solve_bs_kernel ("two": syndromes through HBM, any e).
+// Chosen per chunk by a time estimate per 4 byte positions, each kernel taking the longer of its
+// VALU issue time (ops / R, R the VALU rate it sustains) and its memory time (bytes / BW);
+// both constants per kernel were fitted on the A/B (tools/syn_ab.py, profiles/r03_syn_ab.jsonl:
+// fixed and random erasure patterns of zfec(64,96), (32,48), (16,24) and C4):
+//   direct: ceil(e / 8) v_perm row groups (5 selector ops + 4.5 per row) over all k slots;
+//           R 28 (1e12 lane-ops/s), BW 5.6 TB/s; reads k blocks, writes the chunk (or e rows);
+//   fused:  phase 1 (k - e)(8.75 + e) + 15 e (bit-sliced rows of the present parity rows,
+//           syndrome scaling), phase 2 2.75 e per touched 8-row group + e^2 + 14 e;
+//           R 17, BW 5.0; the direct decode's bytes;
+//   two:    phase 1 P (k - e) 8.75 + (k - e) e + 15 e over P touched parity groups, the data
+//           read once per group (BW 5.0, or 4.0 when P = 2); phase 2 2.75 e per touched 16-row
+//           group + e^2 + 14 e, 2 e rows of syndrome traffic; R 14.5.
+// A syndrome path is taken when its estimate is under SEC_SYN_RATIO (default 0.9) of the direct
+// one.  SEC_SYN=0 / 1 turns the syndrome paths off / forces them wherever they apply (fused
+// where eligible); SEC_SYN_FUSED=0 turns the fused kernel off.  All read per plan build.
 double vperm_ops(int rows, int slots)
 {
     double v = 0;
@@ -296,29 +296,47 @@ double vperm_ops(int rows, int slots)
     return v * slots;
 }
 
-int syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies)
+// shape of the syndrome kernels for this chunk, or -1 (direct); `fused`: the one-wave kernel
+int syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies, bool &fused)
 {
+    fused = false;
     const char *env = getenv("SEC_SYN");
     if (env && env[0] == '0')
         return -1;
     const int sh = sec_syn_shape(c.k, c.m);
     if (sh < 0 || e < 1 || c.B < 16 || c.B > 0xFFFFFFFFull - 8192 || c.padlen >= c.B)
         return -1;
-    if (env && env[0] == '1')
-        return sh;
-    constexpr double kVperOp = 1.0 / 4.63;
-    const int k = c.k, NR = sec_bs_rows(sh), G = (e + sec::kMaxRows - 1) / sec::kMaxRows;
-    uint64_t touched = 0;  // parity row groups that hold a present row
+    const int k = c.k, NR = sec_bs_rows(sh), NR2 = sec_solve_rows(sh);
+    uint64_t touched = 0, g8 = 0, g16 = 0;  // parity groups with a present row, data groups with a lost one
     for (int s = 0; s < k; ++s)
-        if (idx[s] >= k)
+        if (idx[s] >= k) {
             touched |= 1ull << ((idx[s] - k) / NR);
-    auto t = [&](double ops, double bytes) { return std::max(ops * kVperOp, bytes); };
-    const double direct = t(vperm_ops(e, k), 4.0 * (k * G + (copies ? k : e)));
-    const double p1 = t(__builtin_popcountll(touched) * (k - e) * (8.75 + NR) + 6.0 * e, 4.0 * (k + (copies ? k : e)));
-    const double p2 = t(vperm_ops(e, e), 4.0 * (e * G + e));
+            g8 |= 1ull << (s / 8);
+            g16 |= 1ull << (s / NR2);
+        }
+    const int P = __builtin_popcountll(touched);
+    const char *fz = getenv("SEC_SYN_FUSED");
+    const bool can_fuse = P == 1 && e <= 16 && !(fz && fz[0] == '0');
+    if (env && env[0] == '1') {
+        fused = can_fuse;
+        return sh;
+    }
+    auto t = [](double ops, double R, double bytes, double bw) { return std::max(ops / R, bytes / bw); };
+    const double E = e, KE = k - e, out = copies ? k : e;
+    const double direct = t(vperm_ops(e, k), 28, 4.0 * (k + out), 5.6);
+    const double p2 = 2.75 * E * __builtin_popcountll(g16) + E * E + 14 * E;
+    const double two = t(P * KE * 8.75 + KE * E + 15 * E, 14.5, 4.0 * (k + (P - 1) * KE + (copies ? KE : 0) + E),
+                         P > 1 ? 4.0 : 5.0) +
+                       t(p2, 14.5, 4.0 * 2 * E, 5.0);
+    const double fuse = can_fuse ? t(KE * (8.75 + E) + 15 * E + 2.75 * E * __builtin_popcountll(g8) + E * E + 14 * E,
+                                     17, 4.0 * (k + out), 5.0)
+                                 : 1e30;
     const char *ratio = getenv("SEC_SYN_RATIO");
-    const double lim = ratio && *ratio ? atof(ratio) : 0.85;
-    return p1 + p2 < lim * direct ? sh : -1;
+    const double lim = (ratio && *ratio ? atof(ratio) : 0.9) * direct;
+    if (std::min(two, fuse) >= lim)
+        return -1;
+    fused = fuse <= two;
+    return sh;
 }
 
 // Work for one chunk.  `valid` = positions where every block is fully readable and
@@ -975,6 +993,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
     std::vector<PendingExpand> pending;
     std::vector<uint32_t> tab_of((size_t)nchunks, 0), e_of((size_t)nchunks, 0);
     std::vector<int> syn_of((size_t)nchunks, -1);  // syndrome-decode shape, or -1 (syn_choice)
+    std::vector<char> fuse_of((size_t)nchunks, 0);  // ... in the one-wave kernel
     for (int attempt = 0;; ++attempt) {
         pending.clear();
         size_t need = 0;
@@ -995,9 +1014,12 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             bool whole = true;
             for (int s = 0; s < k && whole && !host; ++s)
                 whole = idx[s] == k - 1 || slot_avail(c, block_avail, L.perm[L.first[i] + s]) >= c.B;
-            const int sh = syn_of[i] = whole ? syn_choice(c, idx, (int)miss.size(), !recover && !nocopy) : -1;
-            // the syndrome path's table is A^-1 (e x e), the direct path's the decode matrix rows
-            std::string key = (sh >= 0 ? "S" : "") + std::to_string(k) + "/" + std::to_string(c.m) + ":";
+            bool fz = false;
+            const int sh = syn_of[i] = whole ? syn_choice(c, idx, (int)miss.size(), !recover && !nocopy, fz) : -1;
+            fuse_of[i] = fz;
+            if (sh >= 0)
+                continue;  // the syndrome path's matrices are compile-time (its scalings: the plan image)
+            std::string key = std::to_string(k) + "/" + std::to_string(c.m) + ":";
             for (int s = 0; s < k; ++s)
                 key += std::to_string(idx[s]) + ",";
             auto it = tc.index.find(key);
@@ -1007,26 +1029,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             }
             const int e = (int)miss.size();
             std::vector<uint8_t> coef;
-            if (sh >= 0) {
-                // syndrome q belongs to the q-th present parity row (ascending); lost primary r
-                // = A^-1 s with A[q][r] = enc[k + that row][miss[r]]
-                std::vector<int> prow;
-                for (int s = 0; s < k; ++s)
-                    if (idx[s] >= k)
-                        prow.push_back(idx[s]);
-                std::sort(prow.begin(), prow.end());
-                const std::vector<uint8_t> enc = sec::encode_matrix(k, c.m);
-                std::vector<uint8_t> a((size_t)e * e);
-                for (int q = 0; q < e; ++q)
-                    for (int r = 0; r < e; ++r)
-                        a[(size_t)q * e + r] = enc[(size_t)prow[q] * k + miss[r]];
-                if (!sec::gf_invert(a, e))
-                    return SEC_ESINGULAR;
-                coef.resize((size_t)e * e);
-                for (int q = 0; q < e; ++q)  // layout [slot q][missing r]
-                    for (int r = 0; r < e; ++r)
-                        coef[(size_t)q * e + r] = a[(size_t)r * e + q];
-            } else {
+            {
                 std::vector<int> iv(idx, idx + k);
                 std::vector<uint8_t> minv;
                 if (!sec::decode_matrix(k, c.m, iv, minv))
@@ -1075,15 +1078,15 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         std::vector<uint32_t> srow, mrow, savail;
         Bins bins;
         std::vector<sec::TailItem> tail;
-        // syndrome decodes: phase-1 descriptors, slots and tiles (per shape); phase-2
-        // descriptors (appended to descs), tiles and tail items
+        // syndrome decodes: phase-1 descriptors, slots and tiles, phase-2 descriptors and tiles
+        // (tiles per shape), the scalings of both
         std::vector<sec::SynDesc> sdescs;
         std::vector<uint64_t> ssoff;
         std::vector<uint32_t> ssavail;
-        std::map<int, std::vector<sec::Tile>> stiles;
-        std::vector<sec::DecDesc> descs2;
-        Bins bins2;
-        std::vector<sec::TailItem> tail2;
+        std::map<int, std::vector<sec::Tile>> stiles, vtiles, ftiles;
+        std::vector<sec::SolveDesc> vdescs;
+        std::vector<uint64_t> masks;                                    // w / z scalings (scale_mask)
+        std::map<std::string, std::pair<uint32_t, uint32_t>> mask_of;  // pattern -> (wq0, zq0)
         const int syn_lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
         for (int64_t i = c0; i < c1; ++i) {
             const sec_dec_chunk &c = chunks[i];
@@ -1130,7 +1133,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 sd.out_off = d.out_off;
                 sd.syn_off = sp.syn_bytes;
                 sd.B = (uint32_t)c.B;
-                sd.last = copies ? (uint32_t)(nout - (uint64_t)(k - 1) * c.B) : 0;
+                sd.last = recover ? (uint32_t)c.B : (uint32_t)(nout - (uint64_t)(k - 1) * c.B);
                 sd.slot0 = (uint32_t)ssoff.size();
                 ssoff.resize(ssoff.size() + (size_t)(k + p), 0);
                 ssavail.resize(ssavail.size() + (size_t)(k + p), 0);
@@ -1140,54 +1143,106 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                     ssoff[j] = soff[slot0 + s];
                     ssavail[j] = savail[slot0 + s];
                 }
-                sp.syn_bytes += (uint64_t)e * c.B;
                 std::vector<int> gs;  // touched row groups, ascending
                 for (int g = 0; g * NR < p; ++g)
                     if ((sd.pmask >> (g * NR)) & ((NR >= 64 ? ~0ull : (1ull << NR) - 1)))
                         gs.push_back(g);
+                const bool fused = fuse_of[i];  // both phases in one wave (syn_choice)
+                if (!fused)
+                    sp.syn_bytes += (uint64_t)e * sec::syn_stride(c.B);
+                // the scalings of this erasure pattern (shared by the chunks that have it)
+                uint64_t lost = 0;
+                std::string key = std::to_string(k) + "/" + std::to_string(c.m) + ":";
+                for (int s = 0; s < k; ++s) {
+                    key += std::to_string(idx[s]) + ",";
+                    if (idx[s] >= k)
+                        lost |= 1ull << s;
+                }
+                auto mk = mask_of.find(key);
+                if (mk == mask_of.end()) {
+                    std::vector<int> S, Lost;
+                    for (int r = 0; r < p; ++r)
+                        if ((sd.pmask >> r) & 1)
+                            S.push_back(r);
+                    for (int s = 0; s < k; ++s)
+                        if ((lost >> s) & 1)
+                            Lost.push_back(s);
+                    std::vector<uint8_t> w, z;
+                    sec::cauchy_scales(k, S, Lost, w, z);
+                    const std::pair<uint32_t, uint32_t> at{(uint32_t)masks.size(), (uint32_t)(masks.size() + e)};
+                    for (uint8_t v : w)
+                        masks.push_back(sec::scale_mask(v));
+                    for (uint8_t v : z)
+                        masks.push_back(sec::scale_mask(v));
+                    mk = mask_of.emplace(key, at).first;
+                }
+                sd.wq0 = mk->second.first;
+                sd.zq0 = mk->second.second;
+                sd.flags = recover ? 2u : 0u;
                 const uint32_t si = (uint32_t)sdescs.size();
                 sdescs.push_back(sd);
                 const uint64_t step = (uint64_t)sec_bs_span() * (syn_lanes / 64);
+                if (fused) {
+                    auto &ft = ftiles[sh];
+                    for (uint64_t t = 0; t < c.B; t += step)
+                        ft.push_back(sec::Tile{si, (uint32_t)t, (uint32_t)(gs[0] * NR), copies ? 1u : 0u});
+                    continue;
+                }
                 auto &st = stiles[sh];
                 for (uint64_t t0 = 0; t0 < c.B; t0 += 8 * step)  // runs of 8 positions per group: one XCD
                     for (int g : gs)
                         for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
                             st.push_back(sec::Tile{si, (uint32_t)t, (uint32_t)(g * NR), copies && g == gs[0] ? 1u : 0u});
-                // phase 2: the e syndrome rows are the slots of a plain decode whose matrix is A^-1
-                sec::DecDesc d2 = d;
-                d2.k = (uint32_t)e;
-                d2.slot0 = (uint32_t)soff.size();
-                const int64_t valid2 = recover ? (int64_t)c.B : (int64_t)nout - (int64_t)(k - 1) * (int64_t)c.B;
-                d2.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid2, (int64_t)c.B));
-                for (int q = 0; q < e; ++q) {
-                    soff.push_back(sd.syn_off + (uint64_t)q * c.B);
-                    srow.push_back(0xFFFFFFFFu);
-                    savail.push_back((uint32_t)c.B);
-                    mrow.push_back(mr[q]);
-                }
-                const uint32_t di = (uint32_t)((c1 - c0) + descs2.size());
-                descs2.push_back(d2);
-                add_work(bins2, tail2, di, c.B, valid2, e, e, true, 0, false, dec_small_kb(e));
+                // phase 2: the groups of lost rows, their tiles interleaved as phase 1's
+                sec::SolveDesc vd{};
+                vd.out_off = d.out_off;
+                vd.syn_off = sd.syn_off;
+                vd.lost = lost;
+                vd.pmask = sd.pmask;
+                vd.B = (uint32_t)c.B;
+                vd.last = recover ? (uint32_t)c.B : (uint32_t)(nout - (uint64_t)(k - 1) * c.B);
+                vd.zq0 = mk->second.second;
+                vd.recover = recover ? 1u : 0u;
+                const uint32_t vi = (uint32_t)vdescs.size();
+                vdescs.push_back(vd);
+                const int NR2 = sec_solve_rows(sh);
+                std::vector<int> gl;
+                for (int g = 0; g * NR2 < k; ++g)
+                    if ((lost >> (g * NR2)) & ((NR2 >= 64 ? ~0ull : (1ull << NR2) - 1)))
+                        gl.push_back(g);
+                auto &vt = vtiles[sh];
+                for (uint64_t t0 = 0; t0 < c.B; t0 += 8 * step)
+                    for (int g : gl)
+                        for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
+                            vt.push_back(sec::Tile{vi, (uint32_t)t, (uint32_t)(g * NR2), 0u});
             } else if (nout > 0 && !(nocopy && e_of[i] == 0)) {
                 add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true, 0, false,
                          recover || nocopy ? dec_small_kb(c.k) : dec_copy_kb(c.k));
             }
         }
-        descs.insert(descs.end(), descs2.begin(), descs2.end());
-        std::vector<sec::Tile> tiles, tiles2, stl;
+        std::vector<sec::Tile> tiles, stl, vtl;
         flatten(bins, sp.groups, tiles, true);
-        flatten(bins2, sp.groups2, tiles2, true);
         for (auto &kv : stiles) {
             sp.syn1.push_back({kv.first, {(uint32_t)stl.size(), (uint32_t)kv.second.size()}});
             stl.insert(stl.end(), kv.second.begin(), kv.second.end());
         }
-        sp.ntail2 = (uint32_t)tail2.size();
+        for (auto &kv : vtiles) {
+            sp.syn2.push_back({kv.first, {(uint32_t)vtl.size(), (uint32_t)kv.second.size()}});
+            vtl.insert(vtl.end(), kv.second.begin(), kv.second.end());
+        }
+        std::vector<sec::Tile> ftl;
+        for (auto &kv : ftiles) {
+            sp.synf.push_back({kv.first, {(uint32_t)ftl.size(), (uint32_t)kv.second.size()}});
+            ftl.insert(ftl.end(), kv.second.begin(), kv.second.end());
+        }
+        sp.off_ftiles = img.put(ftl.data(), ftl.size() * sizeof(sec::Tile));
         sp.off_sdesc = img.put(sdescs.data(), sdescs.size() * sizeof(sec::SynDesc));
         sp.off_stiles = img.put(stl.data(), stl.size() * sizeof(sec::Tile));
         sp.off_ssoff = img.put(ssoff.data(), ssoff.size() * 8);
         sp.off_ssavail = img.put(ssavail.data(), ssavail.size() * 4);
-        sp.off_tiles2 = img.put(tiles2.data(), tiles2.size() * sizeof(sec::Tile));
-        sp.off_tail2 = img.put(tail2.data(), tail2.size() * sizeof(sec::TailItem));
+        sp.off_vdesc = img.put(vdescs.data(), vdescs.size() * sizeof(sec::SolveDesc));
+        sp.off_vtiles = img.put(vtl.data(), vtl.size() * sizeof(sec::Tile));
+        sp.off_masks = img.put(masks.data(), masks.size() * 8);
         sp.ntail = (uint32_t)tail.size();
         sp.off_desc = img.put(descs.data(), descs.size() * sizeof(sec::DecDesc));
         sp.off_tiles = img.put(tiles.data(), tiles.size() * sizeof(sec::Tile));
@@ -1224,37 +1279,34 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_tail");
     }
-    if (sp.syn1.empty())
+    if (sp.syn1.empty() && sp.synf.empty())
         return SEC_OK;
-    if (!syn)
+    if (!syn && !sp.syn1.empty())
         return SEC_EINVAL;
-    // syndrome decodes: phase 1 (syndromes + present primaries' copies), then phase 2 on the
-    // syndrome rows (blocks = the scratch), in stream order
+    // syndrome decodes: phase 1 (scaled syndromes + present primaries' copies), then phase 2
+    // (the Cauchy solve) on the syndrome planes, in stream order
+    const uint64_t *masks = plan.meta.as<uint64_t>(sp.off_masks);
     const sec::SynDesc *sd = plan.meta.as<sec::SynDesc>(sp.off_sdesc);
     const sec::Tile *st = plan.meta.as<sec::Tile>(sp.off_stiles);
-    const sec::SynSlots ss{plan.meta.as<uint64_t>(sp.off_ssoff), plan.meta.as<uint32_t>(sp.off_ssavail)};
+    const sec::SynSlots ss{plan.meta.as<uint64_t>(sp.off_ssoff), plan.meta.as<uint32_t>(sp.off_ssavail), masks};
     const int lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
-    const sec::Tile *dt2 = plan.meta.as<sec::Tile>(sp.off_tiles2);
-    auto phase1 = [&](size_t i, uint32_t first, uint32_t count) {
-        const auto &g = sp.syn1[i];
-        int e = sec_launch_syndrome_bs(g.first, lanes, blocks, out, syn, sd, st + g.second.first + first, count, ss, s);
-        return e ? hip_fail((hipError_t)e, "sec_syndrome_bs_kernel") : SEC_OK;
-    };
-    auto phase2 = [&](size_t i, uint32_t first, uint32_t count, hipStream_t q) {
-        const Group &g = sp.groups2[i];
-        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, syn, out, dd, dt2 + g.first + first, count, tabs, sl, q,
-                                  g.mfma);
-        return e ? hip_fail((hipError_t)e, "sec_decode_kernel") : SEC_OK;
-    };
-    for (size_t i = 0; i < sp.syn1.size(); ++i)
-        RC(phase1(i, 0, sp.syn1[i].second.second));
-    for (size_t i = 0; i < sp.groups2.size(); ++i)
-        RC(phase2(i, 0, sp.groups2[i].count, s));
-    if (sp.ntail2) {
-        int e = sec_launch_decode_tail(syn, out, dd, plan.meta.as<sec::TailItem>(sp.off_tail2), sp.ntail2, tabs, sl,
-                                       s);
+    const sec::Tile *ft = plan.meta.as<sec::Tile>(sp.off_ftiles);
+    for (const auto &g : sp.synf) {
+        int e = sec_launch_decode_bs(g.first, lanes, blocks, out, sd, ft + g.second.first, g.second.second, ss, s);
         if (e)
-            return hip_fail((hipError_t)e, "sec_decode_tail");
+            return hip_fail((hipError_t)e, "sec_decode_bs_kernel");
+    }
+    for (const auto &g : sp.syn1) {
+        int e = sec_launch_syndrome_bs(g.first, lanes, blocks, out, syn, sd, st + g.second.first, g.second.second, ss, s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_syndrome_bs_kernel");
+    }
+    const sec::SolveDesc *vd = plan.meta.as<sec::SolveDesc>(sp.off_vdesc);
+    const sec::Tile *vt = plan.meta.as<sec::Tile>(sp.off_vtiles);
+    for (const auto &g : sp.syn2) {
+        int e = sec_launch_solve_bs(g.first, lanes, syn, out, vd, vt + g.second.first, g.second.second, masks, s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_solve_bs_kernel");
     }
     return SEC_OK;
 }

@@ -123,6 +123,63 @@ inline void normalise_slots(int k, std::vector<int> &idx, std::vector<int> &perm
     }
 }
 
+// zfec's evaluation points: p_0 = 0, p_i = alpha^(i-1) (the seed rows above)
+inline uint8_t point(int i) { return i == 0 ? 0 : gf().exp[(i - 1) % 255]; }
+
+// Scalings of the syndrome decode's Cauchy solve (kernels_bs.hip).  zfec's parity row r is the
+// Lagrange basis at x_r = p_{k+r}: c[r][j] = a_r b_j / (x_r + y_j) with y_j = p_j,
+// a_r = prod_{i<k} (x_r + y_i), b_j = 1 / prod_{i<k, i!=j} (y_j + y_i).  For the present parity
+// rows S (ascending) and the lost data rows L (ascending), |S| = |L| = e, the e x e system
+// A = c[S][L] = D_a C D_b has C a Cauchy matrix, whose inverse is again one up to diagonals, so
+//     A^-1[l][r] = z_l c[r][l] w_r,
+//     w_r = prod_{l in L} (x_r + y_l) / prod_{r' in S, r' != r} (x_r + x_r') / a_r^2,
+//     z_l = prod_{r in S} (x_r + y_l) / prod_{l' in L, l' != l} (y_l + y_l') / b_l^2.
+// Checked against a Gauss-Jordan inverse for every shape (tests/test_cauchy.py restates it).
+inline void cauchy_scales(int k, const std::vector<int> &S, const std::vector<int> &Lost, std::vector<uint8_t> &w,
+                          std::vector<uint8_t> &z)
+{
+    const Gf &g = gf();
+    auto div = [&](uint8_t a, uint8_t b) { return g.mul(a, g.inv[b]); };
+    const size_t e = S.size();
+    w.assign(e, 0);
+    z.assign(e, 0);
+    for (size_t q = 0; q < e; ++q) {
+        const uint8_t x = point(k + S[q]);
+        uint8_t num = 1, den = 1, a = 1;
+        for (int l : Lost)
+            num = g.mul(num, x ^ point(l));
+        for (size_t q2 = 0; q2 < e; ++q2)
+            if (q2 != q)
+                den = g.mul(den, x ^ point(k + S[q2]));
+        for (int i = 0; i < k; ++i)
+            a = g.mul(a, x ^ point(i));
+        w[q] = div(div(num, den), g.mul(a, a));
+    }
+    for (size_t t = 0; t < e; ++t) {
+        const uint8_t y = point(Lost[t]);
+        uint8_t num = 1, den = 1, binv = 1;  // binv = 1 / b_l
+        for (int r : S)
+            num = g.mul(num, point(k + r) ^ y);
+        for (size_t t2 = 0; t2 < e; ++t2)
+            if (t2 != t)
+                den = g.mul(den, y ^ point(Lost[t2]));
+        for (int i = 0; i < k; ++i)
+            if (i != Lost[t])
+                binv = g.mul(binv, y ^ point(i));
+        z[t] = g.mul(div(num, den), g.mul(binv, binv));
+    }
+}
+
+// Multiplication by c on bit planes (kernels_bs.hip scale_planes): byte s = c * alpha^s, so
+// plane t of c * x is the XOR of the planes s of x whose byte s has bit t set.
+inline uint64_t scale_mask(uint8_t c)
+{
+    uint64_t m = 0;
+    for (int s = 0; s < 8; ++s)
+        m |= (uint64_t)gf().mul(c, (uint8_t)(1u << s)) << (8 * s);
+    return m;
+}
+
 // Inverse of zfec's decode matrix for normalised slot indices.
 inline bool decode_matrix(int k, int m, const std::vector<int> &idx, std::vector<uint8_t> &minv)
 {

@@ -66,24 +66,45 @@ struct DecSlots {
     const uint32_t *avail;  // bytes of the block that exist in memory; the rest read as zero
 };
 
-// One chunk of a syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel; 48 B).  Block j of
+// One chunk of a syndrome decode (kernels_bs.hip sec_syndrome_bs_kernel, sec_decode_bs_kernel; 56 B).  Block j of
 // the chunk (data j < k, parity row r at j = k + r) is at blocks + off[slot0 + j] with
 // avail[slot0 + j] readable bytes, when its bit in dmask / pmask is set.
 struct SynDesc {
     uint64_t out_off;  // reassembled chunk in `out`: present primaries are copied there (tile flag)
-    uint64_t syn_off;  // syndrome q (of the q-th present parity row) at syn + syn_off + q * B
+    uint64_t syn_off;  // syndrome q (of the q-th present parity row) at syn + syn_off + q * syn_stride(B)
     uint64_t dmask;    // bit j: data block j present (k <= 64)
     uint64_t pmask;    // bit r: parity row r present (m - k <= 64)
     uint32_t B;
-    uint32_t last;     // bytes of output row k-1 (n - (k-1)*B): its stores stop there
+    uint32_t last;     // bytes of output row k-1 (n - (k-1)*B): its stores stop there (recover-only: B)
     uint32_t slot0;
-    uint32_t pad;
+    uint32_t wq0;      // masks[wq0 + q]: the scaling w of syndrome q (scale_mask)
+    uint32_t zq0;      // fused kernel: masks[zq0 + t], the scaling z of the t-th lost row
+    uint32_t flags;    // fused kernel: bit 1 = recover-only (recovered rows by rank)
 };
 
 struct SynSlots {
     const uint64_t *off;
     const uint32_t *avail;
+    const uint64_t *masks;  // scalings of both phases (scale_mask layout)
 };
+
+// One chunk of a syndrome decode, phase 2 (kernels_bs.hip sec_solve_bs_kernel; 48 B): the lost
+// data rows from the scaled bit-sliced syndromes.
+struct SolveDesc {
+    uint64_t out_off;
+    uint64_t syn_off;  // as SynDesc
+    uint64_t lost;     // bit l: data row l is recovered
+    uint64_t pmask;    // bit r: parity row r present (syndrome q = the q-th set bit)
+    uint32_t B;
+    uint32_t last;     // bytes output row k-1 holds (reassembly; recover-only: B)
+    uint32_t zq0;      // masks[zq0 + t]: the scaling z of the t-th recovered row (ascending)
+    uint32_t recover;  // 1: recovered row t at out_off + t * B (else row l at out_off + l * B)
+};
+
+// Syndromes are stored bit-sliced (a lane's 8 planes where its 32 bytes would be), at the
+// lanes' unclamped positions: rows of whole 2048-position wave spans.
+constexpr uint64_t kSynSpan = 2048;
+constexpr uint64_t syn_stride(uint64_t B) { return (B + kSynSpan - 1) / kSynSpan * kSynSpan; }
 
 struct Tile {
     uint32_t chunk;  // descriptor index
@@ -143,6 +164,14 @@ int sec_syn_shape(int k, int m);
 int sec_launch_syndrome_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, uint8_t *syn,
                            const sec::SynDesc *descs, const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl,
                            void *stream);
+// Both phases in one kernel (e <= 16 and every present parity row in the tile's row group r0):
+// the syndromes stay in registers
+int sec_launch_decode_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, const sec::SynDesc *descs,
+                         const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream);
+// Phase 2: the lost data rows of row group r0 / sec_solve_rows(shape) of each tile's chunk
+int sec_solve_rows(int shape);
+int sec_launch_solve_bs(int shape, int lanes, const uint8_t *syn, uint8_t *out, const sec::SolveDesc *descs,
+                        const sec::Tile *t, uint32_t ntiles, const uint64_t *masks, void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
                            uint32_t nitems, const uint32_t *tabs, void *stream);
 // kb (4 or 8): the kernel variant whose load batch is kb slots (every chunk of the group has

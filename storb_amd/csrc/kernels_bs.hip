@@ -136,6 +136,10 @@ __device__ __forceinline__ void st16(u8 *p, u32 a, u32 b, u32 c, u32 d)
     __builtin_nontemporal_store(u32x4{a, b, c, d}, reinterpret_cast<u32x4_u *>(p));
 }
 
+#ifndef SEC_BS_SKIP_DUP
+#define SEC_BS_SKIP_DUP 0
+#endif
+
 // acc (= or ^=) the output plane whose input mask is MSK
 template <u32 MSK, bool FIRST>
 __device__ __forceinline__ void upd(u32 &acc, const u32 (&lo)[16], const u32 (&hi)[16])
@@ -269,8 +273,12 @@ __device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restric
             y[i] = acc[r * 8 + i];
         transpose8(y);
         u8 *o = dst + (u64)(R0 + r) * d.par_stride;
-        st16(o + pa, y[0], y[1], y[2], y[3]);
-        st16(o + pb, y[4], y[5], y[6], y[7]);
+        // SEC_BS_SKIP_DUP (build knob, A/B): a piece whose unclamped start is past B only
+        // repeats the store of the piece clamped to B - 16; skip it
+        if (!SEC_BS_SKIP_DUP || s + lane < B)
+            st16(o + pa, y[0], y[1], y[2], y[3]);
+        if (!SEC_BS_SKIP_DUP || s + 1024 + lane < B)
+            st16(o + pb, y[4], y[5], y[6], y[7]);
     }
 }
 
@@ -308,17 +316,22 @@ __global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs2_kernel(c
         bs_span<K, M, NR, NR, D, false>(in, par, d, s);
 }
 
-// ---- decode, phase 1: syndromes of the present parity rows (wide decodes) -------------------
-// A decode that lost e data blocks and holds e parity rows S instead: for a parity row r in S,
-//     s_r = p_r ^ XOR_{present j} c[r][j] * d_j  =  XOR_{lost j} c[r][j] * d_j,
-// so the lost blocks are A^-1 s with A = c[S][lost] (e x e).  Phase 1 is this kernel: the
-// bit-sliced encode of the PRESENT data blocks (the matrix c at compile time, a block the chunk
-// lacks skipped by a wave-uniform branch), XORed with the present parity rows and stored as e
-// syndrome rows.  While it has each present data block in registers it also stores it to its
-// output row (the copy half of a reassembly).  Phase 2 applies the run-time e x e inverse with
-// sec_decode_kernel (api.cpp).  Per input dword this costs the bit-sliced rows (6 + 2.75 + NR +
-// 6 NR / 64 VALU) instead of ceil(e / 8) v_perm row groups over all k blocks (5 + 36 VALU each),
-// and reads the k blocks once instead of once per 8-row group.
+// ---- decode: syndromes of the present parity rows, then a Cauchy solve (wide decodes) --------
+// A decode that lost e data blocks L and holds e parity rows S instead: for a parity row r in S,
+//     s_r = p_r ^ XOR_{present j} c[r][j] * d_j  =  XOR_{l in L} c[r][l] * d_l,
+// so the lost blocks are A^-1 s with A = c[S][L] (e x e).  zfec's parity rows are a Cauchy
+// matrix up to diagonal scalings (c[r][j] = a_r b_j / (x_r + y_j) on its evaluation points), and
+// so is A^-1:  A^-1[l][r] = z_l c[r][l] w_r  (gf_host.hpp cauchy_scales).  Both phases therefore
+// apply compile-time matrices on bit planes, with run-time diagonal scalings in between:
+//   phase 1 (sec_syndrome_bs_kernel): the bit-sliced encode of the PRESENT data blocks (a block
+//     the chunk lacks skipped by a wave-uniform branch) XORed with the present parity rows,
+//     scaled by w_r and stored as bit planes (no transpose back).  While it has each present data
+//     block in registers it also stores it to its output row (the copy half of a reassembly);
+//   phase 2 (sec_solve_bs_kernel): the transposed parity matrix c[S][l] over the scaled
+//     syndromes for the lost rows l of one 16-row group, scaled by z_l and transposed back.
+// Per input dword phase 1 costs 6 + 2.75 + NR (bit-sliced rows) and 15 per syndrome; phase 2
+// 2.75 per syndrome and row group plus 1 per (syndrome, lost row) and 14 per lost row, against
+// ceil(e / 8) v_perm row groups over all k blocks (5 + 36 VALU each) for the direct decode.
 //
 // Items 0..K-1 of a chunk are its data blocks, K..K+NR-1 the parity rows R0.. of this tile's
 // group; one ring of D items in flight serves both.  Results are zfec's fec_decode (restated in
@@ -367,9 +380,40 @@ struct SynCtx {
     const u8 *blocks;
     const uint64_t *off;
     const uint32_t *avail;
-    u32 slot0, pa, pb;
-    uint64_t dmask, pmask;
+    const uint64_t *wmask;  // masks + wq0
+    u32 slot0, pa, pb, ua, ub;  // clamped (block) and unclamped (syndrome) lane positions
+    uint64_t dmask, pmask, stride;
 };
+
+// a ^ (b & m), m wave-uniform (an SGPR holding 0 or ~0)
+__device__ __forceinline__ u32 xor_and(u32 a, u32 b, u32 m)
+{
+    u32 r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x78" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+
+// bit i of w as 0 / ~0
+__device__ __forceinline__ u32 bitmask(u32 w, int i) { return (u32)((int32_t)(w << (31 - i)) >> 31); }
+
+// y <- c * y on bit planes, m = scale_mask(c) (gf_host.hpp): byte s of m is c * alpha^s, so
+// plane t of the product is the XOR of the planes s whose byte s has bit t set (64 VALU)
+__device__ __forceinline__ void scale_planes(u32 (&y)[8], uint64_t m)
+{
+    const u32 w0 = (u32)m, w1 = (u32)(m >> 32);
+    u32 o[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+        o[t] = y[0] & bitmask(w0, t);
+#pragma unroll
+    for (int s = 1; s < 8; ++s)
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+            o[t] = xor_and(o[t], y[s], bitmask(s < 4 ? w0 : w1, 8 * (s & 3) + t));
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+        y[t] = o[t];
+}
 
 template <int K, int NR, int R0>
 __device__ __forceinline__ bool item_present(const SynCtx &c, int J)
@@ -391,7 +435,44 @@ __device__ __forceinline__ void load_syn_first(std::integer_sequence<int, Js...>
     ((item_present<K, NR, R0>(c, Js) ? load_syn_item<K, NR, R0, Js>(ring[Js], c) : void()), ...);
 }
 
-template <int K, int M, int R0, int NR, int D, int J>
+// acc (8 planes) ^= c[PR][DL] * the input whose plane subsets are lo / hi, skipped when bit BIT
+// of `lost` is clear (phase 2: data row DL not lost; phase 1: parity row PR absent).  The wave-uniform branch lives inside the asm statement, so the compiler sees
+// straight-line code: as C++ branches (one per row and input) the same skips cost 50-100 VGPRs
+// (one wave per SIMD); per block of 4 rows they fit but compute every row of a touched block.
+template <int K, int M, int PR, int DL, int BIT = DL>
+__device__ __forceinline__ void coef_planes_skip(u32 *a, const u32 (&lo)[16], const u32 (&hi)[16], uint64_t lost)
+{
+    constexpr uint32_t c = gfc::Matrix<K, M>::v.c[PR][DL];
+    constexpr u32 m0 = plane_mask(c, 0), m1 = plane_mask(c, 1), m2 = plane_mask(c, 2), m3 = plane_mask(c, 3),
+                  m4 = plane_mask(c, 4), m5 = plane_mask(c, 5), m6 = plane_mask(c, 6), m7 = plane_mask(c, 7);
+    asm volatile("s_bitcmp1_b64 %8, %25\n\t"
+                 "s_cbranch_scc0 1f\n\t"
+                 "v_bitop3_b32 %0, %0, %9, %10 bitop3:0x96\n\t"
+                 "v_bitop3_b32 %1, %1, %11, %12 bitop3:0x96\n\t"
+                 "v_bitop3_b32 %2, %2, %13, %14 bitop3:0x96\n\t"
+                 "v_bitop3_b32 %3, %3, %15, %16 bitop3:0x96\n\t"
+                 "v_bitop3_b32 %4, %4, %17, %18 bitop3:0x96\n\t"
+                 "v_bitop3_b32 %5, %5, %19, %20 bitop3:0x96\n\t"
+                 "v_bitop3_b32 %6, %6, %21, %22 bitop3:0x96\n\t"
+                 "v_bitop3_b32 %7, %7, %23, %24 bitop3:0x96\n"
+                 "1:"
+                 : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7])
+                 : "s"(lost), "v"(lo[m0 & 15]), "v"(hi[m0 >> 4]), "v"(lo[m1 & 15]), "v"(hi[m1 >> 4]),
+                   "v"(lo[m2 & 15]), "v"(hi[m2 >> 4]), "v"(lo[m3 & 15]), "v"(hi[m3 >> 4]), "v"(lo[m4 & 15]),
+                   "v"(hi[m4 >> 4]), "v"(lo[m5 & 15]), "v"(hi[m5 >> 4]), "v"(lo[m6 & 15]), "v"(hi[m6 >> 4]),
+                   "v"(lo[m7 & 15]), "v"(hi[m7 >> 4]), "i"(BIT)
+                 : "scc");
+}
+
+// data block J's contribution to the present parity rows R0 + r of the group
+template <int K, int M, int R0, int J, int... Rs>
+__device__ __forceinline__ void syn_rows(std::integer_sequence<int, Rs...>, u32 *acc, const u32 (&lo)[16],
+                                         const u32 (&hi)[16], uint64_t pmask)
+{
+    (coef_planes_skip<K, M, R0 + Rs, J, R0 + Rs>(&acc[Rs * 8], lo, hi, pmask), ...);
+}
+
+template <int K, int M, int R0, int NR, int D, bool FUSED, int J>
 __device__ __forceinline__ void syn_item(u32 (&acc)[NR * 8], u32 (&ring)[D][8], const SynCtx &c, u8 *orow0, u32 B,
                                          u32 last, bool copies, u8 *syn, u32 &q)
 {
@@ -421,26 +502,33 @@ __device__ __forceinline__ void syn_item(u32 (&acc)[NR * 8], u32 (&ring)[D][8], 
         u32 lo[16], hi[16];
         subsets(x[0], x[1], x[2], x[3], lo);
         subsets(x[4], x[5], x[6], x[7], hi);
-        block_rows<K, M, R0, J, false>(std::make_integer_sequence<int, NR * 8>{}, acc, lo, hi);
-    } else {  // parity row R0 + r: syndrome = its bytes ^ the present blocks' contribution
+        syn_rows<K, M, R0, J>(std::make_integer_sequence<int, NR>{}, acc, lo, hi, c.pmask);  // present rows only
+    } else {  // parity row R0 + r: syndrome = its planes ^ the present blocks' contribution, * w
         constexpr int r = J - K;
+        transpose8(x);
         u32 y[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-            y[i] = acc[r * 8 + i];
-        transpose8(y);
-        u8 *o = syn + (u64)q * B;
-        st16(o + c.pa, y[0] ^ x[0], y[1] ^ x[1], y[2] ^ x[2], y[3] ^ x[3]);
-        st16(o + c.pb, y[4] ^ x[4], y[5] ^ x[5], y[6] ^ x[6], y[7] ^ x[7]);
+            y[i] = acc[r * 8 + i] ^ x[i];
+        scale_planes(y, c.wmask[q]);
+        if constexpr (FUSED) {  // kept for the solve in the same wave
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                acc[r * 8 + i] = y[i];
+        } else {
+            u8 *o = syn + (u64)q * c.stride;
+            st16(o + c.ua, y[0], y[1], y[2], y[3]);
+            st16(o + c.ub, y[4], y[5], y[6], y[7]);
+        }
         ++q;
     }
 }
 
-template <int K, int M, int R0, int NR, int D, int... Js>
+template <int K, int M, int R0, int NR, int D, bool FUSED, int... Js>
 __device__ __forceinline__ void syn_items(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], u32 (&ring)[D][8],
                                           const SynCtx &c, u8 *orow0, u32 B, u32 last, bool copies, u8 *syn, u32 &q)
 {
-    (syn_item<K, M, R0, NR, D, Js>(acc, ring, c, orow0, B, last, copies, syn, q), ...);
+    (syn_item<K, M, R0, NR, D, FUSED, Js>(acc, ring, c, orow0, B, last, copies, syn, q), ...);
 }
 
 template <int K, int M, int R0, int NR, int D>
@@ -449,7 +537,8 @@ __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__re
 {
     const u32 B = d.B;
     const u32 lane = (threadIdx.x & 63) * 16;
-    SynCtx c{blocks, sl.off, sl.avail, d.slot0, min(s + lane, B - 16), min(s + 1024 + lane, B - 16), d.dmask, d.pmask};
+    SynCtx c{blocks,  sl.off,     sl.avail, sl.masks + d.wq0,     d.slot0,         min(s + lane, B - 16),
+             min(s + 1024 + lane, B - 16), s + lane, s + 1024 + lane, d.dmask, d.pmask, sec::syn_stride(B)};
     u32 ring[D][8];
     load_syn_first<K, NR, R0>(std::make_integer_sequence<int, D>{}, ring, c);
     u32 acc[NR * 8];
@@ -458,11 +547,12 @@ __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__re
         acc[i] = 0;
     // syndrome row of this group's first present parity row: the present rows below R0
     u32 q = (u32)__builtin_popcountll(d.pmask & ((1ull << R0) - 1ull));
-    syn_items<K, M, R0, NR, D>(std::make_integer_sequence<int, K + NR>{}, acc, ring, c, out + d.out_off, B, d.last,
-                               copies, syn + d.syn_off, q);
+    syn_items<K, M, R0, NR, D, false>(std::make_integer_sequence<int, K + NR>{}, acc, ring, c, out + d.out_off, B,
+                                      d.last, copies, syn + d.syn_off, q);
 }
 
-// The syndromes go to `syn`; sec_decode_kernel then solves for the lost blocks (api.cpp).
+// The scaled syndromes go to `syn` as bit planes; sec_solve_bs_kernel then solves for the lost
+// blocks.
 template <int K, int M, int NR, int D>
 __global__ __launch_bounds__(256) void sec_syndrome_bs_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                               u8 *__restrict__ syn,
@@ -484,6 +574,235 @@ __global__ __launch_bounds__(256) void sec_syndrome_bs_kernel(const u8 *__restri
             syn_span<K, M, 0, NR, D>(blocks, out, syn, d, sl, s, copies);
         else
             syn_span<K, M, NR, NR, D>(blocks, out, syn, d, sl, s, copies);
+    }
+}
+
+// ---- decode, phase 2: lost row l = z_l * XOR_{r in S} c[r][l] * (w_r s_r) ----------------------
+struct SolveCtx {
+    const u8 *syn;  // the chunk's syndrome rows
+    uint64_t stride, pmask, lost;
+    u32 ua, ub;
+};
+
+template <int J>
+__device__ __forceinline__ void load_syndrome(u32 (&x)[8], const SolveCtx &c)
+{
+    const u32 q = (u32)__builtin_popcountll(c.pmask & ((1ull << J) - 1ull));
+    const u8 *p = c.syn + (u64)q * c.stride;
+    const u32x4 a = *reinterpret_cast<const u32x4 *>(p + c.ua), b = *reinterpret_cast<const u32x4 *>(p + c.ub);
+    x[0] = a.x;
+    x[1] = a.y;
+    x[2] = a.z;
+    x[3] = a.w;
+    x[4] = b.x;
+    x[5] = b.y;
+    x[6] = b.z;
+    x[7] = b.w;
+}
+
+// parity input J's contribution c[J][R0 + r] to every lost row r of the group
+template <int K, int M, int R0, int NR, int J, int... Rs>
+__device__ __forceinline__ void solve_rows(std::integer_sequence<int, Rs...>, u32 (&acc)[NR * 8], const u32 (&lo)[16],
+                                           const u32 (&hi)[16], uint64_t lost)
+{
+    (coef_planes_skip<K, M, J, R0 + Rs>(&acc[Rs * 8], lo, hi, lost), ...);
+}
+
+template <int K, int M, int R0, int NR, int D, int J>
+__device__ __forceinline__ void solve_item(u32 (&acc)[NR * 8], u32 (&ring)[D][8], const SolveCtx &c)
+{
+    constexpr int P = M - K;
+    u32 x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        x[i] = ring[J % D][i];
+    if constexpr (J + D < P)
+        if ((c.pmask >> (J + D)) & 1)
+            load_syndrome<J + D>(ring[J % D], c);
+    if (!((c.pmask >> J) & 1))
+        return;
+    u32 lo[16], hi[16];
+    subsets(x[0], x[1], x[2], x[3], lo);
+    subsets(x[4], x[5], x[6], x[7], hi);
+    solve_rows<K, M, R0, NR, J>(std::make_integer_sequence<int, NR>{}, acc, lo, hi, c.lost);
+}
+
+template <int K, int M, int R0, int NR, int D, int... Js>
+__device__ __forceinline__ void solve_items(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], u32 (&ring)[D][8],
+                                            const SolveCtx &c)
+{
+    (solve_item<K, M, R0, NR, D, Js>(acc, ring, c), ...);
+}
+
+template <int K, int M, int R0, int NR, int D, int... Js>
+__device__ __forceinline__ void solve_first(std::integer_sequence<int, Js...>, u32 (&ring)[D][8], const SolveCtx &c)
+{
+    ((((c.pmask >> Js) & 1) ? load_syndrome<Js>(ring[Js], c) : void()), ...);
+}
+
+// Where the recovered rows go: row l (reassembly; row K-1 clamps to `last`) or the l-th lost
+// row in ascending order (recover-only) of the chunk at `out`, scaled by zmask[that rank].
+struct OutCtx {
+    u8 *out;
+    const uint64_t *zmask;
+    uint64_t lost;
+    u32 B, last, recover, pa, pb;
+};
+
+// lost row R0 + r: scale by z, transpose back, store
+template <int K, int R0, int NR, int r>
+__device__ __forceinline__ void solve_out(u32 (&acc)[NR * 8], const OutCtx &o)
+{
+    constexpr int l = R0 + r;
+    if (!((o.lost >> l) & 1))
+        return;
+    const u32 t = (u32)__builtin_popcountll(o.lost & ((1ull << l) - 1ull));
+    u32 y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        y[i] = acc[r * 8 + i];
+    scale_planes(y, o.zmask[t]);
+    transpose8(y);
+    u8 *dst = o.out + (u64)(o.recover ? t : (u32)l) * o.B;
+    if (l == K - 1 && !o.recover) {
+        st16_clamped(dst, o.pa, o.last, y[0], y[1], y[2], y[3]);
+        st16_clamped(dst, o.pb, o.last, y[4], y[5], y[6], y[7]);
+    } else {
+        st16(dst + o.pa, y[0], y[1], y[2], y[3]);
+        st16(dst + o.pb, y[4], y[5], y[6], y[7]);
+    }
+}
+
+template <int K, int R0, int NR, int... Rs>
+__device__ __forceinline__ void solve_outs(std::integer_sequence<int, Rs...>, u32 (&acc)[NR * 8], const OutCtx &o)
+{
+    (solve_out<K, R0, NR, Rs>(acc, o), ...);
+}
+
+template <int K, int M, int R0, int NR, int D>
+__device__ __forceinline__ void solve_span(const u8 *__restrict__ syn, u8 *__restrict__ out, const sec::SolveDesc &d,
+                                           const uint64_t *__restrict__ masks, u32 s)
+{
+    constexpr int P = M - K;
+    static_assert(D >= 1 && D <= P && R0 + NR <= K, "solve shape");
+    const u32 B = d.B;
+    const u32 lane = (threadIdx.x & 63) * 16;
+    const SolveCtx c{syn + d.syn_off, sec::syn_stride(B), d.pmask, d.lost, s + lane, s + 1024 + lane};
+    u32 ring[D][8];
+    solve_first<K, M, R0, NR, D>(std::make_integer_sequence<int, D>{}, ring, c);
+    u32 acc[NR * 8];
+#pragma unroll
+    for (int i = 0; i < NR * 8; ++i)
+        acc[i] = 0;
+    solve_items<K, M, R0, NR, D>(std::make_integer_sequence<int, P>{}, acc, ring, c);
+    const OutCtx o{out + d.out_off, masks + d.zq0, d.lost, B, d.last, d.recover, min(s + lane, B - 16),
+                   min(s + 1024 + lane, B - 16)};
+    solve_outs<K, R0, NR>(std::make_integer_sequence<int, NR>{}, acc, o);
+}
+
+// Tiles carry the row group's first data row in r0 (groups of NR rows).
+template <int K, int M, int NR, int D>
+__global__ __launch_bounds__(256) void sec_solve_bs_kernel(const u8 *__restrict__ syn, u8 *__restrict__ out,
+                                                           const sec::SolveDesc *__restrict__ descs,
+                                                           const sec::Tile *__restrict__ tiles,
+                                                           const uint64_t *__restrict__ masks)
+{
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::SolveDesc d = descs[tl.chunk];
+    const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
+    if (s >= d.B)
+        return;
+    static_assert(K % NR == 0 && K / NR <= 4, "row groups");
+    if (tl.r0 == 0)
+        solve_span<K, M, 0, NR, D>(syn, out, d, masks, s);
+    if constexpr (K / NR > 1)
+        if (tl.r0 == NR)
+            solve_span<K, M, NR, NR, D>(syn, out, d, masks, s);
+    if constexpr (K / NR > 2)
+        if (tl.r0 == 2 * NR)
+            solve_span<K, M, 2 * NR, NR, D>(syn, out, d, masks, s);
+    if constexpr (K / NR > 3)
+        if (tl.r0 == 3 * NR)
+            solve_span<K, M, 3 * NR, NR, D>(syn, out, d, masks, s);
+}
+
+// ---- decode, both phases in one wave (e <= 16, the present parity rows in one group) ---------
+// The scaled syndromes stay in the phase-1 accumulators (the compiler parks what does not fit
+// in the 256 VGPRs in AGPRs: one wave per SIMD), so they never go through HBM: traffic is the
+// decode's own (k blocks read, the chunk or the e rows written).
+template <int K, int M, int RP0, int NRP, int NR2, int G, int... Js>
+__device__ __forceinline__ void fused_group(std::integer_sequence<int, Js...>, const u32 (&sy)[NRP * 8],
+                                            uint64_t pmask, const OutCtx &o)
+{
+    constexpr int R0 = G * NR2;
+    if (!((o.lost >> R0) & ((1ull << NR2) - 1ull)))
+        return;
+    u32 acc[NR2 * 8];
+#pragma unroll
+    for (int i = 0; i < NR2 * 8; ++i)
+        acc[i] = 0;
+    auto one = [&](auto jc) {
+        constexpr int r = decltype(jc)::value;
+        if (!((pmask >> (RP0 + r)) & 1))
+            return;
+        u32 lo[16], hi[16];
+        subsets(sy[r * 8 + 0], sy[r * 8 + 1], sy[r * 8 + 2], sy[r * 8 + 3], lo);
+        subsets(sy[r * 8 + 4], sy[r * 8 + 5], sy[r * 8 + 6], sy[r * 8 + 7], hi);
+        solve_rows<K, M, R0, NR2, RP0 + r>(std::make_integer_sequence<int, NR2>{}, acc, lo, hi, o.lost);
+    };
+    (one(std::integral_constant<int, Js>{}), ...);
+    solve_outs<K, R0, NR2>(std::make_integer_sequence<int, NR2>{}, acc, o);
+}
+
+template <int K, int M, int RP0, int NRP, int NR2, int... Gs>
+__device__ __forceinline__ void fused_groups(std::integer_sequence<int, Gs...>, const u32 (&sy)[NRP * 8],
+                                             uint64_t pmask, const OutCtx &o)
+{
+    (fused_group<K, M, RP0, NRP, NR2, Gs>(std::make_integer_sequence<int, NRP>{}, sy, pmask, o), ...);
+}
+
+template <int K, int M, int RP0, int NRP, int NR2, int D>
+__device__ __forceinline__ void fused_span(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+                                           const sec::SynDesc &d, const sec::SynSlots &sl, u32 s, bool copies)
+{
+    const u32 B = d.B;
+    const u32 lane = (threadIdx.x & 63) * 16;
+    SynCtx c{blocks,  sl.off,     sl.avail, sl.masks + d.wq0,     d.slot0,         min(s + lane, B - 16),
+             min(s + 1024 + lane, B - 16), s + lane, s + 1024 + lane, d.dmask, d.pmask, 0};
+    u32 ring[D][8];
+    load_syn_first<K, NRP, RP0>(std::make_integer_sequence<int, D>{}, ring, c);
+    u32 acc[NRP * 8];
+#pragma unroll
+    for (int i = 0; i < NRP * 8; ++i)
+        acc[i] = 0;
+    u32 q = 0;  // every present parity row is in this group
+    syn_items<K, M, RP0, NRP, D, true>(std::make_integer_sequence<int, K + NRP>{}, acc, ring, c, out + d.out_off, B,
+                                       d.last, copies, nullptr, q);
+    const uint64_t lost = ~d.dmask & (K >= 64 ? ~0ull : (1ull << K) - 1ull);
+    const OutCtx o{out + d.out_off, sl.masks + d.zq0, lost, B, d.last, d.flags & 2u ? 1u : 0u, c.pa, c.pb};
+    fused_groups<K, M, RP0, NRP, NR2>(std::make_integer_sequence<int, K / NR2>{}, acc, d.pmask, o);
+}
+
+// Tiles: r0 = the parity group's first row; ntail bit 0 = copy the present primaries.
+template <int K, int M, int NRP, int NR2, int D>
+__global__ __launch_bounds__(256) void sec_decode_bs_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+                                                            const sec::SynDesc *__restrict__ descs,
+                                                            const sec::Tile *__restrict__ tiles, const sec::SynSlots sl)
+{
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::SynDesc d = descs[tl.chunk];
+    const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
+    if (s >= d.B)
+        return;
+    const bool copies = tl.ntail & 1;
+    if constexpr (M - K <= NRP) {
+        fused_span<K, M, 0, NRP, NR2, D>(blocks, out, d, sl, s, copies);
+    } else {
+        static_assert(M - K == 2 * NRP, "two row groups");
+        if (tl.r0 == 0)
+            fused_span<K, M, 0, NRP, NR2, D>(blocks, out, d, sl, s, copies);
+        else
+            fused_span<K, M, NRP, NRP, NR2, D>(blocks, out, d, sl, s, copies);
     }
 }
 
@@ -570,8 +889,93 @@ hipError_t launch_syn(int lanes, const u8 *blocks, u8 *out, u8 *syn, const sec::
                           (hipEvent_t)b, 0, blocks, out, syn, d, t, sl);
     return hipGetLastError();
 }
+
+// phase-2 rows per group: (10,14) 10, (8,*) 8, the rest 16
+constexpr int solve_nr(int k) { return k <= 16 ? k : 16; }
+
+template <int K, int M, int D>
+hipError_t launch_solve(int lanes, const u8 *syn, u8 *out, const sec::SolveDesc *d, const sec::Tile *t, u32 nt,
+                        const uint64_t *masks, hipStream_t s)
+{
+    void *a = nullptr, *b = nullptr;
+    sec_next_launch_events(&a, &b);
+    hipExtLaunchKernelGGL((sec_solve_bs_kernel<K, M, solve_nr(K), D>), dim3(nt), dim3(lanes), 0, s, (hipEvent_t)a,
+                          (hipEvent_t)b, 0, syn, out, d, t, masks);
+    return hipGetLastError();
+}
 }  // namespace
 
+int sec_solve_rows(int shape) { return shape >= 0 && shape < kNShapes ? solve_nr(kShapes[shape].k) : 0; }
+
+// Ring depths: the syndromes' 8-dword items, D of them in flight (SEC_SOLVE_RING, build knob;
+// 4 against 2: +2-7 % on the two-kernel decodes, r03_syn_ab.jsonl)
+#ifndef SEC_SOLVE_RING
+#define SEC_SOLVE_RING 4
+#endif
+int sec_launch_solve_bs(int shape, int lanes, const uint8_t *syn, uint8_t *out, const sec::SolveDesc *descs,
+                        const sec::Tile *t, uint32_t ntiles, const uint64_t *masks, void *stream)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    if (lanes < 64 || lanes > 256 || lanes % 64)
+        return hipErrorInvalidValue;
+    hipStream_t s = (hipStream_t)stream;
+    constexpr int R = SEC_SOLVE_RING;
+    switch (shape) {
+    case 0: return launch_solve<10, 14, R < 4 ? R : 4>(lanes, syn, out, descs, t, ntiles, masks, s);
+    case 1: return launch_solve<8, 12, R < 4 ? R : 4>(lanes, syn, out, descs, t, ntiles, masks, s);
+    case 2: return launch_solve<16, 24, R>(lanes, syn, out, descs, t, ntiles, masks, s);
+    case 3: return launch_solve<32, 48, R>(lanes, syn, out, descs, t, ntiles, masks, s);
+    case 4: return launch_solve<64, 96, R>(lanes, syn, out, descs, t, ntiles, masks, s);
+    case 5: return launch_solve<8, 11, R < 3 ? R : 3>(lanes, syn, out, descs, t, ntiles, masks, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+namespace {
+// solve rows per group in the one-wave kernel: 8 (16 cost 282 VGPRs = one wave per SIMD, and a
+// lone wave leaves the memory pipe idle while it solves: 0.8x the two-kernel path; 8 rows: 224)
+constexpr int fused_nr(int k) { return k <= 10 ? k : 8; }
+
+template <int K, int M, int NRP, int D>
+hipError_t launch_fused(int lanes, const u8 *blocks, u8 *out, const sec::SynDesc *d, const sec::Tile *t, u32 nt,
+                        sec::SynSlots sl, hipStream_t s)
+{
+    void *a = nullptr, *b = nullptr;
+    sec_next_launch_events(&a, &b);
+    hipExtLaunchKernelGGL((sec_decode_bs_kernel<K, M, NRP, fused_nr(K), D>), dim3(nt), dim3(lanes), 0, s,
+                          (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, d, t, sl);
+    return hipGetLastError();
+}
+}  // namespace
+
+// fused kernel ring (SEC_FUSED_RING, build knob): 6 against 4 +0-4 % (r03_syn_ab.jsonl)
+#ifndef SEC_FUSED_RING
+#define SEC_FUSED_RING 6
+#endif
+int sec_launch_decode_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, const sec::SynDesc *descs,
+                         const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    if (lanes < 64 || lanes > 256 || lanes % 64)
+        return hipErrorInvalidValue;
+    hipStream_t s = (hipStream_t)stream;
+    constexpr int R = SEC_FUSED_RING;
+    switch (shape) {
+    case 0: return launch_fused<10, 14, 4, R>(lanes, blocks, out, descs, t, ntiles, sl, s);
+    case 1: return launch_fused<8, 12, 4, R>(lanes, blocks, out, descs, t, ntiles, sl, s);
+    case 2: return launch_fused<16, 24, 8, R>(lanes, blocks, out, descs, t, ntiles, sl, s);
+    case 3: return launch_fused<32, 48, 16, R>(lanes, blocks, out, descs, t, ntiles, sl, s);
+    case 4: return launch_fused<64, 96, 16, R>(lanes, blocks, out, descs, t, ntiles, sl, s);
+    case 5: return launch_fused<8, 11, 3, R>(lanes, blocks, out, descs, t, ntiles, sl, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+#ifndef SEC_SYN_RING
+#define SEC_SYN_RING 4
+#endif
 int sec_syn_shape(int k, int m)
 {
     const int sh = sec_bs_shape(k, m);
@@ -587,12 +991,13 @@ int sec_launch_syndrome_bs(int shape, int lanes, const uint8_t *blocks, uint8_t 
     if (lanes < 64 || lanes > 256 || lanes % 64)
         return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
-    switch (shape) {  // ring depths as the encode's (kernels' register budgets are alike)
+    switch (shape) {  // ring depths as the encode's (kernels' register budgets are alike); the
+                      // 16-row groups' SEC_SYN_RING (build knob, A/B)
     case 0: return launch_syn<10, 14, 4, RING_K(10, 5)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
     case 1: return launch_syn<8, 12, 4, RING_K(8, 4)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
     case 2: return launch_syn<16, 24, 8, RING_K(16, 10)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
-    case 3: return launch_syn<32, 48, 16, RING_K(32, 2)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
-    case 4: return launch_syn<64, 96, 16, RING_K(64, 2)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 3: return launch_syn<32, 48, 16, SEC_SYN_RING>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 4: return launch_syn<64, 96, 16, SEC_SYN_RING>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
     case 5: return launch_syn<8, 11, 3, RING_K(8, 4)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
     default: return hipErrorInvalidValue;
     }

@@ -1,8 +1,9 @@
 """GPU parity of the syndrome decode (wide decodes with many lost data blocks).
 
 A chunk that lost e data blocks and holds e parity rows instead is decoded in two phases
-(kernels_bs.hip sec_syndrome_bs_kernel: bit-sliced syndromes of the present parity rows and the
-copies of the present primaries; then sec_decode_kernel applies the e x e inverse).  The result
+(kernels_bs.hip sec_syndrome_bs_kernel: bit-sliced syndromes of the present parity rows, scaled
+by the Cauchy solve's w, and the copies of the present primaries; then sec_solve_bs_kernel
+applies the transposed parity matrix and the scaling z, gf_host.hpp cauchy_scales).  The result
 must be zfec's fec_decode bytes (/root/reference/storb/util/piece.py:196-197 via easyfec),
 checked here against the source chunk (every chunk) and the oracle's padded blocks
 (oracle/fec_oracle.c) for:
@@ -33,10 +34,10 @@ from storb_amd._lib import DEC_DTYPE, ENC_DTYPE  # noqa: E402
 SHAPES = [(16, 24), (32, 48), (64, 96), (10, 14), (8, 12), (8, 11)]
 
 
-def _engine(monkeypatch, syn):
+def _engine(monkeypatch, syn, fused=None):
     from storb_amd.engine import Engine
 
-    for var, val in (("SEC_SYN", syn),):
+    for var, val in (("SEC_SYN", syn), ("SEC_SYN_FUSED", fused)):
         if val is None:
             monkeypatch.delenv(var, raising=False)
         else:
@@ -142,13 +143,15 @@ def _run(eng, k, m, cases, recover=False, host=None, check_oracle=3):
 
 @pytest.mark.parametrize("k,m", SHAPES)
 @pytest.mark.parametrize("recover", [False, True])
-def test_syndrome_decode_forced_device(k, m, recover, monkeypatch):
-    """SEC_SYN=1: every chunk on the syndrome path."""
+@pytest.mark.parametrize("fused", [None, "0"])
+def test_syndrome_decode_forced_device(k, m, recover, fused, monkeypatch):
+    """SEC_SYN=1: every chunk on the syndrome path (the one-wave kernel where it applies, or with
+    SEC_SYN_FUSED=0 always the two kernels with the syndromes in HBM)."""
     rng = random.Random(k * 1000 + m + recover)
     sizes = [16 * k, 17 * k - 3, 2048 * k + 5 * k, 6554 * k - 4 if k == 10 else 4099 * k - 1, 65536 * k,
              rng.randrange(20000, 300000)]
     sizes = [n for n in sizes if -(-n // k) * (k - 1) < n]  # easyfec: the last block not empty
-    eng = _engine(monkeypatch, "1")
+    eng = _engine(monkeypatch, "1", fused)
     try:
         cases = _cases(rng, k, m, sizes)
         _run(eng, k, m, cases, recover=recover)
@@ -174,8 +177,8 @@ def test_syndrome_decode_forced_host(k, m, host, monkeypatch):
 
 def test_syndrome_default_rule_and_off_give_same_bytes(monkeypatch):
     """The default choice (api.cpp syn_choice's estimate) on the verdict's case: zfec(64,96) with
-    16 data blocks lost takes the syndrome path, one lost block the direct path; SEC_SYN=0
-    decodes the same chunks directly, to the same bytes."""
+    16 data blocks lost (parity rows of one group) takes the syndrome path, one lost block the
+    direct path; SEC_SYN=0 decodes the same chunks directly, to the same bytes."""
     many = [(1 << 20, list(range(16, 64)) + list(range(64, 80)))]  # 16 lost, parity group 0
     one = [(1 << 20, list(range(1, 64)) + [95])]
     for syn_env, want_many, want_one in ((None, (1, 0), (0, 1)), ("0", (0, 1), (0, 1))):
@@ -235,6 +238,28 @@ def test_syndrome_mixed_batch_with_direct_chunks(monkeypatch):
                          block_avail=np.array(av, np.uint64))
         assert torch.equal(out, src)
         syn, direct = eng.decode_paths()
-        assert syn >= 6 and syn + direct == 24, (syn, direct)  # the (64,96) chunks take the syndrome path
+        # the (32,48) chunks (12 lost, parity rows of one group) take the one-wave syndrome kernel;
+        # the (64,96) ones (20 lost, parity rows of both groups) stay direct or take two kernels
+        assert syn >= 6 and syn + direct == 24, (syn, direct)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("k,m,e,fused", [(64, 96, 32, "0"), (64, 96, 24, None), (32, 48, 12, None), (16, 24, 6, None)])
+def test_syndrome_random_patterns(k, m, e, fused, monkeypatch):
+    """Random lost data blocks and random present parity rows (both parity groups of (64,96)),
+    forced onto the syndrome path, reassembled and recover-only, against the sources."""
+    rng = random.Random(1000 * k + e)
+    eng = _engine(monkeypatch, "1", fused)
+    try:
+        cases = []
+        for n in (rng.randrange(4096 * k, 40000 * k), 1 << 20, 64 * k - 3):
+            lost = rng.sample(range(k), e)
+            keep = [j for j in range(k) if j not in lost] + rng.sample(range(k, m), e)
+            rng.shuffle(keep)
+            cases.append((n, keep))
+        _run(eng, k, m, cases)
+        _run(eng, k, m, cases, recover=True)
+        assert eng.decode_paths() == (2 * len(cases), 0)
     finally:
         eng.close()

@@ -31,7 +31,26 @@ CASES = [
     ("zfec(16,24) 8MiB x128, 8 lost (every parity row)", 16, 24, 8 << 20, 128, 8),
     ("zfec(16,24) 8MiB x128, 4 lost", 16, 24, 8 << 20, 128, 4),
     ("C4 zfec(10,14) 64KiB x8192, 4 lost", 10, 14, 65536, 8192, 4),
+    # random lost data blocks and random present parity rows (seeded): what retrievals see
+    ("zfec(64,96) 1MiB x1024, 16 lost (random, parity random)", 64, 96, 1 << 20, 1024, 16, 1),
+    ("zfec(64,96) 1MiB x1024, 24 lost (random, parity random)", 64, 96, 1 << 20, 1024, 24, 2),
+    ("zfec(32,48) 1MiB x1024, 12 lost (random, parity random)", 32, 48, 1 << 20, 1024, 12, 3),
+    ("zfec(32,48) 1MiB x1024, 16 lost (random)", 32, 48, 1 << 20, 1024, 16, 4),
 ]
+
+
+def erased_of(k, m, e, seed):
+    """The erased block numbers: e data blocks and m - k - e parity rows, both random (seed), or
+    (seed 0) every other data block from 0 and the last parity rows."""
+    import random
+
+    if not seed:
+        lost = tuple(range(0, 2 * e, 2)) if 2 * e <= k else tuple(range(e))
+        return lost, lost
+    rng = random.Random(seed)
+    lost = tuple(sorted(rng.sample(range(k), e)))
+    keep_par = set(rng.sample(range(k, m), e))
+    return lost, lost + tuple(r for r in range(k, m) if r not in keep_par)
 
 
 def main():
@@ -55,17 +74,17 @@ def main():
         lib = os.path.join(ROOT, "storb_amd", "lib", f"libstorbec_{tag}.so") if tag else None
         variants.append((name, dict(kv.split("=") for kv in env.split("+")) if env else {}, lib))
     sel = [c for c in CASES if not a.cases or any(t in c[0] for t in a.cases.split(","))]
-    for name, k, m, n, nch, e in sel:
+    for name, k, m, n, nch, e, *seed in sel:
         src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
         B = -(-n // k)
         ed, _ = bench.enc_descs(nch, n, k, m)
         par = torch.empty(nch * (m - k) * B, dtype=torch.uint8, device="cuda")
-        lost = tuple(range(0, 2 * e, 2)) if 2 * e <= k else tuple(range(e))
+        lost, erased = erased_of(k, m, e, seed[0] if seed else 0)
         eng0 = Engine(0)
         eng0.encode_batch(ed, src, par)
         eng0.close()
-        dd, sn, offs, av = bench.dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), lost)
-        rd, rsn, roffs, rav = bench.dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), lost, recover=True)
+        dd, sn, offs, av = bench.dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), erased)
+        rd, rsn, roffs, rav = bench.dec_descs(nch, n, k, m, B, src.data_ptr(), par.data_ptr(), erased, recover=True)
         out = torch.empty_like(src)
         rec = torch.empty(nch * e * B, dtype=torch.uint8, device="cuda")
         res = {v[0]: {"reassemble": [], "recover_only": []} for v in variants}
@@ -105,7 +124,8 @@ def main():
                             os.environ.pop(key, None)
                         else:
                             os.environ[key] = val
-        row = {"case": name, "k": k, "m": m, "chunk": n, "chunks": nch, "lost": list(lost)}
+        row = {"case": name, "k": k, "m": m, "chunk": n, "chunks": nch, "lost": list(lost),
+               "parity_kept": [s for s in sn[:k].tolist() if s >= k]}
         for vname, r in res.items():
             row[vname] = {mode: round(float(np.median(v)), 3) for mode, v in r.items()}
             row[vname]["paths(syn,direct)"] = paths.get(vname)
