@@ -1858,7 +1858,7 @@ public:
 
     // 0: staged; 1: every range in persistently pinned memory (zero-copy, nothing locked);
     // 2: zero-copy on pages this call locked (plus persistently pinned ones)
-    int acquire(const std::vector<HostRange> &rs)
+    int acquire(const std::vector<HostRange> &rs, bool may_lock = true)
     {
         TransientLocks &tl = transient_locks();
         std::lock_guard<std::mutex> g(tl.mu);
@@ -1876,7 +1876,7 @@ public:
         }
         if (pg.empty())
             return 1;
-        if (getenv_zero("SEC_REGISTER_MIN") || total < env_size("SEC_REGISTER_MIN", (size_t)4 << 20))
+        if (!may_lock || getenv_zero("SEC_REGISTER_MIN") || total < env_size("SEC_REGISTER_MIN", (size_t)4 << 20))
             return 0;
         std::sort(pg.begin(), pg.end());
         // ranges less than kGap apart are locked as one (e.g. around a decode's erased blocks);
@@ -1948,9 +1948,9 @@ private:
 
 // Decides a host call's path: zero-copy on the caller's pinned buffers, zero-copy on pages
 // locked for the call (`lock`), or staged.  True = run the device path on host addresses.
-bool host_direct(sec_ctx *ctx, const std::vector<HostRange> &rs, HostLock &lock)
+bool host_direct(sec_ctx *ctx, const std::vector<HostRange> &rs, HostLock &lock, unsigned flags)
 {
-    switch (lock.acquire(rs)) {
+    switch (lock.acquire(rs, !(flags & SEC_F_STAGED))) {
     case 1: ++ctx->zero_copy_calls; return true;
     case 2: ++ctx->registered_calls; return true;
     default: ++ctx->staged_calls; return false;
@@ -1961,7 +1961,8 @@ bool host_direct(sec_ctx *ctx, const std::vector<HostRange> &rs, HostLock &lock)
 int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in, uint8_t *parity,
                 uint8_t *digests, unsigned flags, bool digest)
 {
-    if (!ctx || nchunks < 0 || (nchunks > 0 && !chunks) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC)))
+    if (!ctx || nchunks < 0 || (nchunks > 0 && !chunks) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC | SEC_F_STAGED)) ||
+        ((flags & SEC_F_STAGED) && !(flags & SEC_F_HOST)))
         return SEC_EINVAL;
     if (nchunks == 0)
         return SEC_OK;
@@ -1995,7 +1996,7 @@ int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, cons
     // as every host call).  Digest mode keeps the staged path: SHA-1 is one latency-bound lane
     // per piece, which would stall on every PCIe read.
     HostLock lock(ctx->stream());
-    if (host && !digest && host_direct(ctx, encode_ranges(chunks, nchunks, in, parity), lock)) {
+    if (host && !digest && host_direct(ctx, encode_ranges(chunks, nchunks, in, parity), lock, flags)) {
         host = false;
         flags &= ~(SEC_F_HOST | SEC_F_ASYNC);
     } else if (host && digest) {
@@ -2018,7 +2019,8 @@ int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, cons
         key.resize(sizeof(sec_enc_chunk) * (size_t)nchunks);
         memcpy(key.data(), chunks, sizeof(sec_enc_chunk) * (size_t)nchunks);
     }
-    const unsigned kflags = (flags & ~SEC_F_ASYNC) | (digest ? 0x10000u : 0u);  // ASYNC does not change the plan
+    // ASYNC and STAGED do not change the plan
+    const unsigned kflags = (flags & ~(SEC_F_ASYNC | SEC_F_STAGED)) | (digest ? 0x10000u : 0u);
     key.insert(key.end(), (const uint8_t *)&kflags, (const uint8_t *)&kflags + sizeof(unsigned));
     if (!(plan.valid && plan.gen == ctx->enc_tabs.gen && plan.key == key)) {
         plan.valid = false;
@@ -2395,7 +2397,8 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
                         unsigned flags)
 {
     if (!ctx || nchunks < 0 || (nchunks > 0 && (!chunks || !sharenums || !block_offs)) ||
-        (flags & ~(SEC_F_HOST | SEC_F_ASYNC | SEC_F_RECOVER)))
+        (flags & ~(SEC_F_HOST | SEC_F_ASYNC | SEC_F_RECOVER | SEC_F_STAGED)) ||
+        ((flags & SEC_F_STAGED) && !(flags & SEC_F_HOST)))
         return SEC_EINVAL;
     if (nchunks == 0)
         return SEC_OK;
@@ -2434,7 +2437,7 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
     bool direct = false;
     if (host &&
         host_direct(ctx, decode_ranges(chunks, nchunks, sharenums, block_offs, block_avail, blocks, out, recover),
-                    lock)) {
+                    lock, flags)) {
         host = false;
         direct = true;
         flags &= ~(SEC_F_HOST | SEC_F_ASYNC);
@@ -2492,7 +2495,7 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
     }
     // ASYNC does not change the plan; whether an avail array came does (0x10000), and how a
     // joining call runs the kernels (recover 0x4 / nocopy 0x20000)
-    const unsigned kflags = (flags & ~SEC_F_ASYNC) | (!host && block_avail ? 0x10000u : 0u) |
+    const unsigned kflags = (flags & ~(SEC_F_ASYNC | SEC_F_STAGED)) | (!host && block_avail ? 0x10000u : 0u) |
                             (prec ? SEC_F_RECOVER : 0u) | (nocopy ? 0x20000u : 0u);
     key.insert(key.end(), (const uint8_t *)&kflags, (const uint8_t *)&kflags + sizeof(unsigned));
     const bool reuse = plan.valid && plan.gen == ctx->dec_tabs.gen && plan.key == key;

@@ -22,7 +22,7 @@ import weakref
 import numpy as np
 
 from . import _lib
-from ._lib import DEC_DTYPE, ENC_DTYPE, MSG_DTYPE, SEC_F_ASYNC, SEC_F_HOST, SEC_F_RECOVER
+from ._lib import DEC_DTYPE, ENC_DTYPE, MSG_DTYPE, SEC_F_ASYNC, SEC_F_HOST, SEC_F_RECOVER, SEC_F_STAGED
 
 
 class Error(Exception):
@@ -126,19 +126,23 @@ class Engine:
         return ms.value, n.value
 
     # -- device-resident batches --------------------------------------------
-    def encode_batch(self, descs: np.ndarray, src, parity, *, host: bool = False, asynchronous: bool = False) -> None:
+    def encode_batch(self, descs: np.ndarray, src, parity, *, host: bool = False, asynchronous: bool = False,
+                     staged: bool = False) -> None:
+        """sec_encode_batch.  staged (host only): never page-lock pageable buffers for the call
+        (SEC_F_STAGED), for callers whose other threads fault in memory meanwhile."""
         descs = np.ascontiguousarray(descs, dtype=ENC_DTYPE)
         s, _ks = addr(src)
         p, _kp = addr(parity)
-        flags = (SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0)
+        flags = (SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0) | (SEC_F_STAGED if staged else 0)
         self._check(self.lib.sec_encode_batch(self._ctx, _ptr(descs), len(descs), s or None, p or None, flags))
 
     def decode_batch(self, descs: np.ndarray, sharenums: np.ndarray, block_offs: np.ndarray, blocks, out, *,
                      block_avail: np.ndarray | None = None, recover_only: bool = False, host: bool = False,
-                     asynchronous: bool = False) -> None:
+                     asynchronous: bool = False, staged: bool = False) -> None:
         """sec_decode_batch_ex.  block_avail (per slot, optional): bytes of the block that exist,
         the rest read as zero (zfec's padded last data block read in place: B - padlen).
-        recover_only: write just the missing primaries (SEC_F_RECOVER), e*B bytes per chunk."""
+        recover_only: write just the missing primaries (SEC_F_RECOVER), e*B bytes per chunk.
+        staged: as encode_batch."""
         descs = np.ascontiguousarray(descs, dtype=DEC_DTYPE)
         sn = np.ascontiguousarray(sharenums, dtype=np.int32)
         bo = np.ascontiguousarray(block_offs, dtype=np.uint64)
@@ -148,7 +152,7 @@ class Engine:
         b, _kb = addr(blocks)
         o, _ko = addr(out)
         flags = ((SEC_F_HOST if host else 0) | (SEC_F_ASYNC if asynchronous else 0) |
-                 (SEC_F_RECOVER if recover_only else 0))
+                 (SEC_F_RECOVER if recover_only else 0) | (SEC_F_STAGED if staged else 0))
         self._check(self.lib.sec_decode_batch_ex(self._ctx, _ptr(descs), len(descs), _ptr(sn), _ptr(bo),
                                                  None if av is None else _ptr(av), b or None, o or None, flags))
 
@@ -234,12 +238,13 @@ class Engine:
         mv = memoryview(out)
         return [bytes(mv[20 * i:20 * (i + 1)]) for i in range(len(datas))]
 
-    def encode_host_raw(self, chunks, shapes, digests: bool = False):
+    def encode_host_raw(self, chunks, shapes, digests: bool = False, staged: bool = False):
         """``encode_host`` without the per-block ``bytes``: returns (buf, layout) where buf is
         this engine's pinned result scratch and layout[i] = (offset, B, m - k) of chunk i's
         parity blocks in it, back to back.  buf is reused by the engine's next call.  With
         ``digests=True``: (buf, layout, dig), dig = the SHA-1 of every chunk's m blocks in order,
-        20 bytes each (GPU-computed after the encode, sec_encode_digest_batch)."""
+        20 bytes each (GPU-computed after the encode, sec_encode_digest_batch).  staged: as
+        encode_batch."""
         n = len(chunks)
         descs = np.zeros(n, dtype=ENC_DTYPE)
         keep = []
@@ -260,7 +265,7 @@ class Engine:
                 self.encode_digest_batch(descs, 0, out, dig, host=True)
             return out, layout, dig
         if n:
-            self.encode_batch(descs, 0, out, host=True)
+            self.encode_batch(descs, 0, out, host=True, staged=staged)
         return out, layout
 
     def encode_host(self, chunks, shapes, digests: bool = False):

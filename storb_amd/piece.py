@@ -115,14 +115,31 @@ class EncodedPieces(BaseModel):  # piece.py:50-51
 
 _pools: dict = {}
 _pools_lock = threading.Lock()
-HASH_WORKERS = 16  # at most this many hash-pool threads (piece copies and hashlib SHA-1)
+# at most this many hash-pool threads (piece copies and hashlib SHA-1); STORB_HASH_WORKERS overrides
+HASH_WORKERS = int(os.environ.get("STORB_HASH_WORKERS", "16") or 16)
+
+
+def _cgroup_cpus() -> int | None:
+    """The CPU quota of this process's cgroup (cgroup v2 cpu.max "quota period"), rounded up, or
+    None when unlimited or unknown: a container's CPU share is often a quota, not an affinity
+    mask, and threads beyond it are throttled rather than run."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota == "max":
+            return None
+        return max(1, -(-int(quota) // int(period)))
+    except (OSError, ValueError):
+        return None
 
 
 def _usable_cpus() -> int:
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 2
+        n = os.cpu_count() or 2
+    q = _cgroup_cpus()
+    return min(n, q) if q else n
 
 
 def _pool(name: str) -> ThreadPoolExecutor:
@@ -131,7 +148,9 @@ def _pool(name: str) -> ThreadPoolExecutor:
     with _pools_lock:
         p = _pools.get(name)
         if p is None:
-            n = 1 if name.startswith("stream") else max(1, min(HASH_WORKERS, _usable_cpus() - 1))
+            # half the CPUs: SHA-1 on 8 threads of a 16-CPU quota ran at 15.3 GB/s, on 16 at 14.1, and
+            # the per-chunk upload at 4.9 against 3.4 GiB/s (r03_upload_ab.jsonl)
+            n = 1 if name.startswith("stream") else max(1, min(HASH_WORKERS, _usable_cpus() // 2))
             p = _pools[name] = ThreadPoolExecutor(n, thread_name_prefix=f"storb_amd_{name}")
         return p
 
@@ -384,7 +403,11 @@ def _pieces_parallel(chunks: list, shapes: list, digests: bool = False, hash_ids
         out.append(ps)
         if hash_ids:  # queued behind this chunk's data fills (FIFO), so they never wait long
             hfut.append([hp.submit(_hash_filled, f, v) for f, v in zip(jobs[-k:], views)])
-    res = get_engine().encode_host_raw(list(chunks), [(k, m) for (k, m, _, _) in shapes], digests=digests)
+    # staged, not page-locked: the pool is faulting in the new pieces meanwhile, and locking
+    # waits on the same memory-map lock (6.4 against 0.55 ms for one 8 MiB chunk on MI355X,
+    # profiles/r03_upload_ab.jsonl)
+    res = get_engine().encode_host_raw(list(chunks), [(k, m) for (k, m, _, _) in shapes], digests=digests,
+                                       staged=True)
     buf, layout = res[0], res[1]
     for i, (ps, (o, B, p)) in enumerate(zip(out, layout)):
         pj = []

@@ -387,6 +387,43 @@ def test_zero_copy_pinned_buffers_and_host_rewrites():
         eng.close()
 
 
+def test_staged_flag_never_locks():
+    """SEC_F_STAGED (engine staged=True): a large pageable call that would be page-locked is
+    staged instead, pinned buffers stay zero-copy, the bytes are the same; the flag without
+    SEC_F_HOST is rejected."""
+    from storb_amd import _lib
+    from storb_amd.engine import Engine
+
+    eng = Engine(0)
+    try:
+        nch, n, k, m = 8, (1 << 20) + 11, 16, 24  # 8 MiB of pageable input: above SEC_REGISTER_MIN
+        B = -(-n // k)
+        d = _enc_descs(nch, n, k, m)[0]
+        rng = np.random.default_rng(41)
+        src = rng.integers(0, 256, nch * n, dtype=np.uint8)
+        par_locked = np.zeros(nch * (m - k) * B, np.uint8)
+        par_staged = np.zeros_like(par_locked)
+        z0, r0, s0 = eng.host_paths()
+        eng.encode_batch(d, src, par_locked, host=True)
+        z1, r1, s1 = eng.host_paths()
+        eng.encode_batch(d, src, par_staged, host=True, staged=True)
+        z2, r2, s2 = eng.host_paths()
+        assert (z2 - z1, r2 - r1, s2 - s1) == (0, 0, 1), ((z0, r0, s0), (z1, r1, s1), (z2, r2, s2))
+        assert np.array_equal(par_locked, par_staged)
+        want = oracle_parity(src[:n].tobytes(), k, m)
+        assert par_staged[:(m - k) * B].tobytes() == b"".join(want)
+        hin, hpar = eng.host_empty(nch * n), eng.host_empty(par_locked.size)
+        hin[:] = src
+        eng.encode_batch(d, hin, hpar, host=True, staged=True)  # pinned: still zero-copy
+        assert eng.host_paths()[0] == z2 + 1 and np.array_equal(hpar, par_locked)
+        dev = torch.zeros(16, dtype=torch.uint8, device="cuda")
+        rc = eng.lib.sec_encode_batch(eng._ctx, d.ctypes.data, 1, dev.data_ptr(), dev.data_ptr(),
+                                      _lib.SEC_F_STAGED)
+        assert rc == _lib.SEC_EINVAL
+    finally:
+        eng.close()
+
+
 def test_registered_buffer_host_path():
     """sec_host_register on an existing numpy buffer: results are exact whichever path the
     runtime's mapping allows (zero-copy needs device address == host address)."""

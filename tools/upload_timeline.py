@@ -64,7 +64,9 @@ def main():
     print(json.dumps({"unit": "ms from the call's start, median", "chunk_bytes": cs, "k": k, "m": m, "B": B,
                       "chunks": len(rows), **med,
                       "GiB_per_s": round(cs / (med["hash_done"] / 1e3) / 2**30, 3),
-                      "cpus": len(os.sched_getaffinity(0)), "hash_threads": piece._usable_cpus()}))
+                      "cpus": piece._usable_cpus(), "hash_workers": piece.HASH_WORKERS,
+                      "pool_threads": piece._pool("hash")._max_workers,
+                      "SEC_REGISTER_MIN": os.environ.get("SEC_REGISTER_MIN", "")}))
 
 
 if __name__ == "__main__":
