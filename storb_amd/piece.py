@@ -414,10 +414,13 @@ def _pieces_parallel(chunks: list, shapes: list, digests: bool = False, hash_ids
         for r in range(p):
             b, v = _new_bytes(B)
             ps.append(b)
-            jobs.append(hp.submit(_fill, v, buf[o + r * B:o + (r + 1) * B]))
-            pj.append((jobs[-1], v))
-        if hash_ids:
-            hfut[i].extend(hp.submit(_hash_filled, f, v) for f, v in pj)
+            if hash_ids:  # the pool's queue holds the data pieces' hashes: the caller, idle
+                # until its pieces exist, copies the parity itself (r03_upload_timeline.json)
+                _fill(v, buf[o + r * B:o + (r + 1) * B])
+                hfut[i].append(hp.submit(_sha1_hex, v))
+            else:
+                jobs.append(hp.submit(_fill, v, buf[o + r * B:o + (r + 1) * B]))
+                pj.append((jobs[-1], v))
     ids = None
     if digests:
         hx, ids, f = res[2].tobytes().hex(), [], 0
