@@ -73,7 +73,7 @@ def main():
         name, _, env = v.partition("@")
         lib = os.path.join(ROOT, "storb_amd", "lib", f"libstorbec_{tag}.so") if tag else None
         variants.append((name, dict(kv.split("=") for kv in env.split("+")) if env else {}, lib))
-    sel = [c for c in CASES if not a.cases or any(t in c[0] for t in a.cases.split(","))]
+    sel = [c for c in CASES if not a.cases or any(t in c[0] for t in a.cases.split(";"))]
     for name, k, m, n, nch, e, *seed in sel:
         src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
         B = -(-n // k)
