@@ -137,10 +137,6 @@ __device__ __forceinline__ void st16(u8 *p, u32 a, u32 b, u32 c, u32 d)
     __builtin_nontemporal_store(u32x4{a, b, c, d}, reinterpret_cast<u32x4_u *>(p));
 }
 
-#ifndef SEC_BS_SKIP_DUP
-#define SEC_BS_SKIP_DUP 0
-#endif
-
 // acc (= or ^=) the output plane whose input mask is MSK
 template <u32 MSK, bool FIRST>
 __device__ __forceinline__ void upd(u32 &acc, const u32 (&lo)[16], const u32 (&hi)[16])
@@ -274,12 +270,10 @@ __device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restric
             y[i] = acc[r * 8 + i];
         transpose8(y);
         u8 *o = dst + (u64)(R0 + r) * d.par_stride;
-        // SEC_BS_SKIP_DUP (build knob, A/B): a piece whose unclamped start is past B only
-        // repeats the store of the piece clamped to B - 16; skip it
-        if (!SEC_BS_SKIP_DUP || s + lane < B)
-            st16(o + pa, y[0], y[1], y[2], y[3]);
-        if (!SEC_BS_SKIP_DUP || s + 1024 + lane < B)
-            st16(o + pb, y[4], y[5], y[6], y[7]);
+        // (pieces clamped to B - 16 repeat a neighbour's store; skipping them measured neutral on
+        // C4, r03_c4_skip_dup_ab.jsonl)
+        st16(o + pa, y[0], y[1], y[2], y[3]);
+        st16(o + pb, y[4], y[5], y[6], y[7]);
     }
 }
 

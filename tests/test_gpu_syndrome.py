@@ -245,10 +245,12 @@ def test_syndrome_mixed_batch_with_direct_chunks(monkeypatch):
         eng.close()
 
 
-@pytest.mark.parametrize("k,m,e,fused", [(64, 96, 32, "0"), (64, 96, 24, None), (32, 48, 12, None), (16, 24, 6, None)])
+@pytest.mark.parametrize("k,m,e,fused", [(64, 96, 32, "0"), (64, 96, 24, None), (64, 96, 16, None), (64, 96, 9, None),
+                                         (64, 96, 16, "0"), (32, 48, 12, None), (16, 24, 6, None)])
 def test_syndrome_random_patterns(k, m, e, fused, monkeypatch):
-    """Random lost data blocks and random present parity rows (both parity groups of (64,96)),
-    forced onto the syndrome path, reassembled and recover-only, against the sources."""
+    """Random lost data blocks and random present parity rows (both parity groups of (64,96): the
+    two kernels), forced onto the syndrome path, reassembled and recover-only, against the
+    sources."""
     rng = random.Random(1000 * k + e)
     eng = _engine(monkeypatch, "1", fused)
     try:

@@ -75,7 +75,6 @@ VARIANTS = {
     "bsr16": {"SEC_BS_RING": 16},
     "bsld": {"SEC_BS_NT_LOAD": 0},  # bit-sliced encode with cached (not streaming) loads
     "bsw3": {"SEC_BS_WAVES": 3},  # bit-sliced encode capped for 3 waves per SIMD
-    "bsdup": {"SEC_BS_SKIP_DUP": 1},
     # syndrome decode ring depths: phase 1 of the 16-row groups, phase 2 (solve), the fused kernel
     "synr4": {"SEC_SYN_RING": 4, "SEC_SOLVE_RING": 4},
     "fr2": {"SEC_FUSED_RING": 2},
