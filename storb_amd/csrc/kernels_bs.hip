@@ -535,24 +535,182 @@ __device__ __forceinline__ void syn_items(std::integer_sequence<int, Js...>, u32
     (syn_item<K, M, R0, NR, D, FUSED, Js>(acc, ring, c, orow0, B, last, copies, syn, q), ...);
 }
 
+// ---- phase 1's loads for k >= 32: an LDS ring filled by global_load_lds (no VGPRs) ----------
+// SEC_FUSED_LDS (build knob): phase 1's blocks stream through a per-wave LDS ring of D slots
+// (two 1 KiB halves each, one global_load_lds_dwordx4 per half: lane l's 16 bytes land at
+// slot + 16 l), so D blocks are in flight without ring registers.  Every item issues its two
+// loads, an absent one from the chunk's first present data block (just read: an L2 hit), so
+// the loads issued after an item's are a compile-time count N and the wait for it is a plain
+// `s_waitcnt vmcnt(N)`: loads complete in order, so at most N outstanding retires it whatever
+// stores are in flight (a run-time count needs a branch per wait, which cost 80 VGPRs).  Data
+// block K-1 (possibly short, read in place) keeps the register path and is not counted
+// (waiting for fewer loads is stricter).  Used for k >= 32 (zfec(32,48), (64,96)), where it
+// measured +0-5 % reassembling and +7-16 % recover-only over the register ring; the small-k
+// shapes keep the register ring (LDS ring -8 % on (32,48) with 8 lost, -9 % (16,24), -20 % C4;
+// the direct decode is chosen there anyway), r03_syn_ab_lds.jsonl.
+#ifndef SEC_FUSED_LDS
+#define SEC_FUSED_LDS 1
+#endif
+#ifndef SEC_FUSED_LDS_RING
+#define SEC_FUSED_LDS_RING 8
+#endif
+
+template <int D>
+struct LdsRing {
+    u32x4 v[4][D][2][64];  // [wave of a 256-lane workgroup][slot][half][lane]
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm()
+{
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// Item addresses, one per lane (lane t: item t in `a`, item 64 + t in `b`), read with a
+// compile-time readlane: a per-item load of the slot table would be a vector load whose wait
+// drains every DMA in flight (the table is not provably unwritten, so it is no scalar load).
+struct ItemAddrs {
+    u64 a, b;
+};
+
+template <int J>
+__device__ __forceinline__ const u8 *item_addr(const ItemAddrs &ia)
+{
+    const u64 v = J < 64 ? ia.a : ia.b;
+    const u32 lo = __builtin_amdgcn_readlane((u32)v, J % 64), hi = __builtin_amdgcn_readlane((u32)(v >> 32), J % 64);
+    return reinterpret_cast<const u8 *>(((u64)hi << 32) | lo);
+}
+
+template <int K, int NR, int R0, int D, int J>
+__device__ __forceinline__ void lds_issue(LdsRing<D> &ring, u32 w, u32 (&xs)[8], const SynCtx &c, const ItemAddrs &ia)
+{
+    const bool here = item_present<K, NR, R0>(c, J);
+    if constexpr (J == K - 1) {  // register path (short block k-1)
+        if (here)
+            load_syn_item<K, NR, R0, J>(xs, c);
+    } else {
+        const u8 *blk = item_addr<J>(ia);  // absent items: the first present data block
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + c.pa),
+                                         (__attribute__((address_space(3))) void *)&ring.v[w][J % D][0][0], 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + c.pb),
+                                         (__attribute__((address_space(3))) void *)&ring.v[w][J % D][1][0], 16, 0, 0);
+    }
+}
+
+template <int K, int NR, int R0, int D, int... Js>
+__device__ __forceinline__ void lds_first(std::integer_sequence<int, Js...>, LdsRing<D> &ring, u32 w, u32 (&xs)[8],
+                                          const SynCtx &c, const ItemAddrs &ia)
+{
+    (lds_issue<K, NR, R0, D, Js>(ring, w, xs, c, ia), ...);
+}
+
+// loads issued after item J's when J is consumed: 2 per DMA item in (J, J + D)
+template <int K, int NI, int D, int J>
+constexpr int later_dmas()
+{
+    int n = 0;
+    for (int t = J + 1; t < J + D && t < NI; ++t)
+        n += t != K - 1 ? 2 : 0;
+    return n;
+}
+
+template <int K, int M, int R0, int NR, int D, bool FUSED, int J>
+__device__ __forceinline__ void syn_item_lds(u32 (&acc)[NR * 8], LdsRing<D> &ring, u32 w, u32 (&xs)[8],
+                                             const SynCtx &c, const ItemAddrs &ia, u8 *orow0, u32 B, u32 last,
+                                             bool copies, u8 *syn, u32 &q)
+{
+    constexpr int NI = K + NR;
+    u32 x[8];
+    if constexpr (J == K - 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            x[i] = xs[i];
+    } else {
+        wait_vm<later_dmas<K, NI, D, J>()>();
+        const u32x4 a = ring.v[w][J % D][0][threadIdx.x & 63], b = ring.v[w][J % D][1][threadIdx.x & 63];
+        x[0] = a.x;
+        x[1] = a.y;
+        x[2] = a.z;
+        x[3] = a.w;
+        x[4] = b.x;
+        x[5] = b.y;
+        x[6] = b.z;
+        x[7] = b.w;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read before it is refilled
+    }
+    if constexpr (J + D < NI)
+        lds_issue<K, NR, R0, D, J + D>(ring, w, xs, c, ia);
+    if (!item_present<K, NR, R0>(c, J))
+        return;
+    syn_process<K, M, R0, NR, FUSED, J>(acc, x, c, orow0, B, last, copies, syn, q);
+}
+
+template <int K, int M, int R0, int NR, int D, bool FUSED, int... Js>
+__device__ __forceinline__ void syn_items_lds(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], LdsRing<D> &ring,
+                                              u32 w, u32 (&xs)[8], const SynCtx &c, const ItemAddrs &ia, u8 *orow0,
+                                              u32 B, u32 last, bool copies, u8 *syn, u32 &q)
+{
+    (syn_item_lds<K, M, R0, NR, D, FUSED, Js>(acc, ring, w, xs, c, ia, orow0, B, last, copies, syn, q), ...);
+}
+
+// lane t: item t's block (data t, or parity row R0 + t - K) and item 64 + t's; an absent item's
+// loads read the first present data block (before k-1: e < k - 1)
+template <int K, int NR, int R0>
+__device__ __forceinline__ ItemAddrs item_addrs(const SynCtx &c)
+{
+    constexpr int NI = K + NR;
+    const u32 t = threadIdx.x & 63;
+    const u32 first = (u32)__builtin_ctzll(c.dmask);
+    auto addr = [&](u32 it) -> u64 {
+        if (it >= (u32)NI)
+            return 0;
+        const bool here = it < (u32)K ? ((c.dmask >> it) & 1) : ((c.pmask >> (R0 + it - K)) & 1);
+        const u32 slot = !here ? first : it < (u32)K ? it : it + R0;
+        return (u64)(uintptr_t)(c.blocks + c.off[c.slot0 + slot]);
+    };
+    return ItemAddrs{addr(t), NI > 64 ? addr(64 + t) : 0};
+}
+
+#if SEC_FUSED_LDS
+using FusedLds = LdsRing<SEC_FUSED_LDS_RING>;
+#else
+struct FusedLds {};
+#endif
+template <int K>
+using Phase1Lds = std::conditional_t<(K >= 32), FusedLds, char>;  // the LDS ring of k >= 32
+
 template <int K, int M, int R0, int NR, int D>
 __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__restrict__ out, u8 *__restrict__ syn,
-                                         const sec::SynDesc &d, const sec::SynSlots &sl, u32 s, bool copies)
+                                         const sec::SynDesc &d, const sec::SynSlots &sl, u32 s, bool copies,
+                                         Phase1Lds<K> &lring)
 {
     const u32 B = d.B;
     const u32 lane = (threadIdx.x & 63) * 16;
     SynCtx c{blocks,  sl.off,     sl.avail, sl.masks + d.wq0,     d.slot0,         min(s + lane, B - 16),
              min(s + 1024 + lane, B - 16), s + lane, s + 1024 + lane, d.dmask, d.pmask, sec::syn_stride(B)};
-    u32 ring[D][8];
-    load_syn_first<K, NR, R0>(std::make_integer_sequence<int, D>{}, ring, c);
     u32 acc[NR * 8];
 #pragma unroll
     for (int i = 0; i < NR * 8; ++i)
         acc[i] = 0;
     // syndrome row of this group's first present parity row: the present rows below R0
     u32 q = (u32)__builtin_popcountll(d.pmask & ((1ull << R0) - 1ull));
-    syn_items<K, M, R0, NR, D, false>(std::make_integer_sequence<int, K + NR>{}, acc, ring, c, out + d.out_off, B,
-                                      d.last, copies, syn + d.syn_off, q);
+#if SEC_FUSED_LDS
+    if constexpr (K >= 32) {
+        constexpr int DL = SEC_FUSED_LDS_RING;
+        const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        u32 xs[8];
+        const ItemAddrs ia = item_addrs<K, NR, R0>(c);
+        lds_first<K, NR, R0, DL>(std::make_integer_sequence<int, DL>{}, lring, w, xs, c, ia);
+        syn_items_lds<K, M, R0, NR, DL, false>(std::make_integer_sequence<int, K + NR>{}, acc, lring, w, xs, c, ia,
+                                               out + d.out_off, B, d.last, copies, syn + d.syn_off, q);
+    } else
+#endif
+    {
+        u32 ring[D][8];
+        load_syn_first<K, NR, R0>(std::make_integer_sequence<int, D>{}, ring, c);
+        syn_items<K, M, R0, NR, D, false>(std::make_integer_sequence<int, K + NR>{}, acc, ring, c, out + d.out_off,
+                                          B, d.last, copies, syn + d.syn_off, q);
+    }
 }
 
 // The scaled syndromes go to `syn` as bit planes; sec_solve_bs_kernel then solves for the lost
@@ -570,14 +728,15 @@ __global__ __launch_bounds__(256) void sec_syndrome_bs_kernel(const u8 *__restri
     if (s >= d.B)
         return;
     const bool copies = tl.ntail & 1;  // the chunk's first touched row group copies the primaries
+    __shared__ Phase1Lds<K> lring;     // one ring for both row-group variants
     if constexpr (M - K <= NR) {
-        syn_span<K, M, 0, NR, D>(blocks, out, syn, d, sl, s, copies);
+        syn_span<K, M, 0, NR, D>(blocks, out, syn, d, sl, s, copies, lring);
     } else {
         static_assert(M - K == 2 * NR, "two row groups");
         if (tl.r0 == 0)
-            syn_span<K, M, 0, NR, D>(blocks, out, syn, d, sl, s, copies);
+            syn_span<K, M, 0, NR, D>(blocks, out, syn, d, sl, s, copies, lring);
         else
-            syn_span<K, M, NR, NR, D>(blocks, out, syn, d, sl, s, copies);
+            syn_span<K, M, NR, NR, D>(blocks, out, syn, d, sl, s, copies, lring);
     }
 }
 
@@ -765,134 +924,10 @@ __device__ __forceinline__ void fused_groups(std::integer_sequence<int, Gs...>, 
     (fused_group<K, M, RP0, NRP, NR2, Gs>(std::make_integer_sequence<int, NRP>{}, sy, pmask, o), ...);
 }
 
-// ---- the fused kernel's loads: an LDS ring filled by global_load_lds (no VGPRs) -------------
-// SEC_FUSED_LDS (build knob): phase 1's blocks stream through a per-wave LDS ring of D slots
-// (two 1 KiB halves each, one global_load_lds_dwordx4 per half: lane l's 16 bytes land at
-// slot + 16 l), so D blocks are in flight without ring registers.  Every item issues its two
-// loads, an absent one from the chunk's first present data block (just read: an L2 hit), so
-// the loads issued after an item's are a compile-time count N and the wait for it is a plain
-// `s_waitcnt vmcnt(N)`: loads complete in order, so at most N outstanding retires it whatever
-// stores are in flight (a run-time count needs a branch per wait, which cost 80 VGPRs).  Data
-// block K-1 (possibly short, read in place) keeps the register path and is not counted
-// (waiting for fewer loads is stricter).  Used for k >= 32 (zfec(32,48), (64,96)), where it
-// measured +0-5 % reassembling and +7-16 % recover-only over the register ring; the small-k
-// shapes keep the register ring (LDS ring -8 % on (32,48) with 8 lost, -9 % (16,24), -20 % C4;
-// the direct decode is chosen there anyway), r03_syn_ab_lds.jsonl.
-#ifndef SEC_FUSED_LDS
-#define SEC_FUSED_LDS 1
-#endif
-#ifndef SEC_FUSED_LDS_RING
-#define SEC_FUSED_LDS_RING 8
-#endif
-
-template <int D>
-struct LdsRing {
-    u32x4 v[4][D][2][64];  // [wave of a 256-lane workgroup][slot][half][lane]
-};
-
-template <int N>
-__device__ __forceinline__ void wait_vm()
-{
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-
-// Item addresses, one per lane (lane t: item t in `a`, item 64 + t in `b`), read with a
-// compile-time readlane: a per-item load of the slot table would be a vector load whose wait
-// drains every DMA in flight (the table is not provably unwritten, so it is no scalar load).
-struct ItemAddrs {
-    u64 a, b;
-};
-
-template <int J>
-__device__ __forceinline__ const u8 *item_addr(const ItemAddrs &ia)
-{
-    const u64 v = J < 64 ? ia.a : ia.b;
-    const u32 lo = __builtin_amdgcn_readlane((u32)v, J % 64), hi = __builtin_amdgcn_readlane((u32)(v >> 32), J % 64);
-    return reinterpret_cast<const u8 *>(((u64)hi << 32) | lo);
-}
-
-template <int K, int NR, int R0, int D, int J>
-__device__ __forceinline__ void lds_issue(LdsRing<D> &ring, u32 w, u32 (&xs)[8], const SynCtx &c, const ItemAddrs &ia)
-{
-    const bool here = item_present<K, NR, R0>(c, J);
-    if constexpr (J == K - 1) {  // register path (short block k-1)
-        if (here)
-            load_syn_item<K, NR, R0, J>(xs, c);
-    } else {
-        const u8 *blk = item_addr<J>(ia);  // absent items: the first present data block
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + c.pa),
-                                         (__attribute__((address_space(3))) void *)&ring.v[w][J % D][0][0], 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + c.pb),
-                                         (__attribute__((address_space(3))) void *)&ring.v[w][J % D][1][0], 16, 0, 0);
-    }
-}
-
-template <int K, int NR, int R0, int D, int... Js>
-__device__ __forceinline__ void lds_first(std::integer_sequence<int, Js...>, LdsRing<D> &ring, u32 w, u32 (&xs)[8],
-                                          const SynCtx &c, const ItemAddrs &ia)
-{
-    (lds_issue<K, NR, R0, D, Js>(ring, w, xs, c, ia), ...);
-}
-
-// loads issued after item J's when J is consumed: 2 per DMA item in (J, J + D)
-template <int K, int NI, int D, int J>
-constexpr int later_dmas()
-{
-    int n = 0;
-    for (int t = J + 1; t < J + D && t < NI; ++t)
-        n += t != K - 1 ? 2 : 0;
-    return n;
-}
-
-template <int K, int M, int R0, int NR, int D, int J>
-__device__ __forceinline__ void syn_item_lds(u32 (&acc)[NR * 8], LdsRing<D> &ring, u32 w, u32 (&xs)[8],
-                                             const SynCtx &c, const ItemAddrs &ia, u8 *orow0, u32 B, u32 last,
-                                             bool copies, u32 &q)
-{
-    constexpr int NI = K + NR;
-    u32 x[8];
-    if constexpr (J == K - 1) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            x[i] = xs[i];
-    } else {
-        wait_vm<later_dmas<K, NI, D, J>()>();
-        const u32x4 a = ring.v[w][J % D][0][threadIdx.x & 63], b = ring.v[w][J % D][1][threadIdx.x & 63];
-        x[0] = a.x;
-        x[1] = a.y;
-        x[2] = a.z;
-        x[3] = a.w;
-        x[4] = b.x;
-        x[5] = b.y;
-        x[6] = b.z;
-        x[7] = b.w;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read before it is refilled
-    }
-    if constexpr (J + D < NI)
-        lds_issue<K, NR, R0, D, J + D>(ring, w, xs, c, ia);
-    if (!item_present<K, NR, R0>(c, J))
-        return;
-    syn_process<K, M, R0, NR, true, J>(acc, x, c, orow0, B, last, copies, nullptr, q);
-}
-
-template <int K, int M, int R0, int NR, int D, int... Js>
-__device__ __forceinline__ void syn_items_lds(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], LdsRing<D> &ring,
-                                              u32 w, u32 (&xs)[8], const SynCtx &c, const ItemAddrs &ia, u8 *orow0,
-                                              u32 B, u32 last, bool copies, u32 &q)
-{
-    (syn_item_lds<K, M, R0, NR, D, Js>(acc, ring, w, xs, c, ia, orow0, B, last, copies, q), ...);
-}
-
-#if SEC_FUSED_LDS
-using FusedLds = LdsRing<SEC_FUSED_LDS_RING>;
-#else
-struct FusedLds {};
-#endif
-
 template <int K, int M, int RP0, int NRP, int NR2, int D>
 __device__ __forceinline__ void fused_span(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                            const sec::SynDesc &d, const sec::SynSlots &sl, u32 s, bool copies,
-                                           std::conditional_t<(K >= 32), FusedLds, char> &lring)
+                                           Phase1Lds<K> &lring)
 {
     const u32 B = d.B;
     const u32 lane = (threadIdx.x & 63) * 16;
@@ -908,26 +943,10 @@ __device__ __forceinline__ void fused_span(const u8 *__restrict__ blocks, u8 *__
         constexpr int DL = SEC_FUSED_LDS_RING;
         const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         u32 xs[8];
-        // lane t: item t's block (data t, or parity row RP0 + t - K) and item 64 + t's; an absent
-        // item's loads read the first present data block (before k-1: e < k - 1)
-        ItemAddrs ia;
-        {
-            constexpr int NI = K + NRP;
-            const u32 t = threadIdx.x & 63;
-            const u32 first = (u32)__builtin_ctzll(d.dmask);
-            auto addr = [&](u32 it) -> u64 {
-                if (it >= (u32)NI)
-                    return 0;
-                const bool here = it < (u32)K ? ((d.dmask >> it) & 1) : ((d.pmask >> (RP0 + it - K)) & 1);
-                const u32 slot = !here ? first : it < (u32)K ? it : it + RP0;
-                return (u64)(uintptr_t)(c.blocks + c.off[c.slot0 + slot]);
-            };
-            ia.a = addr(t);
-            ia.b = NI > 64 ? addr(64 + t) : 0;
-        }
+        const ItemAddrs ia = item_addrs<K, NRP, RP0>(c);
         lds_first<K, NRP, RP0, DL>(std::make_integer_sequence<int, DL>{}, lring, w, xs, c, ia);
-        syn_items_lds<K, M, RP0, NRP, DL>(std::make_integer_sequence<int, K + NRP>{}, acc, lring, w, xs, c, ia,
-                                          out + d.out_off, B, d.last, copies, q);
+        syn_items_lds<K, M, RP0, NRP, DL, true>(std::make_integer_sequence<int, K + NRP>{}, acc, lring, w, xs, c, ia,
+                                                out + d.out_off, B, d.last, copies, nullptr, q);
     } else
 #endif
     {
@@ -953,7 +972,7 @@ __global__ __launch_bounds__(256) void sec_decode_bs_kernel(const u8 *__restrict
     if (s >= d.B)
         return;
     const bool copies = tl.ntail & 1;
-    __shared__ std::conditional_t<(K >= 32), FusedLds, char> lring;  // one ring for both row-group variants
+    __shared__ Phase1Lds<K> lring;  // one ring for both row-group variants
     if constexpr (M - K <= NRP) {
         fused_span<K, M, 0, NRP, NR2, D>(blocks, out, d, sl, s, copies, lring);
     } else {

@@ -1,0 +1,10 @@
+#!/bin/bash
+# LDS-DMA ring in the two-kernel syndrome path's phase 1 (k >= 32): syndrome tests, then the A/B
+# against the register ring (libstorbec_nolds.so) on the two-kernel and default paths.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
+export TMPDIR=/tmp
+echo "== syndrome tests" && timeout -k 10 400 python3 -u -m pytest tests/test_gpu_syndrome.py -x -v --timeout 120 --timeout-method thread > $O/pt_syn.log 2>&1 || { tail -40 $O/pt_syn.log; exit 1; }
+tail -1 $O/pt_syn.log
+echo "== syn A/B" && timeout -k 10 700 python3 -u tools/syn_ab.py --rounds 3 --cases "zfec(64,96);zfec(32,48) 1MiB" --variants "two@SEC_SYN=1+SEC_SYN_FUSED=0,two_regring@SEC_SYN=1+SEC_SYN_FUSED=0/nolds,auto,auto_regring@/nolds" > $O/syn_ab_two_lds.jsonl 2> $O/syn_ab_two_lds.err || { tail -20 $O/syn_ab_two_lds.err; exit 1; }
+cat $O/syn_ab_two_lds.jsonl
