@@ -80,7 +80,8 @@ VARIANTS = {
     "fr2": {"SEC_FUSED_RING": 2},
     "fr6": {"SEC_FUSED_RING": 6},
     "nolds": {"SEC_FUSED_LDS": 0},  # fused syndrome decode: register ring instead of the LDS-DMA ring
-    "lds6": {"SEC_FUSED_LDS_RING": 6},  # bit-sliced encode: no repeated stores past B (clamped lanes)
+    "lds6": {"SEC_FUSED_LDS_RING": 6},
+    "nopf": {"SEC_FUSED_PREFETCH": 0},  # fused syndrome decode: one span per wave (no cross-span prefetch)  # bit-sliced encode: no repeated stores past B (clamped lanes)
     # decode workgroups per CU capped through padding LDS (160 KiB per CU): 3 or 2 per CU
     "dpad3": {"SEC_DEC_LDS_PAD": 50000},
     "dpad2": {"SEC_DEC_LDS_PAD": 60000},
