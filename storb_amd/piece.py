@@ -69,6 +69,35 @@ PREFETCH_MIN_CHUNK = 512 << 10
 # 4 MiB object fell from 1236-1289 to 811 MiB/s per chunk, 1327-1469 to 868 streamed).
 PARALLEL_COPY_MIN = 256 << 10
 HASH_ON_FILL = True  # encode_chunk: each large piece's id hashing starts as soon as that piece is filled
+
+# glibc hands the process's freed heap top back to the kernel once it exceeds ~2x the (dynamic)
+# mmap threshold, so when a caller drops each chunk's pieces after sending them (the validator's
+# loop), the next chunk's pieces start on fresh pages again and fault them in: an 8 MiB chunk's
+# per-chunk upload spent ~0.7 ms in page faults (3.66 GiB/s; 5.37 with the heap kept;
+# tools/upload_timeline.py, profiles/r03_upload_malloc.jsonl).  STORB_AMD_MALLOC_TUNE=1 makes
+# the first large-piece encode set, once per process, M_MMAP_THRESHOLD = 32 MiB (glibc's own
+# dynamic maximum) and M_TRIM_THRESHOLD = 256 MiB (at most 256 MiB of freed heap stays mapped).
+# It is opt-in: a caller that keeps every piece (tools/stream_rate.py) grows the heap instead
+# and measured slower with it (per-chunk 3.6 -> 2.9 GiB/s, streamed 6.9 -> 4.7).  The same
+# effect is available without code as MALLOC_TRIM_THRESHOLD_ / MALLOC_MMAP_THRESHOLD_.
+_malloc_tuned = False
+
+
+def _tune_malloc() -> None:
+    global _malloc_tuned
+    if _malloc_tuned:
+        return
+    _malloc_tuned = True
+    if os.environ.get("STORB_AMD_MALLOC_TUNE", "0") != "1":
+        return
+    try:
+        mallopt = ctypes.CDLL(None).mallopt
+    except (OSError, AttributeError):
+        return
+    mallopt.argtypes, mallopt.restype = [ctypes.c_int, ctypes.c_int], ctypes.c_int
+    m_trim_threshold, m_mmap_threshold = -1, -3  # <malloc.h>
+    mallopt(m_mmap_threshold, 32 << 20)
+    mallopt(m_trim_threshold, 256 << 20)
 STREAM_WINDOW_BYTES = 64 << 20  # chunk bytes per GPU call in the *_stream pipelines
 # encode_chunks_stream(piece_ids=True) over windows whose pieces are all >= PARALLEL_COPY_MIN:
 # the ids come from the GPU SHA-1 kernel, fused after the window's encode, instead of hashlib
@@ -458,6 +487,8 @@ def encode_chunk(chunk: bytes, chunk_idx: int) -> EncodedChunk:
         encoded_pieces = enc_.encode(chunk)
     else:  # piece ids hashed on the pool: data pieces beside the GPU call, parity right after
         hp = _pool("hash")
+        if B >= PARALLEL_COPY_MIN:
+            _tune_malloc()
         if B >= PARALLEL_COPY_MIN and HASH_ON_FILL:  # large pieces: copies on the pool too, each hashed once filled
             pieces, hf = _pieces_parallel([chunk], [(k, m, B, padlen)], hash_ids=True)
             encoded_pieces, futs = pieces[0], hf[0]
