@@ -242,9 +242,138 @@ __device__ __forceinline__ void all_blocks(std::integer_sequence<int, Js...>, u3
 #define SEC_BS_WAVES_ATTR
 #endif
 
+// ---- loads through an LDS ring filled by global_load_lds (k >= 32; see phase 1 below) --------
+#ifndef SEC_FUSED_LDS
+#define SEC_FUSED_LDS 1
+#endif
+#ifndef SEC_FUSED_LDS_RING
+#define SEC_FUSED_LDS_RING 8
+#endif
+
+template <int D>
+struct LdsRing {
+    u32x4 v[4][D][2][64];  // [wave of a 256-lane workgroup][slot][half][lane]
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm()
+{
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// Item addresses, one per lane (lane t: item t in `a`, item 64 + t in `b`), read with a
+// compile-time readlane: a per-item load of the slot table would be a vector load whose wait
+// drains every DMA in flight (the table is not provably unwritten, so it is no scalar load).
+struct ItemAddrs {
+    u64 a, b;
+};
+
+template <int J>
+__device__ __forceinline__ const u8 *item_addr(const ItemAddrs &ia)
+{
+    const u64 v = J < 64 ? ia.a : ia.b;
+    const u32 lo = __builtin_amdgcn_readlane((u32)v, J % 64), hi = __builtin_amdgcn_readlane((u32)(v >> 32), J % 64);
+    return reinterpret_cast<const u8 *>(((u64)hi << 32) | lo);
+}
+
+// loads issued after item J's when J is consumed: 2 per DMA item in (J, J + D)
+template <int K, int NI, int D, int J>
+constexpr int later_dmas()
+{
+    int n = 0;
+    for (int t = J + 1; t < J + D && t < NI; ++t)
+        n += t != K - 1 ? 2 : 0;
+    return n;
+}
+
+#if SEC_FUSED_LDS
+using FusedLds = LdsRing<SEC_FUSED_LDS_RING>;
+#else
+struct FusedLds {};
+#endif
+template <int K>
+using Phase1Lds = std::conditional_t<(K >= 32), FusedLds, char>;  // the LDS ring of k >= 32
+
+// The (32,48) encode reads its blocks through an LDS ring of SEC_ENC_LDS_RING blocks per wave
+// (+10 % over the register ring, r03_enc_lds_ab.jsonl).  (64,96) keeps the register ring: with
+// the LDS ring its two-group kernel takes 257 registers (1 wave per SIMD, -30 %), and one
+// launch per group with the ring (+20 % over the same without it) still trails the two-group
+// kernel's L2 reuse (-3 %).  SEC_ENC_LDS (build knob, A/B): 0 = no LDS ring, 2 = every k >= 32.
+#ifndef SEC_ENC_LDS
+#define SEC_ENC_LDS 1
+#endif
+#ifndef SEC_ENC_LDS_RING
+#define SEC_ENC_LDS_RING 8
+#endif
+template <int K>
+using EncLds = std::conditional_t<((SEC_ENC_LDS == 1 && K == 32) || (SEC_ENC_LDS == 2 && K >= 32)),
+                                  LdsRing<SEC_ENC_LDS_RING>, char>;
+
+// block J's two DMAs into its ring slot; the short last block K-1 goes to registers instead
+template <int K, int D, int J>
+__device__ __forceinline__ void enc_issue(LdsRing<D> &ring, u32 w, u32 (&xs)[8], const u8 *src, u64 B, u32 pa, u32 pb,
+                                          u32 valid)
+{
+    if constexpr (J == K - 1) {
+        load_block<false>(xs, src + (u64)J * B, pa, pb, valid, true);
+    } else {
+        const u8 *blk = src + (u64)J * B;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + pa),
+                                         (__attribute__((address_space(3))) void *)&ring.v[w][J % D][0][0], 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + pb),
+                                         (__attribute__((address_space(3))) void *)&ring.v[w][J % D][1][0], 16, 0, 0);
+    }
+}
+
+template <int K, int D, int... Js>
+__device__ __forceinline__ void enc_first(std::integer_sequence<int, Js...>, LdsRing<D> &ring, u32 w, u32 (&xs)[8],
+                                          const u8 *src, u64 B, u32 pa, u32 pb, u32 valid)
+{
+    (enc_issue<K, D, Js>(ring, w, xs, src, B, pa, pb, valid), ...);
+}
+
+template <int K, int M, int R0, int NR, int D, int J>
+__device__ __forceinline__ void enc_block_lds(u32 (&acc)[NR * 8], LdsRing<D> &ring, u32 w, u32 (&xs)[8],
+                                              const u8 *src, u64 B, u32 pa, u32 pb, u32 valid)
+{
+    u32 x[8];
+    if constexpr (J == K - 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            x[i] = xs[i];
+    } else {
+        wait_vm<later_dmas<K, K, D, J>()>();
+        const u32x4 a = ring.v[w][J % D][0][threadIdx.x & 63], b = ring.v[w][J % D][1][threadIdx.x & 63];
+        x[0] = a.x;
+        x[1] = a.y;
+        x[2] = a.z;
+        x[3] = a.w;
+        x[4] = b.x;
+        x[5] = b.y;
+        x[6] = b.z;
+        x[7] = b.w;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read before it is refilled
+    }
+    if constexpr (J + D < K)
+        enc_issue<K, D, J + D>(ring, w, xs, src, B, pa, pb, valid);
+    transpose8(x);
+    u32 lo[16], hi[16];
+    subsets(x[0], x[1], x[2], x[3], lo);
+    subsets(x[4], x[5], x[6], x[7], hi);
+    block_rows<K, M, R0, J, J == 0>(std::make_integer_sequence<int, NR * 8>{}, acc, lo, hi);
+}
+
+template <int K, int M, int R0, int NR, int D, int... Js>
+__device__ __forceinline__ void enc_blocks_lds(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], LdsRing<D> &ring,
+                                               u32 w, u32 (&xs)[8], const u8 *src, u64 B, u32 pa, u32 pb, u32 valid)
+{
+    (enc_block_lds<K, M, R0, NR, D, Js>(acc, ring, w, xs, src, B, pa, pb, valid), ...);
+}
+
 // One wave's span of one tile: rows [R0, R0 + NR) of the chunk's parity over the lane's pieces.
 template <int K, int M, int R0, int NR, int D, bool NT>
-__device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d, u32 s)
+__device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d, u32 s,
+                                        EncLds<K> &lring)
 {
     static_assert(D >= 1 && D <= K, "ring depth");
     const u32 B = d.B;
@@ -254,12 +383,21 @@ __device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restric
     const u32 pa = min(s + lane, B - 16), pb = min(s + 1024 + lane, B - 16);
     const u8 *src = in + d.in_off;
 
-    u32 ring[D][8];
-#pragma unroll
-    for (int j = 0; j < D; ++j)
-        load_block<NT>(ring[j], src + (u64)j * B, pa, pb, d.valid, j == K - 1);
     u32 acc[NR * 8];
-    all_blocks<K, M, R0, NR, D, NT>(std::make_integer_sequence<int, K>{}, acc, ring, src, B, pa, pb, d.valid);
+    if constexpr (!std::is_same_v<EncLds<K>, char>) {
+        constexpr int DL = SEC_ENC_LDS_RING;
+        const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        u32 xs[8];
+        enc_first<K, DL>(std::make_integer_sequence<int, DL>{}, lring, w, xs, src, B, pa, pb, d.valid);
+        enc_blocks_lds<K, M, R0, NR, DL>(std::make_integer_sequence<int, K>{}, acc, lring, w, xs, src, B, pa, pb,
+                                         d.valid);
+    } else {
+        u32 ring[D][8];
+#pragma unroll
+        for (int j = 0; j < D; ++j)
+            load_block<NT>(ring[j], src + (u64)j * B, pa, pb, d.valid, j == K - 1);
+        all_blocks<K, M, R0, NR, D, NT>(std::make_integer_sequence<int, K>{}, acc, ring, src, B, pa, pb, d.valid);
+    }
 
     u8 *dst = par + d.par_off;
 #pragma unroll
@@ -288,7 +426,8 @@ __global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs_kernel(co
     const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
     if (s >= d.B)
         return;
-    bs_span<K, M, R0, NR, D, true>(in, par, d, s);
+    __shared__ EncLds<K> lring;
+    bs_span<K, M, R0, NR, D, true>(in, par, d, s, lring);
 }
 
 // Two row groups in one launch, the tile's r0 picking one: the plan puts a run of 8 tiles of
@@ -305,10 +444,11 @@ __global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs2_kernel(c
     const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
     if (s >= d.B)
         return;
+    __shared__ EncLds<K> lring;  // one ring for both row-group variants
     if (tl.r0 == 0)
-        bs_span<K, M, 0, NR, D, false>(in, par, d, s);
+        bs_span<K, M, 0, NR, D, false>(in, par, d, s, lring);
     else
-        bs_span<K, M, NR, NR, D, false>(in, par, d, s);
+        bs_span<K, M, NR, NR, D, false>(in, par, d, s, lring);
 }
 
 // ---- decode: syndromes of the present parity rows, then a Cauchy solve (wide decodes) --------
@@ -548,39 +688,6 @@ __device__ __forceinline__ void syn_items(std::integer_sequence<int, Js...>, u32
 // measured +0-5 % reassembling and +7-16 % recover-only over the register ring; the small-k
 // shapes keep the register ring (LDS ring -8 % on (32,48) with 8 lost, -9 % (16,24), -20 % C4;
 // the direct decode is chosen there anyway), r03_syn_ab_lds.jsonl.
-#ifndef SEC_FUSED_LDS
-#define SEC_FUSED_LDS 1
-#endif
-#ifndef SEC_FUSED_LDS_RING
-#define SEC_FUSED_LDS_RING 8
-#endif
-
-template <int D>
-struct LdsRing {
-    u32x4 v[4][D][2][64];  // [wave of a 256-lane workgroup][slot][half][lane]
-};
-
-template <int N>
-__device__ __forceinline__ void wait_vm()
-{
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-
-// Item addresses, one per lane (lane t: item t in `a`, item 64 + t in `b`), read with a
-// compile-time readlane: a per-item load of the slot table would be a vector load whose wait
-// drains every DMA in flight (the table is not provably unwritten, so it is no scalar load).
-struct ItemAddrs {
-    u64 a, b;
-};
-
-template <int J>
-__device__ __forceinline__ const u8 *item_addr(const ItemAddrs &ia)
-{
-    const u64 v = J < 64 ? ia.a : ia.b;
-    const u32 lo = __builtin_amdgcn_readlane((u32)v, J % 64), hi = __builtin_amdgcn_readlane((u32)(v >> 32), J % 64);
-    return reinterpret_cast<const u8 *>(((u64)hi << 32) | lo);
-}
-
 template <int K, int NR, int R0, int D, int J>
 __device__ __forceinline__ void lds_issue(LdsRing<D> &ring, u32 w, u32 (&xs)[8], const SynCtx &c, const ItemAddrs &ia)
 {
@@ -602,16 +709,6 @@ __device__ __forceinline__ void lds_first(std::integer_sequence<int, Js...>, Lds
                                           const SynCtx &c, const ItemAddrs &ia)
 {
     (lds_issue<K, NR, R0, D, Js>(ring, w, xs, c, ia), ...);
-}
-
-// loads issued after item J's when J is consumed: 2 per DMA item in (J, J + D)
-template <int K, int NI, int D, int J>
-constexpr int later_dmas()
-{
-    int n = 0;
-    for (int t = J + 1; t < J + D && t < NI; ++t)
-        n += t != K - 1 ? 2 : 0;
-    return n;
 }
 
 template <int K, int M, int R0, int NR, int D, bool FUSED, int J>
@@ -670,14 +767,6 @@ __device__ __forceinline__ ItemAddrs item_addrs(const SynCtx &c)
     };
     return ItemAddrs{addr(t), NI > 64 ? addr(64 + t) : 0};
 }
-
-#if SEC_FUSED_LDS
-using FusedLds = LdsRing<SEC_FUSED_LDS_RING>;
-#else
-struct FusedLds {};
-#endif
-template <int K>
-using Phase1Lds = std::conditional_t<(K >= 32), FusedLds, char>;  // the LDS ring of k >= 32
 
 template <int K, int M, int R0, int NR, int D>
 __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__restrict__ out, u8 *__restrict__ syn,

@@ -75,13 +75,19 @@ VARIANTS = {
     "bsr16": {"SEC_BS_RING": 16},
     "bsld": {"SEC_BS_NT_LOAD": 0},  # bit-sliced encode with cached (not streaming) loads
     "bsw3": {"SEC_BS_WAVES": 3},  # bit-sliced encode capped for 3 waves per SIMD
+    "bsw2": {"SEC_BS_WAVES": 2, "SEC_ENC_LDS": 2},  # (64,96) LDS-ring encode capped at 256 registers
     # syndrome decode ring depths: phase 1 of the 16-row groups, phase 2 (solve), the fused kernel
     "synr4": {"SEC_SYN_RING": 4, "SEC_SOLVE_RING": 4},
     "fr2": {"SEC_FUSED_RING": 2},
     "fr6": {"SEC_FUSED_RING": 6},
     "nolds": {"SEC_FUSED_LDS": 0},  # fused syndrome decode: register ring instead of the LDS-DMA ring
     "lds6": {"SEC_FUSED_LDS_RING": 6},
-    "nopf": {"SEC_FUSED_PREFETCH": 0},  # fused syndrome decode: one span per wave (no cross-span prefetch)  # bit-sliced encode: no repeated stores past B (clamped lanes)
+    # bit-sliced (32,48) encode: register ring instead of the LDS-DMA ring; the ring for (64,96)
+    # too; ring depths
+    "noencl": {"SEC_ENC_LDS": 0},
+    "encl2": {"SEC_ENC_LDS": 2},
+    "encl4": {"SEC_ENC_LDS_RING": 4},
+    "encl6": {"SEC_ENC_LDS_RING": 6},
     # decode workgroups per CU capped through padding LDS (160 KiB per CU): 3 or 2 per CU
     "dpad3": {"SEC_DEC_LDS_PAD": 50000},
     "dpad2": {"SEC_DEC_LDS_PAD": 60000},
