@@ -294,13 +294,14 @@ struct FusedLds {};
 template <int K>
 using Phase1Lds = std::conditional_t<(K >= 32), FusedLds, char>;  // the LDS ring of k >= 32
 
-// The (32,48) encode reads its blocks through an LDS ring of SEC_ENC_LDS_RING blocks per wave
-// (+10 % over the register ring, r03_enc_lds_ab.jsonl).  (64,96) keeps the register ring: with
-// the LDS ring its two-group kernel takes 257 registers (1 wave per SIMD, -30 %), and one
-// launch per group with the ring (+20 % over the same without it) still trails the two-group
-// kernel's L2 reuse (-3 %).  SEC_ENC_LDS (build knob, A/B): 0 = no LDS ring, 2 = every k >= 32.
+// SEC_ENC_LDS (build knob, A/B; default 0 = the register ring): 1 = the (32,48) encode reads its
+// blocks through an LDS ring of SEC_ENC_LDS_RING blocks per wave, 2 = every k >= 32 encode does.
+// Measured (r03_enc_lds_ab.jsonl): (32,48) +8-10 % on 512 KiB chunks but -14 % on 4 MiB and -7 %
+// on 32 MiB chunks; (64,96) -27 % (its two-group kernel takes 257 registers: 1 wave per SIMD),
+// even when capped at 256, and one launch per group with the ring (+20 % over the same without
+// it) still trails the two-group kernel's L2 reuse.
 #ifndef SEC_ENC_LDS
-#define SEC_ENC_LDS 1
+#define SEC_ENC_LDS 0
 #endif
 #ifndef SEC_ENC_LDS_RING
 #define SEC_ENC_LDS_RING 8

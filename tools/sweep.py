@@ -82,12 +82,13 @@ VARIANTS = {
     "fr6": {"SEC_FUSED_RING": 6},
     "nolds": {"SEC_FUSED_LDS": 0},  # fused syndrome decode: register ring instead of the LDS-DMA ring
     "lds6": {"SEC_FUSED_LDS_RING": 6},
-    # bit-sliced (32,48) encode: register ring instead of the LDS-DMA ring; the ring for (64,96)
-    # too; ring depths
+    # bit-sliced k >= 32 encode through the LDS-DMA ring (kernels_bs.hip SEC_ENC_LDS; default 0,
+    # the register ring): (32,48) only, every k >= 32; ring depths
     "noencl": {"SEC_ENC_LDS": 0},
+    "encl1": {"SEC_ENC_LDS": 1},
     "encl2": {"SEC_ENC_LDS": 2},
-    "encl4": {"SEC_ENC_LDS_RING": 4},
-    "encl6": {"SEC_ENC_LDS_RING": 6},
+    "encl4": {"SEC_ENC_LDS": 1, "SEC_ENC_LDS_RING": 4},
+    "encl6": {"SEC_ENC_LDS": 1, "SEC_ENC_LDS_RING": 6},
     # decode workgroups per CU capped through padding LDS (160 KiB per CU): 3 or 2 per CU
     "dpad3": {"SEC_DEC_LDS_PAD": 50000},
     "dpad2": {"SEC_DEC_LDS_PAD": 60000},
