@@ -70,34 +70,11 @@ PREFETCH_MIN_CHUNK = 512 << 10
 PARALLEL_COPY_MIN = 256 << 10
 HASH_ON_FILL = True  # encode_chunk: each large piece's id hashing starts as soon as that piece is filled
 
-# glibc hands the process's freed heap top back to the kernel once it exceeds ~2x the (dynamic)
-# mmap threshold, so when a caller drops each chunk's pieces after sending them (the validator's
-# loop), the next chunk's pieces start on fresh pages again and fault them in: an 8 MiB chunk's
-# per-chunk upload spent ~0.7 ms in page faults (3.66 GiB/s; 5.37 with the heap kept;
-# tools/upload_timeline.py, profiles/r03_upload_malloc.jsonl).  STORB_AMD_MALLOC_TUNE=1 makes
-# the first large-piece encode set, once per process, M_MMAP_THRESHOLD = 32 MiB (glibc's own
-# dynamic maximum) and M_TRIM_THRESHOLD = 256 MiB (at most 256 MiB of freed heap stays mapped).
-# It is opt-in: a caller that keeps every piece (tools/stream_rate.py) grows the heap instead
-# and measured slower with it (per-chunk 3.6 -> 2.9 GiB/s, streamed 6.9 -> 4.7).  The same
-# effect is available without code as MALLOC_TRIM_THRESHOLD_ / MALLOC_MMAP_THRESHOLD_.
-_malloc_tuned = False
-
-
-def _tune_malloc() -> None:
-    global _malloc_tuned
-    if _malloc_tuned:
-        return
-    _malloc_tuned = True
-    if os.environ.get("STORB_AMD_MALLOC_TUNE", "0") != "1":
-        return
-    try:
-        mallopt = ctypes.CDLL(None).mallopt
-    except (OSError, AttributeError):
-        return
-    mallopt.argtypes, mallopt.restype = [ctypes.c_int, ctypes.c_int], ctypes.c_int
-    m_trim_threshold, m_mmap_threshold = -1, -3  # <malloc.h>
-    mallopt(m_mmap_threshold, 32 << 20)
-    mallopt(m_trim_threshold, 256 << 20)
+# The library never retunes the host process's allocator.  A validator that drops each chunk's
+# pieces after sending them can keep glibc from trimming the freed heap back to the kernel (so the
+# next chunk's pieces do not fault their pages in again) by starting the process with
+# MALLOC_MMAP_THRESHOLD_=33554432 MALLOC_TRIM_THRESHOLD_=268435456 ("Host
+# allocator"; measured in DESIGN.md §5a).
 STREAM_WINDOW_BYTES = 64 << 20  # chunk bytes per GPU call in the *_stream pipelines
 # encode_chunks_stream(piece_ids=True) over windows whose pieces are all >= PARALLEL_COPY_MIN:
 # the ids come from the GPU SHA-1 kernel, fused after the window's encode, instead of hashlib
@@ -403,9 +380,16 @@ def _fill(dst: np.ndarray, src: np.ndarray) -> None:
         dst[len(src):] = 0
 
 
-def _hash_filled(fill: Future, view: np.ndarray) -> str:
-    """SHA-1 hex of a piece once its fill (an earlier task of the same FIFO pool) is done."""
-    fill.result()
+def _hash_filled(fill: Future | None, view: np.ndarray, piece) -> str:
+    """SHA-1 hex of a piece once its fill (an earlier task of the same FIFO pool) is done.
+
+    `piece` is the bytes object (or _PendingBytes) `view` looks into.  The task holds it so the
+    piece outlives the hash: on CPython `view` is a raw view of the object's buffer with no
+    reference to it, and the memo may drop its own reference (eviction) while this task is
+    queued or running, after the caller dropped the piece too."""
+    if fill is not None:
+        fill.result()
+    assert piece is not None
     return hashlib.sha1(view).hexdigest()
 
 
@@ -431,7 +415,7 @@ def _pieces_parallel(chunks: list, shapes: list, digests: bool = False, hash_ids
             jobs.append(hp.submit(_fill, v, src[j * B:min((j + 1) * B, len(src))]))
         out.append(ps)
         if hash_ids:  # queued behind this chunk's data fills (FIFO), so they never wait long
-            hfut.append([hp.submit(_hash_filled, f, v) for f, v in zip(jobs[-k:], views)])
+            hfut.append([hp.submit(_hash_filled, f, v, b) for f, v, b in zip(jobs[-k:], views, ps)])
     # staged, not page-locked: the pool is faulting in the new pieces meanwhile, and locking
     # waits on the same memory-map lock (6.4 against 0.55 ms for one 8 MiB chunk on MI355X,
     # profiles/r03_upload_ab.jsonl)
@@ -446,7 +430,7 @@ def _pieces_parallel(chunks: list, shapes: list, digests: bool = False, hash_ids
             if hash_ids:  # the pool's queue holds the data pieces' hashes: the caller, idle
                 # until its pieces exist, copies the parity itself (r03_upload_timeline.json)
                 _fill(v, buf[o + r * B:o + (r + 1) * B])
-                hfut[i].append(hp.submit(_sha1_hex, v))
+                hfut[i].append(hp.submit(_hash_filled, None, v, b))
             else:
                 jobs.append(hp.submit(_fill, v, buf[o + r * B:o + (r + 1) * B]))
                 pj.append((jobs[-1], v))
@@ -487,8 +471,6 @@ def encode_chunk(chunk: bytes, chunk_idx: int) -> EncodedChunk:
         encoded_pieces = enc_.encode(chunk)
     else:  # piece ids hashed on the pool: data pieces beside the GPU call, parity right after
         hp = _pool("hash")
-        if B >= PARALLEL_COPY_MIN:
-            _tune_malloc()
         if B >= PARALLEL_COPY_MIN and HASH_ON_FILL:  # large pieces: copies on the pool too, each hashed once filled
             pieces, hf = _pieces_parallel([chunk], [(k, m, B, padlen)], hash_ids=True)
             encoded_pieces, futs = pieces[0], hf[0]

@@ -63,3 +63,71 @@ def test_memo_pauses_when_unused_and_resumes():
             assert m.take(o) == "p"
             break
     assert all(m.begin(10) is not None for _ in range(5))
+
+
+class _DeferringPool:
+    """Runs the piece fills at once and holds every other task (the SHA-1s) until run_held()."""
+
+    def __init__(self):
+        self.held = []
+
+    def submit(self, fn, *args):
+        from storb_amd import piece as P
+        f = Future()
+        if fn is P._fill:
+            fn(*args)
+            f.set_result(None)
+        else:
+            self.held.append((f, fn, args))
+        return f
+
+    def run_held(self):
+        for f, fn, args in self.held:
+            f.set_result(fn(*args))
+
+
+class _OracleRawEngine:
+    """encode_host_raw through the CPU oracle (test infrastructure only)."""
+
+    def encode_host_raw(self, chunks, shapes, digests=False, staged=False):
+        import numpy as np
+        from oracle import cfec
+        bufs, layout, o = [], [], 0
+        for c, (k, m) in zip(chunks, shapes):
+            blocks = cfec.easy_encode(bytes(c), k, m)
+            B = len(blocks[0])
+            bufs.extend(blocks[k:])
+            layout.append((o, B, m - k))
+            o += (m - k) * B
+        return np.frombuffer(b"".join(bufs) or b"\0", dtype=np.uint8).copy(), layout
+
+
+def test_hash_tasks_keep_their_pieces_alive(monkeypatch):
+    """a queued or running SHA-1 of encode_chunk's pieces must hold the piece
+    object itself, not only a raw view of its buffer, so neither the memo's eviction nor the caller
+    dropping the piece can free the bytes under the hash."""
+    import gc
+    import hashlib
+    import random
+    import sys
+
+    from storb_amd import piece as P
+
+    pool = _DeferringPool()
+    monkeypatch.setattr(P, "_pool", lambda name: pool)
+    monkeypatch.setattr(P, "get_engine", lambda: _OracleRawEngine())
+    chunk = random.Random(7).randbytes(3 * 300_000 + 11)
+    k, m, B, padlen = 4, 6, -(-len(chunk) // 4), 4 * (-(-len(chunk) // 4)) - len(chunk)
+    pieces, futs = P._pieces_parallel([chunk], [(k, m, B, padlen)], hash_ids=True)
+    ps, fs = pieces[0], futs[0]
+    assert len(ps) == m and len(pool.held) == m
+    want = [hashlib.sha1(p).hexdigest() for p in ps]
+    for p, (_, fn, args) in zip(ps, pool.held):
+        assert any(a is p for a in args), "hash task does not hold its piece"
+    # the caller and the memo drop every piece while the hashes are still queued
+    refs = [sys.getrefcount(p) for p in ps]
+    del pieces, ps, p
+    gc.collect()
+    assert all(r >= 3 for r in refs)
+    pool.run_held()
+    assert [f.result() for f in fs] == want
