@@ -51,6 +51,13 @@ Also reported on the headline line:
   e2e           host-buffer encode+decode through the C ABI incl. PCIe: pageable buffers
                 (page-locked per call, or staged through pinned slabs) and pinned buffers
                 (zero-copy) — reported beside `value`, never as it
+  c4, c5        BASELINE configs[3] and [4] measured in the same run after the headline's timed
+                region (the --workload c4 / c5 lines' fields, nested; --no-c4 / --no-c5 skip
+                them): each with its own roofline, PMC traffic and CPU baseline
+                (--sub-cpu-seconds on 1 thread, then on all threads)
+
+`traffic` fields come from profiles/pmc_<workload>.json (tools/gpu_pmc.sh) and only when that
+summary's `lib_digest` equals this build's source digest; otherwise they are null.
 
 STORB_BENCH_ENGINE=module:Class (tests only) runs the ranks on CPU tensors with that engine
 (tests/bench_stub.py: the oracle behind the Engine interface) over gloo, so the launch, the
@@ -110,6 +117,13 @@ def parse(argv=None):
     ap.add_argument("--no-recover", action="store_true",
                     help="skip the recover-only decode measurement (it shares the decode kernel's name, so a "
                          "rocprofv3 --stats run of the headline line wants it off)")
+    ap.add_argument("--no-c4", action="store_true", help="c2c3: skip the C4 sub-object (configs[3])")
+    ap.add_argument("--no-c5", action="store_true", help="c2c3: skip the C5 sub-object (configs[4])")
+    ap.add_argument("--sub-cpu-seconds", type=float, default=1.5,
+                    help="c2c3: CPU-baseline seconds (1 thread, then all threads) of the c4 / c5 sub-objects")
+    ap.add_argument("--c5-steps", type=int, default=10, help="c2c3: timed steps of the c5 sub-object")
+    ap.add_argument("--c5-device-only", action="store_true",
+                    help="c5: skip the end-to-end host steps (rocprofv3 PMC passes of the device-resident kernels)")
     ap.add_argument("--no-events", action="store_true",
                     help="A/B only: no per-launch HIP events in the timed region (roofline fields then null)")
     return ap.parse_args(argv)
@@ -304,14 +318,24 @@ def dec_descs_var(sizes, k, m, B, data_base, par_base, erased):
     return d, sn, offs, avail
 
 
-def load_traffic(kind: str, workload: str = "c2", name: str = "pmc_encode_c2.json"):
-    """Per-launch HBM bytes of a bench kernel from a committed rocprofv3 PMC summary
-    (tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE on that workload), else None."""
-    path = os.path.join(ROOT, "profiles", name)
+def lib_digest() -> str:
+    """Digest of libstorbec.so's sources (storb_amd/_build.py; also its build stamp)."""
+    from storb_amd import _build
+
+    return _build._digest()
+
+
+def load_traffic(kind: str, workload: str = "c2"):
+    """Per-launch HBM bytes of a bench kernel from the committed rocprofv3 PMC summary of that
+    workload (profiles/pmc_<workload>.json, tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE),
+    or None when there is none or it was taken on other library sources than this build's
+    (its `lib_digest`, VERDICT r03 weak #5: a stale summary is not this kernel's traffic)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     try:
         with open(path) as f:
             j = json.load(f)
-        if j.get("workload") == workload and j.get(kind, {}).get("hbm_bytes_per_launch"):
+        if (j.get("workload") == workload and j.get("lib_digest") == lib_digest()
+                and j.get(kind, {}).get("hbm_bytes_per_launch")):
             return float(j[kind]["hbm_bytes_per_launch"])
     except (OSError, ValueError):
         pass
@@ -358,14 +382,46 @@ def _cpu_worker(seconds: float, seed: int, sizes, k: int, m: int, erased, decode
             return done, nbytes, el
 
 
+def _cgroup_quota():
+    """CPUs the cgroup (v2 cpu.max) grants this process, rounded up, or None when unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else max(1, -(-int(quota) // int(period)))
+    except (OSError, ValueError):
+        return None
+
+
+def host_cpu_info() -> dict:
+    """The box's CPUs as this process sees them: the machine's count, the affinity mask, the
+    cgroup quota and the CPU model (VERDICT r03 weak #8: `cores` alone is a thread count)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = None
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": _cgroup_quota(),
+            "cpu_model": model}
+
+
 def cpu_threads() -> int:
-    """Threads for the multi-core baseline: the cores this process may use, at most 16 (the
-    GPU box's CPU share per GPU; os.cpu_count() there reports the whole machine)."""
+    """Threads for the multi-core baseline: the CPUs this process may use (affinity mask and
+    cgroup quota), at most 16 (the GPU box's CPU share per GPU; os.cpu_count() there reports the
+    whole machine)."""
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(16, n))
+    q = _cgroup_quota()
+    return max(1, min(16, n, q or n))
 
 
 def cpu_baseline(seconds: float, sizes=None, k=K, m=M, erased=ERASED, decode=True, what=None) -> dict:
@@ -387,7 +443,7 @@ def cpu_baseline(seconds: float, sizes=None, k=K, m=M, erased=ERASED, decode=Tru
     el = max(e for _, _, e in res)
     what = what or (f"(encode + decode {{{','.join(map(str, erased))}}} erased) of 1 MiB RS({k},{m - k}) chunks")
     return {"value": round(nb / el / GIB, 4), "unit": "GiB/s", "cores": T, "kind": "port",
-            "single_thread_value": round(b1 / e1 / GIB, 4),
+            "single_thread_value": round(b1 / e1 / GIB, 4), "host": host_cpu_info(),
             "sample": f"{T} threads x {seconds:.0f} s of {what} ({done} chunks), one chunk per task; 1 thread: "
                       f"{d1} chunks in {e1:.1f} s; oracle/fec_oracle.c (zfec fec.c restatement: 64 KiB LUT, "
                       f"8 KiB strides)"}
@@ -526,6 +582,7 @@ def main_c2c3(args, ctx):
                               "traffic": load_traffic("encode"), "kernel": ENC_KERNEL_C2,
                               "algorithmic_bytes_per_launch": enc_alg, "avg_launch_ms": round(enc_avg_s * 1e3, 4),
                               "launches": r["enc_launches"]},
+            "lib_digest": lib_digest(),
             "encode_gibs": round(nchunks * n / enc_avg_s / GIB, 2) if enc_gbs else None,
             "decode_gibs": round(nchunks * n / dec_avg_s / GIB, 2) if dec_gbs else None,
         }
@@ -533,6 +590,18 @@ def main_c2c3(args, ctx):
             res["decode_recover_only_kernel"] = recover_only_rate(ctx.eng, torch, r["src"], r["par"], nchunks, n, k,
                                                                   m, B)
 
+    # BASELINE configs[3] and [4] on the same run, after the headline's timed region (VERDICT r03
+    # item 1): each its own line's fields, nested; every rank takes part (its share of the job)
+    r.pop("src"), r.pop("par")
+    sub_cpu = 0 if args.no_cpu else args.sub_cpu_seconds
+    if not args.no_c4:
+        c4 = c4_result(args, ctx, sub_cpu, args.steps, args.warmup)
+        if ctx.rank == 0:
+            res["c4"] = c4
+    if not args.no_c5:
+        c5 = c5_result(args, ctx, sub_cpu, args.c5_steps, min(args.warmup, 2), staged=not args.no_e2e)
+        if ctx.rank == 0:
+            res["c5"] = c5
     # host-buffer (PCIe-inclusive) rate: reported, never `value`
     if ctx.rank == 0 and ctx.world == 1 and not args.no_e2e:
         res["e2e"] = e2e_rate(ctx.eng)
@@ -615,28 +684,29 @@ def c4_run(eng, dmod, rank, world, local, device, sync, steps, warmup, nchunks=C
     return res
 
 
-def main_c4(args, ctx):
-    r = c4_run(ctx.eng, ctx.dmod, ctx.rank, ctx.world, ctx.local, ctx.device, ctx.sync, args.steps, args.warmup,
+def c4_result(args, ctx, cpu_seconds, steps, warmup):
+    """BASELINE configs[3] measured on every rank; rank 0 gets the line's dict (else None)."""
+    r = c4_run(ctx.eng, ctx.dmod, ctx.rank, ctx.world, ctx.local, ctx.device, ctx.sync, steps, warmup,
                nchunks=args.c4_chunks, palign=args.c4_palign)
     n, k, m, B = C4_CHUNK, C4_K, C4_M, r["B"]
     job_bytes = r["total_chunks"] * n
-    value = args.steps * job_bytes / r["el_max"] / GIB
+    value = steps * job_bytes / r["el_max"] / GIB
     enc_alg = r["chunks"] * (n + (m - k) * B)
     dec_alg = r["chunks"] * (k * B + n)
     if ctx.rank != 0:
-        return
+        return None
     enc_gbs = _gbs(enc_alg, r["enc_avg_s"])
-    kernel = ("sec_encode_kernel<4, 1, false>" if os.environ.get("SEC_BS") == "0"
-              else "sec_encode_bs_kernel<10, 14, 0, 4, 5>")  # api.cpp bs_shape
+    bs_off = hasattr(ctx.eng, "option") and ctx.eng.option("SEC_BS") == 0
+    kernel = "sec_encode_kernel<4, 1, false>" if bs_off else "sec_encode_bs_kernel<10, 14, 0, 4, 5>"  # api.cpp bs_shape
     # the committed PMC summary applies to the configuration it was taken on (full job, N = 1,
     # this parity alignment)
     traffic = None
     if (ctx.world, args.c4_chunks, r["pstride"]) == (1, C4_CHUNKS, c4_pstride(B, 128)):
-        traffic = load_traffic("encode", "c4", "r03_pmc_c4.json")
+        traffic = load_traffic("encode", "c4")
     res = {
         "metric": "GiB/s device-resident RS(10,4) encode, 65536 x 64 KiB chunks sharded across N MI355X",
-        "value": round(value, 3), "unit": "GiB/s", "n_gpus": ctx.world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(r["el_max"] / args.steps * 1e3, 4),
+        "value": round(value, 3), "unit": "GiB/s", "n_gpus": ctx.world, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(r["el_max"] / steps * 1e3, 4),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (torch.randint uniform bytes, seed 4 per share), HBM-resident",
         "config": {"workload": f"BASELINE configs[3]: {r['total_chunks']} x 64 KiB chunks, RS(k=10,m=4)="
@@ -651,14 +721,21 @@ def main_c4(args, ctx):
                      "avg_launch_ms": round(r["enc_avg_s"] * 1e3, 4), "launches": r["enc_launches"]},
         "decode_kernel": {"achieved": _gbs(dec_alg, r["dec_avg_s"]), "unit": "GB/s",
                           "erased": list(C4_ERASED), "block_9": "read in place, avail = B - padlen",
+                          "traffic": traffic and load_traffic("decode", "c4"),
                           "algorithmic_bytes_per_launch": dec_alg,
                           "avg_launch_ms": round(r["dec_avg_s"] * 1e3, 4), "launches": r["dec_launches"]},
         "cpu_baseline": None,
     }
-    if ctx.world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, [C4_CHUNK] * 16, C4_K, C4_M, C4_ERASED, decode=False,
+    if ctx.world == 1 and cpu_seconds > 0:
+        res["cpu_baseline"] = cpu_baseline(cpu_seconds, [C4_CHUNK] * 16, C4_K, C4_M, C4_ERASED, decode=False,
                                            what="RS(10,4) encode of 64 KiB chunks (B = 6554, padlen 4)")
-    print(json.dumps(res), flush=True)
+    return res
+
+
+def main_c4(args, ctx):
+    res = c4_result(args, ctx, 0 if args.no_cpu else args.cpu_seconds, args.steps, args.warmup)
+    if res is not None:
+        print(json.dumps(res), flush=True)
 
 
 # ---------------------------------------------------------------- BASELINE configs[4] (C5)
@@ -677,7 +754,7 @@ def c5_sizes(total: int = 1 << 30) -> list[int]:
     return sizes
 
 
-def c5_run(ctx, steps, warmup, total=1 << 30, keep=False, staged=True):
+def c5_run(ctx, steps, warmup, total=1 << 30, keep=False, staged=True, device_only=False):
     """C5 on this rank's share (contiguous chunk range balanced by bytes): the timed steps are
     encode + decode END TO END from pinned host buffers (host=True on Engine.host_empty memory:
     the kernels read the chunks and write parity / reassembled chunks over PCIe); then, outside
@@ -706,15 +783,17 @@ def c5_run(ctx, steps, warmup, total=1 << 30, keep=False, staged=True):
         eng.encode_batch(ed, host, hpar, host=True)
         eng.decode_batch(dd, sn, offs, 0, hout, block_avail=av, host=True)
 
-    for _ in range(warmup):
-        step()
-    if warmup and not np.array_equal(hout[:nbytes], host):
-        raise SystemExit(f"bench c5: rank {ctx.rank} end-to-end round trip mismatch")
-    el_max = timed_region(ctx.dmod, ctx.local, ctx.sync, steps, step)
-    hout[:] = 0
-    step()  # the last timed step's output, checked (a fast wrong answer is not a result)
-    if not np.array_equal(hout[:nbytes], host):
-        raise SystemExit(f"bench c5: rank {ctx.rank} end-to-end output mismatch")
+    el_max = float("nan")
+    if not device_only:  # (device_only: rocprofv3 PMC passes of the device-resident kernels alone)
+        for _ in range(warmup):
+            step()
+        if warmup and not np.array_equal(hout[:nbytes], host):
+            raise SystemExit(f"bench c5: rank {ctx.rank} end-to-end round trip mismatch")
+        el_max = timed_region(ctx.dmod, ctx.local, ctx.sync, steps, step)
+        hout[:] = 0
+        step()  # the last timed step's output, checked (a fast wrong answer is not a result)
+        if not np.array_equal(hout[:nbytes], host):
+            raise SystemExit(f"bench c5: rank {ctx.rank} end-to-end output mismatch")
 
     # device-resident, after the timed region
     src = torch.from_numpy(host).to(ctx.device)
@@ -744,8 +823,7 @@ def c5_run(ctx, steps, warmup, total=1 << 30, keep=False, staged=True):
         pg = np.array(host)
         ppar, pout = np.empty(max(npar, 1), np.uint8), np.empty_like(pg)
         sdd, ssn, soffs, sav = dec_descs_var(sizes, k, m, B, pg.ctypes.data, ppar.ctypes.data, C5_ERASED)
-        os.environ["SEC_REGISTER_MIN"] = "0"
-        try:
+        with eng.options(SEC_REGISTER_MIN=0):  # never page-lock: stage
             eng.encode_batch(ed, pg, ppar, host=True)
             t0 = time.perf_counter()
             for _ in range(3):
@@ -754,8 +832,6 @@ def c5_run(ctx, steps, warmup, total=1 << 30, keep=False, staged=True):
             for _ in range(3):
                 eng.decode_batch(sdd, ssn, soffs, 0, pout, block_avail=sav, host=True)
             t2 = time.perf_counter()
-        finally:
-            os.environ.pop("SEC_REGISTER_MIN")
         if not np.array_equal(pout, pg):
             raise SystemExit(f"bench c5: rank {ctx.rank} staged round trip mismatch")
         res["staged_encode_gibs"] = round(3 * nbytes / (t1 - t0) / GIB, 2)
@@ -765,19 +841,22 @@ def c5_run(ctx, steps, warmup, total=1 << 30, keep=False, staged=True):
     return res
 
 
-def main_c5(args, ctx):
-    r = c5_run(ctx, args.steps, args.warmup, total=args.c5_bytes, staged=not args.no_e2e)
-    value = args.steps * 2 * r["job_bytes"] / r["el_max"] / GIB
+def c5_result(args, ctx, cpu_seconds, steps, warmup, staged=True):
+    """BASELINE configs[4] measured on every rank; rank 0 gets the line's dict (else None)."""
+    r = c5_run(ctx, steps, warmup, total=args.c5_bytes, staged=staged, device_only=args.c5_device_only)
+    value = steps * 2 * r["job_bytes"] / r["el_max"] / GIB
     if ctx.rank != 0:
-        return
+        return None
     enc_gbs, dec_gbs = _gbs(r["enc_alg"], r["enc_avg_s"]), _gbs(r["dec_alg"], r["dec_avg_s"])
     dom_dec = r["dec_avg_s"] >= r["enc_avg_s"]
+    full = ctx.world == 1 and args.c5_bytes == 1 << 30  # the configuration the PMC summary is taken on
     res = {
         "metric": "GiB/s end-to-end RS(8,3) encode+decode of mixed 4 KiB-4 MiB chunks from pinned host memory, "
                   "N MI355X",
-        "value": round(value, 3), "unit": "GiB/s", "n_gpus": ctx.world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(r["el_max"] / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "u8",
+        "value": round(value, 3) if value == value else None, "unit": "GiB/s", "n_gpus": ctx.world,
+        "steps": steps, "warmup": warmup,
+        "ms_per_step": round(r["el_max"] / steps * 1e3, 4) if value == value else None,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (numpy uniform bytes, seed 5 per share) in pinned host memory",
         "config": {"workload": f"BASELINE configs[4]: {sum(r['per_rank_chunks'])} chunks, sizes log-uniform in "
                                f"[4 KiB, 4 MiB] (seed 5), {r['job_bytes']} B, RS(k=8,m=3)=zfec(8,11): encode + "
@@ -790,23 +869,34 @@ def main_c5(args, ctx):
                      "unit": "GB/s",
                      "frac": (round((dec_gbs if dom_dec else enc_gbs) / PEAK_HBM_GBS, 4)
                               if (dec_gbs if dom_dec else enc_gbs) else None),
-                     "traffic": None, "kernel": "decode (reassemble)" if dom_dec else "encode",
+                     "traffic": load_traffic("decode" if dom_dec else "encode", "c5") if full else None,
+                     "kernel": "sec_decode_kernel<3, 1, false, 0> (reassemble)" if dom_dec
+                               else "sec_encode_kernel<3, 1, false>",
                      "algorithmic_bytes_per_launch": r["dec_alg"] if dom_dec else r["enc_alg"],
                      "avg_launch_ms": round((r["dec_avg_s"] if dom_dec else r["enc_avg_s"]) * 1e3, 4)},
         "device_resident": {"encode_GBs": enc_gbs, "encode_gibs": round(r["bytes"] / r["enc_avg_s"] / GIB, 2),
                             "decode_GBs": dec_gbs, "decode_gibs": round(r["bytes"] / r["dec_avg_s"] / GIB, 2),
-                            "encode_ms": round(r["enc_avg_s"] * 1e3, 4), "decode_ms": round(r["dec_avg_s"] * 1e3, 4)},
+                            "encode_ms": round(r["enc_avg_s"] * 1e3, 4), "decode_ms": round(r["dec_avg_s"] * 1e3, 4),
+                            "encode_traffic": load_traffic("encode", "c5") if full else None,
+                            "decode_traffic": load_traffic("decode", "c5") if full else None},
         "staged": ({"encode_gibs": r["staged_encode_gibs"], "decode_gibs": r["staged_decode_gibs"],
                     "path": "pageable numpy buffers staged through the library's pinned slabs (hipMemcpyAsync)"}
                    if "staged_encode_gibs" in r else None),
         "cpu_baseline": None,
     }
-    if ctx.world == 1 and not args.no_cpu:
+    if ctx.world == 1 and cpu_seconds > 0:
         sample = c5_sizes()[:64]
-        res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, sample, C5_K, C5_M, C5_ERASED,
+        res["cpu_baseline"] = cpu_baseline(cpu_seconds, sample, C5_K, C5_M, C5_ERASED,
                                            what=f"(encode + decode {{1,3,5}} erased) of the first 64 C5 chunks "
                                                 f"({sum(sample)} B), RS(8,3)")
-    print(json.dumps(res), flush=True)
+    return res
+
+
+def main_c5(args, ctx):
+    res = c5_result(args, ctx, 0 if args.no_cpu else args.cpu_seconds, args.steps, args.warmup,
+                    staged=not args.no_e2e)
+    if res is not None:
+        print(json.dumps(res), flush=True)
 
 
 # ---------------------------------------------------------------- host-buffer rates (headline line)
@@ -840,11 +930,8 @@ def e2e_rate(eng, nchunks=1024, steps=3) -> dict:
     p0 = np.array(eng.host_paths())
     enc, dec = _e2e_pass(eng, host, par, out, nchunks, steps)
     p1 = np.array(eng.host_paths())
-    os.environ["SEC_REGISTER_MIN"] = "0"
-    try:
+    with eng.options(SEC_REGISTER_MIN=0):  # never page-lock: stage
         senc, sdec = _e2e_pass(eng, host, par, out, nchunks, steps)
-    finally:
-        os.environ.pop("SEC_REGISTER_MIN")
     p2 = np.array(eng.host_paths())
     ph, pp, po = eng.host_empty(host.size), eng.host_empty(nb), eng.host_empty(host.size)
     ph[:] = host

@@ -132,6 +132,20 @@ int sec_ctx_set_timing(sec_ctx *ctx, int enable);
  * kind 0 = encode, 1 = decode, 2 = SHA-1, 3 = bignum (APDP), and clears them. */
 int sec_timing_collect(sec_ctx *ctx, int kind, double *total_ms, int64_t *launches);
 
+/* ---- context options --------------------------------------------------------
+ * The library picks kernels, tile widths and host paths by measured rules and reads no
+ * environment variable.  A test or an A/B tool that must force another choice sets it on
+ * its own context; the context's cached plans are dropped, so the next call is planned
+ * with it.  Names (e.g. "SEC_SYN": -1 cost rule, 0 direct decode, 1 syndrome path;
+ * "SEC_BS"; "SEC_REGISTER_MIN": bytes, 0 = never page-lock) are listed by
+ * sec_option_name(0, 1, ...) up to NULL; their meaning is documented in api.cpp (enum Opt).
+ * No zfec counterpart: the reference has no tuning surface on this path.
+ * SEC_EINVAL for an unknown name or a value out of the option's range. */
+int sec_ctx_set_option(sec_ctx *ctx, const char *name, int64_t value);
+/* The context's value (NULL ctx: the library default). */
+int sec_ctx_get_option(sec_ctx *ctx, const char *name, int64_t *value);
+const char *sec_option_name(int index);
+
 /* ---- matrices (host arithmetic, no device needed) ------------------------ */
 /* Rows k..m-1 of zfec's systematic encode matrix ((m-k)*k bytes, row-major). */
 int sec_encode_matrix(int k, int m, uint8_t *out_rows);

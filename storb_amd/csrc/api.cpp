@@ -116,13 +116,89 @@ struct PinBuf {
 
 size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-size_t env_size(const char *name, size_t dflt)
+// ---- context options (sec_ctx_set_option) --------------------------------------
+// The plan rules below pick kernels, tile widths and host paths from measured defaults.  A
+// test or an A/B tool that must force another choice sets it on ITS context through
+// sec_ctx_set_option; the library reads no environment variable.  Setting an option drops the
+// context's cached plans, so the next call is planned with it.  Names keep the SEC_ prefix the
+// knobs had as environment variables in rounds 1-3 (tools/sweep.py variant strings use them).
+enum Opt {
+    O_SYN,               // syndrome decodes: -1 cost rule, 0 off, 1 wherever they apply
+    O_SYN_FUSED,         // 0: never the one-wave fused kernel
+    O_SYN_RATIO,         // syndrome path taken under this many per mille of the direct estimate
+    O_SYN_SUBSET,        // decodes handed more than k blocks choose the syndrome-friendly subset (0: first k)
+    O_BS,                // bit-sliced encode: -1 rule (bs_shape), 0 off, 1 every shape it has
+    O_BS_LANES,          // lanes of a bit-sliced / syndrome tile (64, 128, 256)
+    O_BS_SPLIT,          // 1: one launch per 16-row group (64,96)
+    O_BS_R8,             // 1: (32,48) as two interleaved groups of 8 rows
+    O_TILE_U,            // 0 rule (1), or 1 / 2 / 4 u-steps per lane
+    O_ENC_LANES,         // 0 rule, or lanes of U = 1 encode tiles
+    O_FULL_LANES,        // 0 rule, or lanes of U = 1 tiles (both kernels)
+    O_WIDE_K8,           // 8-row groups go to the W kernels from k > this
+    O_DEC_REC_KB,        // -1 rule, 0 off, 8: the 8-slot small-batch decode for 4 < k <= 8 too
+    O_DEC_COPY_KB,       // 0, 4 or 8: reassembling decodes of k <= that through the small-batch variant
+    O_RAGGED_KERNEL,     // 1: ragged ends in a separate tail launch (round-1 form)
+    O_EXACT_LANES,       // 1: chunk-sized tiles, one launch per width (round-1 form)
+    O_SHA1_SPLIT,        // -1 rule, 0 one-lane kernel, 1 two-wave kernel
+    O_SLAB_BYTES,        // host staging slab
+    O_SLAB_BYTES_DIGEST, // host staging slab of SHA-1 / bignum calls
+    O_COPY_THREADS,      // 0 rule, or host copy-pool threads
+    O_STAGE_DMA,         // 1: staged EC calls DMA into device memory instead of running on the slabs
+    O_REGISTER_MIN,      // page-lock pageable host buffers for calls moving >= this many bytes (0: never)
+    O_HOST_JOIN,         // 0: the GPU writes every byte of a host reassembly
+    O_COUNT
+};
+
+struct OptSpec {
+    const char *name;
+    int64_t dflt, lo, hi;
+};
+
+constexpr OptSpec kOpts[O_COUNT] = {
+    {"SEC_SYN", -1, -1, 1},
+    {"SEC_SYN_FUSED", 1, 0, 1},
+    {"SEC_SYN_RATIO", 900, 1, 1000000},
+    {"SEC_SYN_SUBSET", 1, 0, 1},
+    {"SEC_BS", -1, -1, 1},
+    {"SEC_BS_LANES", 256, 64, 256},
+    {"SEC_BS_SPLIT", 0, 0, 1},
+    {"SEC_BS_R8", 0, 0, 1},
+    {"SEC_TILE_U", 0, 0, 4},
+    {"SEC_ENC_LANES", 0, 0, 1024},
+    {"SEC_FULL_LANES", 0, 0, 1024},
+    {"SEC_WIDE_K8", 16, 0, 256},
+    {"SEC_DEC_REC_KB", -1, -1, 8},
+    {"SEC_DEC_COPY_KB", 0, 0, 8},
+    {"SEC_RAGGED_KERNEL", 0, 0, 1},
+    {"SEC_EXACT_LANES", 0, 0, 1},
+    {"SEC_SHA1_SPLIT", -1, -1, 1},
+    {"SEC_SLAB_BYTES", (int64_t)64 << 20, (int64_t)1 << 16, (int64_t)1 << 40},
+    {"SEC_SLAB_BYTES_DIGEST", (int64_t)512 << 20, (int64_t)1 << 16, (int64_t)1 << 40},
+    {"SEC_COPY_THREADS", 0, 0, 256},
+    {"SEC_STAGE_DMA", 0, 0, 1},
+    {"SEC_REGISTER_MIN", (int64_t)4 << 20, 0, (int64_t)1 << 62},
+    {"SEC_HOST_JOIN", 1, 0, 1},
+};
+
+struct Options {
+    int64_t v[O_COUNT];
+    Options()
+    {
+        for (int i = 0; i < O_COUNT; ++i)
+            v[i] = kOpts[i].dflt;
+    }
+    int64_t operator[](Opt o) const { return v[o]; }
+    int lanes(Opt o) const { return (int)std::max<int64_t>(64, std::min<int64_t>(256, v[o])) / 64 * 64; }
+};
+
+int opt_index(const char *name)
 {
-    const char *s = getenv(name);
-    if (!s || !*s)
-        return dflt;
-    const long long v = atoll(s);
-    return v > 0 ? (size_t)v : dflt;
+    if (!name)
+        return -1;
+    for (int i = 0; i < O_COUNT; ++i)
+        if (!strcmp(name, kOpts[i].name))
+            return i;
+    return -1;
 }
 
 // ---- plan ---------------------------------------------------------------
@@ -154,6 +230,7 @@ struct SubPlan {
     size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_vdesc = 0, off_vtiles = 0,
            off_masks = 0, off_ftiles = 0;
     uint64_t syn_bytes = 0;  // syndrome scratch of this unit
+    int syn_lanes = 256;     // lanes of the syndrome kernels' tiles (their span per tile)
 };
 
 struct Plan {
@@ -198,28 +275,28 @@ struct Image {
 // zfec(16,24) even, while C4's 6554 B blocks lose 4.7 %; a mixed batch (C5) keeps one tile
 // width, since its large chunks alone at 64 lanes (a second launch) cost it 9 %.  The 1:1
 // copy behind a decode measured no gain from narrower tiles (-1 %).
-// SEC_ENC_LANES / SEC_FULL_LANES override, for A/B.
-int full_lanes(bool decode, bool narrow = false)
+// Options SEC_ENC_LANES / SEC_FULL_LANES override, for A/B.
+int full_lanes(const Options &o, bool decode, bool narrow = false)
 {
-    const size_t dflt = !decode && narrow ? 64 : sec::kLanes;
-    const int l = (int)env_size(decode ? "SEC_FULL_LANES" : "SEC_ENC_LANES", env_size("SEC_FULL_LANES", dflt));
-    return std::max(64, std::min(1024, l)) / 64 * 64;
+    int64_t l = !decode && narrow ? 64 : sec::kLanes;
+    if (o[O_FULL_LANES])
+        l = o[O_FULL_LANES];
+    if (!decode && o[O_ENC_LANES])
+        l = o[O_ENC_LANES];
+    return (int)std::max<int64_t>(64, std::min<int64_t>(1024, l)) / 64 * 64;
 }
 
 // u-steps (4 KiB each) a lane covers per tile.  Larger U = more bytes in flight
-// per lane but more registers; SEC_TILE_U overrides (read per plan build).
+// per lane but more registers; option SEC_TILE_U overrides.
 // The kernels keep all k * U loads of a lane in one batch, so U > 1 only when
 // k * U <= kBatchVecs (wider k goes in U = 1 tiles, batched kBatchVecs blocks at a time).
 // (Full tiles are 256 lanes x 4 KiB x U; see add_work.)
-int pick_u(uint64_t B, int rows, int k)
+int pick_u(const Options &o, int k)
 {
-    const char *env = getenv("SEC_TILE_U");
-    const int forced = env ? atoi(env) : 0;
+    const int forced = (int)o[O_TILE_U];
     // U = 1 by default: one 16 B vector per block per lane, 4 KiB per workgroup and block.
     // Measured on C2 against U = 2 / 4: encode 6.48 vs 6.09 / 5.95 TB/s, decode 6.31 vs
     // 5.79 / 5.62 (profiles/r01_sweep_u.jsonl); U > 1 only on request (SEC_TILE_U).
-    (void)B;
-    (void)rows;
     int u = 1;
     if (forced == 1 || forced == 2 || forced == 4)
         u = forced;
@@ -230,14 +307,13 @@ int pick_u(uint64_t B, int rows, int k)
 
 // Whether a group of `rows` output rows over k blocks runs in the wide (W) kernels, which
 // load the blocks in several batches.  Needed when k * U > kBatchVecs; groups of more than 4
-// rows also go there from k > SEC_WIDE_K8 on (A/B knob), since the W kernels pair blocks for
+// rows also go there from k > SEC_WIDE_K8 on (A/B option), since the W kernels pair blocks for
 // 8-row groups with smaller batches (kernels.hip SEC_WIDE_BATCH).
-bool is_wide(int k, int U, int rows)
+bool is_wide(const Options &o, int k, int U, int rows)
 {
     if (k * U > sec::kBatchVecs)
         return true;
-    const int k8 = (int)env_size("SEC_WIDE_K8", sec::kBatchVecs);  // read per plan build
-    return U == 1 && rows > 4 && k > k8;
+    return U == 1 && rows > 4 && k > o[O_WIDE_K8];
 }
 
 using Bins = std::map<std::tuple<int, int, int, int, int>, std::vector<sec::Tile>>;  // (kind, rows, U, lanes, wide)
@@ -249,24 +325,23 @@ uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 // VGPRs, 8 waves per SIMD instead of 4.  Measured on C3 recover-only (tools/sweep.py
 // --recover, env held during the timed calls): 6.42 against 5.91 TB/s; the same batches cost
 // the reassembling decode 4 %, and 8-slot batches for k <= 8 measured 1.4 % slower on RS(8,3)
-// recover-only (profiles/r02_dec_small_kb_ab.jsonl).  SEC_DEC_REC_KB=0 turns it off, =8 adds
-// the 8-slot variant for 4 < k <= 8 (A/B); read per plan build.
-int dec_small_kb(int k)
+// recover-only (profiles/r02_dec_small_kb_ab.jsonl).  Option SEC_DEC_REC_KB = 0 turns it off,
+// = 8 adds the 8-slot variant for 4 < k <= 8 (A/B).
+int dec_small_kb(const Options &o, int k)
 {
-    const char *e = getenv("SEC_DEC_REC_KB");
-    if (e && e[0] == '0')
+    if (o[O_DEC_REC_KB] == 0)
         return 0;
     if (k <= 4)
         return 4;
-    return e && e[0] == '8' && k <= 8 ? 8 : 0;
+    return o[O_DEC_REC_KB] == 8 && k <= 8 ? 8 : 0;
 }
 
-// A/B only: SEC_DEC_COPY_KB = 4 or 8 runs the reassembling (copying) decodes of chunks with
-// k <= that through the small-batch variant too (default off: 4-slot batches measured -4 %)
-int dec_copy_kb(int k)
+// A/B only: option SEC_DEC_COPY_KB = 4 or 8 runs the reassembling (copying) decodes of chunks
+// with k <= that through the small-batch variant too (default off: 4-slot batches measured -4 %)
+int dec_copy_kb(const Options &o, int k)
 {
-    const size_t v = env_size("SEC_DEC_COPY_KB", 0);
-    return (v == 4 || v == 8) && (size_t)k <= v ? (int)v : 0;
+    const int64_t v = o[O_DEC_COPY_KB];
+    return (v == 4 || v == 8) && k <= v ? (int)v : 0;
 }
 
 // Syndrome decode (kernels_bs.hip) for a chunk that lost e data blocks, when its shape has the
@@ -285,9 +360,9 @@ int dec_copy_kb(int k)
 //   two:    phase 1 P (k - e) 8.75 + (k - e) e + 15 e over P touched parity groups, the data
 //           read once per group (BW 5.0, or 4.0 when P = 2); phase 2 2.75 e per touched 16-row
 //           group + e^2 + 14 e, 2 e rows of syndrome traffic; R 14.5.
-// A syndrome path is taken when its estimate is under SEC_SYN_RATIO (default 0.9) of the direct
-// one.  SEC_SYN=0 / 1 turns the syndrome paths off / forces them wherever they apply (fused
-// where eligible); SEC_SYN_FUSED=0 turns the fused kernel off.  All read per plan build.
+// A syndrome path is taken when its estimate is under SEC_SYN_RATIO (default 900 per mille) of
+// the direct one.  Options SEC_SYN = 0 / 1 turn the syndrome paths off / force them wherever they
+// apply (fused where eligible); SEC_SYN_FUSED = 0 turns the fused kernel off.
 double vperm_ops(int rows, int slots)
 {
     double v = 0;
@@ -297,11 +372,10 @@ double vperm_ops(int rows, int slots)
 }
 
 // shape of the syndrome kernels for this chunk, or -1 (direct); `fused`: the one-wave kernel
-int syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies, bool &fused)
+int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, bool copies, bool &fused)
 {
     fused = false;
-    const char *env = getenv("SEC_SYN");
-    if (env && env[0] == '0')
+    if (o[O_SYN] == 0)
         return -1;
     const int sh = sec_syn_shape(c.k, c.m);
     if (sh < 0 || e < 1 || c.B < 16 || c.B > 0xFFFFFFFFull - 8192 || c.padlen >= c.B)
@@ -315,9 +389,8 @@ int syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies, bool 
             g16 |= 1ull << (s / NR2);
         }
     const int P = __builtin_popcountll(touched);
-    const char *fz = getenv("SEC_SYN_FUSED");
-    const bool can_fuse = P == 1 && e <= 16 && !(fz && fz[0] == '0');
-    if (env && env[0] == '1') {
+    const bool can_fuse = P == 1 && e <= 16 && o[O_SYN_FUSED] != 0;
+    if (o[O_SYN] == 1) {
         fused = can_fuse;
         return sh;
     }
@@ -331,8 +404,7 @@ int syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies, bool 
     const double fuse = can_fuse ? t(KE * (8.75 + E) + 15 * E + 2.75 * E * __builtin_popcountll(g8) + E * E + 14 * E,
                                      17, 4.0 * (k + out), 5.0)
                                  : 1e30;
-    const char *ratio = getenv("SEC_SYN_RATIO");
-    const double lim = (ratio && *ratio ? atof(ratio) : 0.9) * direct;
+    const double lim = (double)o[O_SYN_RATIO] / 1000.0 * direct;
     if (std::min(two, fuse) >= lim)
         return -1;
     fused = fuse <= two;
@@ -348,8 +420,9 @@ int syn_choice(const sec_dec_chunk &c, const int *idx, int e, bool copies, bool 
 // by byte by the last tile of each row group (Tile::ntail): a separate one-thread-per-
 // byte launch cost C4 13-17 % on top of its main kernels (profiles/r01_c4_kernel_stats).
 // Chunks with valid < 16 get no tile: all of [0, B) becomes one-thread tail items.
-void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B, int64_t valid,
-              int rows_total, int k, bool decode, uint64_t start = 0, bool narrow = false, int small_kb = 0)
+void add_work(const Options &o, Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B,
+              int64_t valid, int rows_total, int k, bool decode, uint64_t start = 0, bool narrow = false,
+              int small_kb = 0)
 {
     if (B == 0)
         return;
@@ -361,17 +434,17 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
             tail.push_back(sec::TailItem{chunk, (uint32_t)t});
         return;
     }
-    const bool ragged_kernel = env_size("SEC_RAGGED_KERNEL", 0) != 0;  // A/B: the old tail launch
-    const bool exact = env_size("SEC_EXACT_LANES", 0) != 0;              // A/B: chunk-sized tiles
+    const bool ragged_kernel = o[O_RAGGED_KERNEL] != 0;  // A/B: the old tail launch
+    const bool exact = o[O_EXACT_LANES] != 0;            // A/B: chunk-sized tiles
     if (ragged_kernel)
         for (uint64_t t = v; t < B; ++t)
             tail.push_back(sec::TailItem{chunk, (uint32_t)t});
     for (int g = 0; g < ngroups; ++g) {
         const int r0 = g * sec::kMaxRows;
         const int rows = std::min(sec::kMaxRows, rows_total - r0);
-        const int U = pick_u(B, rows, k);
-        const int wide = is_wide(k, U, rows);  // U == 1 then (pick_u)
-        const int flanes = U == 1 ? std::min(full_lanes(decode, narrow), sec::max_lanes(rows, 1)) : sec::kLanes;
+        const int U = pick_u(o, k);
+        const int wide = is_wide(o, k, U, rows);  // U == 1 then (pick_u)
+        const int flanes = U == 1 ? std::min(full_lanes(o, decode, narrow), sec::max_lanes(rows, 1)) : sec::kLanes;
         const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * U;
         // kind: 0, or the small-batch decode variant's batch (the group's kernel, see dec_small_kb)
         const int kind = small_kb && U == 1 && !wide && k <= small_kb ? small_kb : 0;
@@ -388,8 +461,8 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
                 full.push_back(sec::Tile{chunk, (uint32_t)(from + i * step), (uint32_t)r0, 0});
                 last = &full.back();
             }
-            const int ul = std::min(full_lanes(decode, narrow), sec::max_lanes(rows, 1));
-            auto &ones = bins[{kind, rows, 1, ul, is_wide(k, 1, rows)}];
+            const int ul = std::min(full_lanes(o, decode, narrow), sec::max_lanes(rows, 1));
+            auto &ones = bins[{kind, rows, 1, ul, is_wide(o, k, 1, rows)}];
             for (uint64_t t0 = from + nfull * step; t0 < v; t0 += (uint64_t)sec::kLaneBytes * ul) {  // U > 1 remainder
                 ones.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
                 last = &ones.back();
@@ -409,7 +482,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
             for (uint64_t t0 = nfull * step; t0 < v;) {
                 const uint64_t lanes =
                     std::min<uint64_t>(sec::max_lanes(rows, 1), round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
-                auto &bin = bins[{0, rows, 1, (int)lanes, is_wide(k, 1, rows)}];
+                auto &bin = bins[{0, rows, 1, (int)lanes, is_wide(o, k, 1, rows)}];
                 bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
                 last = &bin.back();
                 t0 += lanes * sec::kLaneBytes;
@@ -426,15 +499,14 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
 // sec_encode_kernel tile.  Tiles of SEC_BS_LANES lanes (default 256 = 8 KiB of each block).
 // A shape of several row groups ((64,96): 2 x 16 rows) runs them in one launch, a run of 8
 // tiles of each group in turn, so the tiles that read the same blocks share an XCD's L2
-// (SEC_BS_SPLIT=1: one launch per group instead).  SEC_BS=0 turns the kernel off (then the
-// v_perm rows), SEC_BS=1 uses it for every shape it has; SEC_BS_R8=1 takes (32,48) in two
-// groups of 8 rows.  All read per plan build.
+// (option SEC_BS_SPLIT = 1: one launch per group instead).  SEC_BS = 0 turns the kernel off
+// (then the v_perm rows), SEC_BS = 1 uses it for every shape it has; SEC_BS_R8 = 1 takes
+// (32,48) in two groups of 8 rows.
 constexpr int kBsAllGroups = 99;  // Group::U of an interleaved launch of every row group
 
-int bs_shape(int k, int m, uint64_t B)
+int bs_shape(const Options &o, int k, int m, uint64_t B)
 {
-    const char *e = getenv("SEC_BS");
-    if (e && e[0] == '0')
+    if (o[O_BS] == 0)
         return -1;
     if (B < 16 || B > 0xFFFFFFFFull - 8192)
         return -1;
@@ -442,19 +514,19 @@ int bs_shape(int k, int m, uint64_t B)
     // here), and C4's RS(10,4) (+0-4 %, whole 65536-chunk job +2 %); the other p <= 4 shapes
     // measured 5-10 % slower here (C5's RS(8,3), zfec(8,12) on 4 MiB chunks; r02_bs_ab.jsonl)
     const int p = m - k;
-    if (!(e && e[0] == '1') && p < 8 && !(k == 10 && m == 14))
+    if (o[O_BS] != 1 && p < 8 && !(k == 10 && m == 14))
         return -1;
-    if (k == 32 && m == 48 && env_size("SEC_BS_R8", 0))
+    if (k == 32 && m == 48 && o[O_BS_R8])
         return sec_bs_shape(k, m, 8);
     return sec_bs_shape(k, m);
 }
 
-void add_bs_work(Bins &bins, uint32_t chunk, uint64_t B, int shape)
+void add_bs_work(const Options &o, Bins &bins, uint32_t chunk, uint64_t B, int shape)
 {
-    const int lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
+    const int lanes = o.lanes(O_BS_LANES);
     const uint64_t step = (uint64_t)sec_bs_span() * (lanes / 64);
     const int ng = sec_bs_groups(shape);
-    if (ng > 1 && !env_size("SEC_BS_SPLIT", 0)) {  // flatten() interleaves the groups
+    if (ng > 1 && !o[O_BS_SPLIT]) {  // flatten() interleaves the groups
         auto &bin = bins[{3, shape, kBsAllGroups, lanes, 0}];
         for (uint64_t t0 = 0; t0 < B; t0 += step)
             bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
@@ -571,6 +643,7 @@ constexpr int kSlots = 2;
 
 struct sec_ctx {
     int device = 0;
+    Options opt;  // sec_ctx_set_option
     hipStream_t own = nullptr;
     hipStream_t ext = nullptr;
     bool timing = false;
@@ -617,7 +690,7 @@ sec::CopyPool &pool(sec_ctx *ctx)
 {
     if (!ctx->pool) {
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        const int n = (int)env_size("SEC_COPY_THREADS", std::min(7u, std::max(1u, hw / 2)));
+        const int n = ctx->opt[O_COPY_THREADS] ? (int)ctx->opt[O_COPY_THREADS] : (int)std::min(7u, std::max(1u, hw / 2));
         ctx->pool.reset(new sec::CopyPool(n));
     }
     return *ctx->pool;
@@ -759,12 +832,11 @@ int timing_end(sec_ctx *ctx, hipEvent_t a, int kind, hipStream_t s)
 
 // SHA-1 kernel for a launch's messages: sec_sha1_split_kernel (message schedule on a second
 // wave) when the messages are few and long, so the round chains are the bound; else one lane
-// per message.  SEC_SHA1_SPLIT = 0 / 1 forces it (read per plan build).
-bool sha1_split(const std::vector<sec::MsgDesc> &md)
+// per message.  Option SEC_SHA1_SPLIT = 0 / 1 forces it.
+bool sha1_split(const Options &o, const std::vector<sec::MsgDesc> &md)
 {
-    const char *e = getenv("SEC_SHA1_SPLIT");
-    if (e && (e[0] == '0' || e[0] == '1'))
-        return e[0] == '1';
+    if (o[O_SHA1_SPLIT] >= 0)
+        return o[O_SHA1_SPLIT] == 1;
     if (md.empty())
         return false;
     uint64_t blocks = 0;
@@ -840,8 +912,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             ib[i] = chunks[i].n;
         // SHA-1 is one sequential chain per piece: a slab's hashing takes as long as
         // one piece, whatever the slab size, so digest mode uses few large slabs
-        ranges = slabs_of(ib, digest ? env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20)
-                                     : env_size("SEC_SLAB_BYTES", (size_t)64 << 20));
+        ranges = slabs_of(ib, (size_t)ctx->opt[digest ? O_SLAB_BYTES_DIGEST : O_SLAB_BYTES]);
     } else {
         ranges.emplace_back(0, nchunks);
     }
@@ -889,17 +960,17 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             }
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
-            const int bs = p > 0 ? bs_shape(c.k, c.m, B) : -1;
+            const int bs = p > 0 ? bs_shape(ctx->opt, c.k, c.m, B) : -1;
             if (bs >= 0)
-                add_bs_work(bins, (uint32_t)(i - c0), B, bs);
+                add_bs_work(ctx->opt, bins, (uint32_t)(i - c0), B, bs);
             else if (p > 0)
-                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, 0, narrow);
+                add_work(ctx->opt, bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, 0, narrow);
         }
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles, false);
         sp.ntail = (uint32_t)tail.size();
         sp.nmsgs = (uint32_t)msgs.size();
-        sp.sha_split = sha1_split(msgs);
+        sp.sha_split = sha1_split(ctx->opt, msgs);
         sp.dig_off = sp.out_bytes;  // host mode: digests follow the slab's parity
         if (host)
             sp.out_bytes += (uint64_t)msgs.size() * 20;
@@ -1015,7 +1086,8 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             for (int s = 0; s < k && whole && !host; ++s)
                 whole = idx[s] == k - 1 || slot_avail(c, block_avail, L.perm[L.first[i] + s]) >= c.B;
             bool fz = false;
-            const int sh = syn_of[i] = whole ? syn_choice(c, idx, (int)miss.size(), !recover && !nocopy, fz) : -1;
+            const int sh = syn_of[i] =
+                whole ? syn_choice(ctx->opt, c, idx, (int)miss.size(), !recover && !nocopy, fz) : -1;
             fuse_of[i] = fz;
             if (sh >= 0)
                 continue;  // the syndrome path's matrices are compile-time (its scalings: the plan image)
@@ -1063,7 +1135,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         std::vector<uint64_t> ib((size_t)nchunks);
         for (int64_t i = 0; i < nchunks; ++i)
             ib[i] = (uint64_t)chunks[i].k * chunks[i].B;
-        ranges = slabs_of(ib, env_size("SEC_SLAB_BYTES", (size_t)64 << 20));
+        ranges = slabs_of(ib, (size_t)ctx->opt[O_SLAB_BYTES]);
     } else {
         ranges.emplace_back(0, nchunks);
     }
@@ -1073,6 +1145,8 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         SubPlan sp;
         sp.c0 = c0;
         sp.c1 = c1;
+        // the syndrome tiles' span is built for this lane count; the launches take it from here
+        const int syn_lanes = sp.syn_lanes = ctx->opt.lanes(O_BS_LANES);
         std::vector<sec::DecDesc> descs((size_t)(c1 - c0));
         std::vector<uint64_t> soff;
         std::vector<uint32_t> srow, mrow, savail;
@@ -1087,7 +1161,6 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         std::vector<sec::SolveDesc> vdescs;
         std::vector<uint64_t> masks;                                    // w / z scalings (scale_mask)
         std::map<std::string, std::pair<uint32_t, uint32_t>> mask_of;  // pattern -> (wq0, zq0)
-        const int syn_lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
         for (int64_t i = c0; i < c1; ++i) {
             const sec_dec_chunk &c = chunks[i];
             const uint64_t base = L.first[i];
@@ -1216,8 +1289,8 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                         for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
                             vt.push_back(sec::Tile{vi, (uint32_t)t, (uint32_t)(g * NR2), 0u});
             } else if (nout > 0 && !(nocopy && e_of[i] == 0)) {
-                add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true, 0, false,
-                         recover || nocopy ? dec_small_kb(c.k) : dec_copy_kb(c.k));
+                add_work(ctx->opt, bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true, 0, false,
+                         recover || nocopy ? dec_small_kb(ctx->opt, c.k) : dec_copy_kb(ctx->opt, c.k));
             }
         }
         std::vector<sec::Tile> tiles, stl, vtl;
@@ -1289,7 +1362,7 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::SynDesc *sd = plan.meta.as<sec::SynDesc>(sp.off_sdesc);
     const sec::Tile *st = plan.meta.as<sec::Tile>(sp.off_stiles);
     const sec::SynSlots ss{plan.meta.as<uint64_t>(sp.off_ssoff), plan.meta.as<uint32_t>(sp.off_ssavail), masks};
-    const int lanes = std::max(64, std::min(256, (int)env_size("SEC_BS_LANES", 256))) / 64 * 64;
+    const int lanes = sp.syn_lanes;  // what the plan's tiles were built for
     const sec::Tile *ft = plan.meta.as<sec::Tile>(sp.off_ftiles);
     for (const auto &g : sp.synf) {
         int e = sec_launch_decode_bs(g.first, lanes, blocks, out, sd, ft + g.second.first, g.second.second, ss, s);
@@ -1381,7 +1454,7 @@ int run_pipeline(sec_ctx *ctx, Plan &plan, Gather gather, Scatter scatter, Launc
 {
     RC(slots_init(ctx));
     CK(hipEventRecord(ctx->meta_ev, ctx->stream()));  // behind the plan upload / table expansion
-    direct = direct && env_size("SEC_STAGE_DMA", 0) == 0;
+    direct = direct && ctx->opt[O_STAGE_DMA] == 0;
     size_t i = 0;
     for (const SubPlan &sp : plan.subs) {
         Slot &sl = ctx->slots[i++ % kSlots];
@@ -1476,7 +1549,7 @@ int msg_batch(sec_ctx *ctx, Plan &plan, const sec_msg *msgs, int64_t nmsgs, uint
                 sp.in_bytes += av;
             }
             sp.nmsgs = (uint32_t)md.size();
-            sp.sha_split = sha1_split(md);
+            sp.sha_split = sha1_split(ctx->opt, md);
             sp.out_bytes = (uint64_t)md.size() * out_per;
             sp.off_msgs = img.put(md.data(), md.size() * sizeof(sec::MsgDesc));
             if (seg_bytes) {
@@ -1724,6 +1797,39 @@ int sec_ctx_set_timing(sec_ctx *ctx, int enable)
     return SEC_OK;
 }
 
+int sec_ctx_set_option(sec_ctx *ctx, const char *name, int64_t value)
+{
+    const int i = opt_index(name);
+    if (!ctx || i < 0)
+        return SEC_EINVAL;
+    if (value < kOpts[i].lo || value > kOpts[i].hi)
+        return SEC_EINVAL;
+    if (ctx->opt.v[i] == value)
+        return SEC_OK;
+    RC(set_dev(ctx));
+    RC(drain_all(ctx));  // nothing in flight may still use a plan or pool built the old way
+    ctx->opt.v[i] = value;
+    for (Plan *p : {&ctx->enc_plan, &ctx->dec_plan, &ctx->sha_plan, &ctx->bn_plan})
+        p->valid = false;
+    if (i == O_COPY_THREADS)
+        ctx->pool.reset();
+    return SEC_OK;
+}
+
+int sec_ctx_get_option(sec_ctx *ctx, const char *name, int64_t *value)
+{
+    const int i = opt_index(name);
+    if (i < 0 || !value)
+        return SEC_EINVAL;
+    *value = ctx ? ctx->opt.v[i] : kOpts[i].dflt;  // NULL ctx: the default
+    return SEC_OK;
+}
+
+const char *sec_option_name(int index)
+{
+    return index >= 0 && index < O_COUNT ? kOpts[index].name : nullptr;
+}
+
 int sec_timing_collect(sec_ctx *ctx, int kind, double *total_ms, int64_t *launches)
 {
     if (!ctx || kind < 0 || kind > 3 || !total_ms || !launches)
@@ -1858,7 +1964,7 @@ public:
 
     // 0: staged; 1: every range in persistently pinned memory (zero-copy, nothing locked);
     // 2: zero-copy on pages this call locked (plus persistently pinned ones)
-    int acquire(const std::vector<HostRange> &rs, bool may_lock = true)
+    int acquire(const std::vector<HostRange> &rs, int64_t register_min, bool may_lock = true)
     {
         TransientLocks &tl = transient_locks();
         std::lock_guard<std::mutex> g(tl.mu);
@@ -1876,7 +1982,7 @@ public:
         }
         if (pg.empty())
             return 1;
-        if (!may_lock || getenv_zero("SEC_REGISTER_MIN") || total < env_size("SEC_REGISTER_MIN", (size_t)4 << 20))
+        if (!may_lock || register_min <= 0 || total < (uint64_t)register_min)
             return 0;
         std::sort(pg.begin(), pg.end());
         // ranges less than kGap apart are locked as one (e.g. around a decode's erased blocks);
@@ -1928,11 +2034,6 @@ public:
 private:
     static constexpr uintptr_t kPageMask = 4095;
     static constexpr uintptr_t kGap = (uintptr_t)4 << 20;
-    static bool getenv_zero(const char *name)
-    {
-        const char *v = getenv(name);
-        return v && v[0] == '0' && v[1] == 0;
-    }
     void unlock_all(TransientLocks &tl)  // tl.mu held
     {
         for (auto &q : locked_) {
@@ -1950,7 +2051,7 @@ private:
 // locked for the call (`lock`), or staged.  True = run the device path on host addresses.
 bool host_direct(sec_ctx *ctx, const std::vector<HostRange> &rs, HostLock &lock, unsigned flags)
 {
-    switch (lock.acquire(rs, !(flags & SEC_F_STAGED))) {
+    switch (lock.acquire(rs, ctx->opt[O_REGISTER_MIN], !(flags & SEC_F_STAGED))) {
     case 1: ++ctx->zero_copy_calls; return true;
     case 2: ++ctx->registered_calls; return true;
     default: ++ctx->staged_calls; return false;
@@ -2088,7 +2189,7 @@ int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *di
     if (!ctx)
         return SEC_EINVAL;
     return msg_batch(ctx, ctx->sha_plan, msgs, nmsgs, digests, 20, flags,
-                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 2, "sec_sha1_kernel", 0,
+                     (size_t)ctx->opt[O_SLAB_BYTES_DIGEST], 2, "sec_sha1_kernel", 0,
                      [](const uint8_t *base0, const Plan &plan, const SubPlan &sp, size_t, uint8_t *o, hipStream_t s) {
                          return sec_launch_sha1(base0, nullptr, plan.meta.as<sec::MsgDesc>(sp.off_msgs), sp.nmsgs, o,
                                                 s, sp.sha_split);
@@ -2272,7 +2373,7 @@ int sec_bn_reduce_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs
     const sec::BnKey *dk = key->dk.as<sec::BnKey>();
     bool prepared = false;
     return msg_batch(ctx, ctx->bn_plan, msgs, nmsgs, out, 256, flags,
-                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 3, "sec_bn_reduce", kSegBytes,
+                     (size_t)ctx->opt[O_SLAB_BYTES_DIGEST], 3, "sec_bn_reduce", kSegBytes,
                      [&](const uint8_t *base0, const Plan &plan, const SubPlan &sp, size_t idx, uint8_t *o,
                          hipStream_t s) {
                          if (!prepared) {
@@ -2299,7 +2400,7 @@ int sec_apdp_tag_batch(sec_ctx *ctx, const sec_bn_key *key, const sec_msg *msgs,
     const uint32_t *table = key->table.as<uint32_t>();
     bool prepared = false;
     return msg_batch(ctx, ctx->bn_plan, msgs, nmsgs, tags, 256, flags,
-                     env_size("SEC_SLAB_BYTES_DIGEST", (size_t)512 << 20), 3, "sec_apdp_tag", kSegBytes,
+                     (size_t)ctx->opt[O_SLAB_BYTES_DIGEST], 3, "sec_apdp_tag", kSegBytes,
                      [&](const uint8_t *base0, const Plan &plan, const SubPlan &sp, size_t idx, uint8_t *o,
                          hipStream_t s) {
                          if (!prepared) {
@@ -2428,10 +2529,9 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
         return SEC_EINVAL;
     // A reassembly of host buffers leaves the present primaries to the host (the copy pool, from
     // the caller's blocks into `out`) and moves only what the GPU computes over PCIe: the
-    // recovered rows, e * B per chunk instead of the whole chunk (SEC_HOST_JOIN=0: the GPU
-    // writes every output byte, the A/B).
-    const char *hj = getenv("SEC_HOST_JOIN");
-    const bool join = host && !recover && !(hj && hj[0] == '0');
+    // recovered rows, e * B per chunk instead of the whole chunk (option SEC_HOST_JOIN = 0: the
+    // GPU writes every output byte, the A/B).
+    const bool join = host && !recover && ctx->opt[O_HOST_JOIN] != 0;
     // pinned (or lockable) caller buffers: the device path on them directly (see encode_impl)
     HostLock lock(ctx->stream());
     bool direct = false;

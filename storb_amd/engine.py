@@ -14,6 +14,7 @@ There is no CPU compute path: every call goes to the HIP kernels; construction r
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -81,7 +82,7 @@ _TIMING_KINDS = {"encode": 0, "decode": 1, "sha1": 2, "bignum": 3}
 class Engine:
     """A libstorbec context on one device.  Not thread-safe; use ``get_engine()`` per thread."""
 
-    def __init__(self, device: int | None = None, lib_path: str | None = None):
+    def __init__(self, device: int | None = None, lib_path: str | None = None, options: dict | None = None):
         self.lib = _lib.load(lib_path)
         self.device = default_device() if device is None else int(device)
         h = ctypes.c_void_p()
@@ -89,6 +90,8 @@ class Engine:
         if rc:
             raise ECRuntimeError(f"cannot create HIP context on device {self.device}: {_lib.strerror(rc)}")
         self._ctx = h
+        for k, v in (options or {}).items():  # sec_ctx_set_option: forced plan choices (tests, A/B)
+            self.set_option(k, int(v))
 
     def _check(self, rc: int) -> None:
         check(rc, self.lib)
@@ -124,6 +127,29 @@ class Engine:
         self._check(self.lib.sec_timing_collect(self._ctx, _TIMING_KINDS[kind], ctypes.byref(ms),
                                           ctypes.byref(n)))
         return ms.value, n.value
+
+    # -- context options (sec_ctx_set_option) ----------------------------------
+    def set_option(self, name: str, value: int) -> None:
+        """Force a plan choice on this context (tests, A/B tools); see include/storb_ec.h.
+        The library reads no environment variable: an option holds only for this engine."""
+        self._check(self.lib.sec_ctx_set_option(self._ctx, name.encode(), int(value)))
+
+    def option(self, name: str) -> int:
+        v = ctypes.c_int64(0)
+        self._check(self.lib.sec_ctx_get_option(self._ctx, name.encode(), ctypes.byref(v)))
+        return v.value
+
+    @contextlib.contextmanager
+    def options(self, **opts):
+        """``with eng.options(SEC_SYN=0): ...``: the options set for the block, restored after."""
+        old = {k: self.option(k) for k in opts}
+        try:
+            for k, v in opts.items():
+                self.set_option(k, v)
+            yield self
+        finally:
+            for k, v in old.items():
+                self.set_option(k, v)
 
     # -- device-resident batches --------------------------------------------
     def encode_batch(self, descs: np.ndarray, src, parity, *, host: bool = False, asynchronous: bool = False,
@@ -408,6 +434,23 @@ def encode_matrix(k: int, m: int) -> bytes:
     out = np.zeros(max((m - k) * k, 1), dtype=np.uint8)
     check(lib.sec_encode_matrix(k, m, _ptr(out)))
     return out[: (m - k) * k].tobytes()
+
+
+def option_names() -> list[str]:
+    """Every context option the library knows (sec_option_name)."""
+    lib = _lib.load()
+    out, i = [], 0
+    while (n := lib.sec_option_name(i)) is not None:
+        out.append(n.decode())
+        i += 1
+    return out
+
+
+def option_default(name: str) -> int:
+    lib = _lib.load()
+    v = ctypes.c_int64(0)
+    check(lib.sec_ctx_get_option(None, name.encode(), ctypes.byref(v)))
+    return v.value
 
 
 def decode_matrix(k: int, m: int, sharenums) -> tuple[bytes, list[int]]:

@@ -10,6 +10,7 @@ checks pass only if its descriptors are right.  Never used by the product or by 
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import time
@@ -78,6 +79,13 @@ class OracleEngine:
                 data = full[:k * B - padlen]
             ctypes.memmove(o + int(d["out_off"]), data, len(data))
         self._record("decode", t0)
+
+    def option(self, name):
+        return -1 if name in ("SEC_BS", "SEC_SYN") else 0
+
+    @contextlib.contextmanager
+    def options(self, **opts):  # the oracle has no plan choices to force
+        yield self
 
     def host_empty(self, nbytes):
         return np.empty(int(nbytes), dtype=np.uint8)

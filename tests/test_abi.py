@@ -91,3 +91,22 @@ def test_easyfec_preconditions_host_side():
     with pytest.raises(easyfec.Error):
         easyfec.Decoder(4, 6).decode([b"ab"] * 3, [0, 1, 2], 0)
     assert issubclass(easyfec.Error, Exception) and not issubclass(easyfec.Error, engine.ECRuntimeError)
+
+
+def test_options_listed_with_defaults_and_no_environment_reads():
+    """plan choices are context options (sec_ctx_set_option), not environment
+    variables read by the library.  Every option is listed with its default; an unknown name or an
+    out-of-range value is SEC_EINVAL; the product sources call no getenv."""
+    from storb_amd._build import CSRC, HEADERS, SOURCES
+
+    names = engine.option_names()
+    assert {"SEC_SYN", "SEC_BS", "SEC_BS_LANES", "SEC_REGISTER_MIN", "SEC_HOST_JOIN"} <= set(names)
+    assert engine.option_default("SEC_SYN") == -1 and engine.option_default("SEC_BS_LANES") == 256
+    assert engine.option_default("SEC_REGISTER_MIN") == 4 << 20
+    lib = _lib.load()
+    v = ctypes.c_int64(0)
+    assert lib.sec_ctx_get_option(None, b"SEC_NOPE", ctypes.byref(v)) == _lib.SEC_EINVAL
+    assert lib.sec_ctx_set_option(None, b"SEC_SYN", 1) == _lib.SEC_EINVAL  # no context
+    for name in SOURCES + HEADERS:
+        with open(os.path.join(CSRC, name)) as f:
+            assert not re.search(r"\bgetenv\s*\(", f.read()), name

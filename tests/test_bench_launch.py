@@ -28,7 +28,8 @@ def _run(args, extra_env=None, timeout=240):
 
 @pytest.mark.timeout(300)
 def test_bench_gpus2_c2c3_spawns_two_ranks():
-    p, lines = _run(["--gpus", "2", "--steps", "2", "--warmup", "1", "--chunks", "3", "--no-cpu", "--no-e2e"],
+    p, lines = _run(["--gpus", "2", "--steps", "2", "--warmup", "1", "--chunks", "3", "--no-cpu", "--no-e2e",
+                     "--c4-chunks", "12", "--c5-bytes", str(6 << 20), "--c5-steps", "1"],
                     {"STORB_STUB_SLOW_RANK": "1"})
     assert p.returncode == 0, p.stderr[-3000:]
     assert len(lines) == 1, p.stdout  # rank 0 only
@@ -39,6 +40,11 @@ def test_bench_gpus2_c2c3_spawns_two_ranks():
     assert j["ms_per_step"] >= 50
     assert j["value"] == pytest.approx(2 * 2 * 2 * 3 * (1 << 20) / (j["ms_per_step"] * 2 / 1e3) / (1 << 30), rel=0.02)
     assert j["decode_recover_only_kernel"]["launches"] == 10
+    # configs[3] and [4] ride on the same line, split over the same two ranks
+    assert j["c4"]["config"]["per_rank_chunks"] == [6, 6] and j["c4"]["n_gpus"] == 2
+    assert j["c4"]["roofline"]["traffic"] is None  # a PMC summary applies to the full job at N = 1 only
+    assert sum(j["c5"]["config"]["per_rank_chunks"]) == len(__import__("bench").c5_sizes(6 << 20))
+    assert j["c4"]["cpu_baseline"] is None and j["c5"]["cpu_baseline"] is None  # N > 1
 
 
 @pytest.mark.timeout(300)
@@ -86,3 +92,21 @@ def test_bench_gpus1_c4_cpu_baseline_line():
     assert j["n_gpus"] == 1 and j["config"]["backend"] is None
     cb = j["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and "RS(10,4)" in cb["sample"]
+    host = cb["host"]  # the box, beside the thread count
+    assert host["os_cpu_count"] >= 1 and host["affinity_cpus"] >= cb["cores"] and "cgroup_cpu_quota" in host
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus1_c2c3_nests_c4_c5_with_cpu_baselines():
+    """N = 1 headline line: configs[3] and [4] measured in the same run, each with its roofline and
+    its own CPU baseline."""
+    p, lines = _run(["--steps", "1", "--warmup", "1", "--chunks", "2", "--no-e2e", "--cpu-seconds", "0.2",
+                     "--sub-cpu-seconds", "0.2", "--c4-chunks", "8", "--c5-bytes", str(4 << 20), "--c5-steps", "1"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = json.loads(lines[0])
+    assert j["cpu_baseline"]["kind"] == "port"
+    for sub, what in (("c4", "RS(10,4)"), ("c5", "RS(8,3)")):
+        s = j[sub]
+        assert s["n_gpus"] == 1 and s["roofline"]["bound"] == "hbm" and s["roofline"]["achieved"] > 0
+        assert s["cpu_baseline"]["value"] > 0 and what in s["cpu_baseline"]["sample"]
+    assert len(j["lib_digest"]) == 64

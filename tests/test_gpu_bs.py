@@ -40,22 +40,20 @@ def _sizes(k, rng):
 
 MODES = {
     "default": {},  # the kernel for the shapes with >= 8 parity rows, v_perm / xb for the rest
-    "all256": {"SEC_BS": "1"},
-    "all128": {"SEC_BS": "1", "SEC_BS_LANES": "128"},
-    "all64": {"SEC_BS": "1", "SEC_BS_LANES": "64"},
-    "split": {"SEC_BS": "1", "SEC_BS_SPLIT": "1"},  # (64,96): one launch per row group
-    "r8": {"SEC_BS": "1", "SEC_BS_R8": "1"},  # (32,48) in two interleaved groups of 8 rows
-    "off": {"SEC_BS": "0"},
+    "all256": {"SEC_BS": 1},
+    "all128": {"SEC_BS": 1, "SEC_BS_LANES": 128},
+    "all64": {"SEC_BS": 1, "SEC_BS_LANES": 64},
+    "split": {"SEC_BS": 1, "SEC_BS_SPLIT": 1},  # (64,96): one launch per row group
+    "r8": {"SEC_BS": 1, "SEC_BS_R8": 1},  # (32,48) in two interleaved groups of 8 rows
+    "off": {"SEC_BS": 0},
 }
 
 
 @pytest.mark.parametrize("mode", list(MODES))
-def test_encode_bit_sliced_shapes_host(mode, monkeypatch):
+def test_encode_bit_sliced_shapes_host(mode):
     from storb_amd.engine import Engine
 
-    for k, v in MODES[mode].items():
-        monkeypatch.setenv(k, v)
-    eng = Engine(0)  # its own plan cache: the knobs are read when a plan is built
+    eng = Engine(0, options=MODES[mode])  # context options (sec_ctx_set_option)
     rng = random.Random(mode)
     chunks, km = [], []
     for k, m in BS_SHAPES + [(4, 6), (10, 14)]:
@@ -79,13 +77,12 @@ def test_encode_bit_sliced_shapes_host(mode, monkeypatch):
 
 
 @pytest.mark.parametrize("k,m", BS_SHAPES)
-def test_encode_bit_sliced_device_padded_stride(k, m, monkeypatch):
+def test_encode_bit_sliced_device_padded_stride(k, m):
     """Device-resident chunks back to back (unaligned block starts), parity blocks at a stride
     larger than B: the kernel writes exactly [0, B) of each parity block and nothing between."""
     from storb_amd.engine import Engine
 
-    monkeypatch.setenv("SEC_BS", "1")
-    engine = Engine(0)
+    engine = Engine(0, options={"SEC_BS": 1})
     rng = random.Random(k * 7 + m)
     n = 4096 * k + 2 * k + 3 if k > 3 else 40000
     B = -(-n // k)

@@ -126,14 +126,12 @@ def _oracle_recovered(data, k, m, keep):
 
 @pytest.mark.parametrize("kb", ["default", "0", "8"])
 @pytest.mark.parametrize("k,m", [(1, 2), (2, 3), (3, 5), (4, 6), (5, 7), (8, 11), (10, 14), (16, 24), (16, 40), (32, 48)])
-def test_recover_only_vs_oracle_device(k, m, kb, monkeypatch):
+def test_recover_only_vs_oracle_device(k, m, kb):
     """kb: the copy-free decodes' small-batch kernel variants (api.cpp dec_small_kb): default
     (4-slot batches for k <= 4), "0" (off: 16-slot batches), "8" (also 8-slot for k <= 8)."""
     from storb_amd.engine import Engine
 
-    if kb != "default":
-        monkeypatch.setenv("SEC_DEC_REC_KB", kb)
-    engine = Engine(0)  # its own plan cache: the knob is read when a plan is built
+    engine = Engine(0, options={} if kb == "default" else {"SEC_DEC_REC_KB": int(kb)})
     rng = random.Random(1000 + k * m)
     sizes = [n for n in (k * k, 4096 * k - 3, 65536, 65536 + 9, 6554 * k - 1, 300007)
              if -(-n // k) * (k - 1) <= n]
@@ -341,16 +339,15 @@ def test_fuzz_mixed_shapes_erasures_one_batch(engine):
 
 
 @pytest.mark.parametrize("mode", ["staged", "locked", "pinned"])
-def test_fuzz_host_reassembly_join(mode, monkeypatch):
+def test_fuzz_host_reassembly_join(mode):
     """Host-buffer reassembly (the host copies the present primaries, the GPU returns only the
     recovered rows) on each host path, randomized: mixed (k, m), random survivors in random
     order (parity-only ones included), block k-1 read in place with its short avail; the output
     buffer is pre-filled so every byte must be written; against the source bytes."""
     from storb_amd.engine import Engine
 
-    if mode == "staged":
-        monkeypatch.setenv("SEC_REGISTER_MIN", "0")  # never page-lock: stage through the slabs
-    eng = Engine(0)
+    # staged: never page-lock, stage through the slabs
+    eng = Engine(0, options={"SEC_REGISTER_MIN": 0} if mode == "staged" else {})
     try:
         rng = random.Random(77)
         shapes, sizes = [], []

@@ -275,16 +275,14 @@ def test_encode_ragged_tails_many_shapes(engine):
         assert p == oracle_parity(c, k, m), (k, m, len(c))
 
 
-def test_host_pipeline_many_slabs(monkeypatch):
+def test_host_pipeline_many_slabs():
     """SEC_F_HOST batches cut into many 1 MiB slabs (chunks straddling slab limits, a chunk
     bigger than a slab, two pipeline slots cycling) — encode, decode and SHA-1."""
     import hashlib
 
     from storb_amd.engine import Engine
 
-    monkeypatch.setenv("SEC_SLAB_BYTES", str(1 << 20))
-    monkeypatch.setenv("SEC_SLAB_BYTES_DIGEST", str(1 << 20))
-    eng = Engine(0)  # fresh context: plans are built with the small slabs
+    eng = Engine(0, options={"SEC_SLAB_BYTES": 1 << 20, "SEC_SLAB_BYTES_DIGEST": 1 << 20})
     try:
         rng = random.Random(31)
         sizes = [rng.randrange(1000, 600000) for _ in range(30)] + [3 << 20, 5, 4096 * 10 + 3]
@@ -452,7 +450,7 @@ def test_registered_buffer_host_path():
         eng.close()
 
 
-def test_pageable_large_calls_lock_pages_per_call(monkeypatch):
+def test_pageable_large_calls_lock_pages_per_call():
     """Large host calls on pageable memory page-lock the caller's ranges for the call, run the
     kernels on them, and unlock them: results exact, the same buffers usable again (a second
     call locks them again), and SEC_REGISTER_MIN=0 forces the staged path with equal bytes."""
@@ -475,12 +473,11 @@ def test_pageable_large_calls_lock_pages_per_call(monkeypatch):
             want = oracle_parity(src[ci * n:(ci + 1) * n].tobytes(), k, m)
             assert pars[0][ci * (m - k) * B:(ci + 1) * (m - k) * B].tobytes() == b"".join(want)
         assert np.array_equal(pars[0], pars[1])
-        monkeypatch.setenv("SEC_REGISTER_MIN", "0")
-        par3 = np.zeros_like(pars[0])
-        eng.encode_batch(d, src, par3, host=True)
+        with eng.options(SEC_REGISTER_MIN=0):
+            par3 = np.zeros_like(pars[0])
+            eng.encode_batch(d, src, par3, host=True)
         assert np.array_equal(par3, pars[0])
         assert eng.host_paths() == (0, 2, 1)
-        monkeypatch.delenv("SEC_REGISTER_MIN")
         # decode from the (pageable) data + parity arrays, blocks 3 (short) and 1 erased
         keep = [0, 2, 4, 5]
         dd = np.zeros(nch, dtype=DEC_DTYPE)
@@ -506,7 +503,7 @@ def test_pageable_large_calls_lock_pages_per_call(monkeypatch):
         eng.close()
 
 
-def test_threads_pageable_locking_interleaved(monkeypatch):
+def test_threads_pageable_locking_interleaved():
     """Per-call page locking under concurrent engines: big calls whose input and
     parity ranges are 2 MiB apart (locked as one registration, gap included) run beside calls
     whose buffers live in that gap.  A range touching another call's transient registration
@@ -516,7 +513,6 @@ def test_threads_pageable_locking_interleaved(monkeypatch):
 
     from storb_amd.engine import Engine
 
-    monkeypatch.setenv("SEC_REGISTER_MIN", str(1 << 20))
     MiB = 1 << 20
     big = np.random.default_rng(5).integers(0, 256, 64 * MiB, dtype=np.uint8)
     k, m = 4, 6
@@ -524,7 +520,7 @@ def test_threads_pageable_locking_interleaved(monkeypatch):
 
     def run(lo_in, n_in, lo_par, iters, seed):
         try:
-            eng = Engine(0)
+            eng = Engine(0, options={"SEC_REGISTER_MIN": MiB})
             try:
                 nch = n_in // MiB
                 d = np.zeros(nch, dtype=ENC_DTYPE)
@@ -592,16 +588,14 @@ def test_largest_block_size(engine):
 
 
 @pytest.mark.parametrize("bs", ["default", "off"])
-def test_encode_wide_policy_shapes(bs, monkeypatch):
+def test_encode_wide_policy_shapes(bs):
     """The policy's wide shapes (64,96), (32,48), (16,24) (files of 1 GiB to 1 TiB, SURVEY
     Appendix B) through the default plan (the bit-sliced compile-time-matrix kernel) and with it
     off (SEC_BS=0: the v_perm rows), against the oracle: ragged tails, padded last blocks, tiny
     and unaligned B, mixed with other shapes in one batch."""
     from storb_amd.engine import Engine
 
-    if bs == "off":
-        monkeypatch.setenv("SEC_BS", "0")
-    eng = Engine(0)  # its own plan cache: the knobs are read when a plan is built
+    eng = Engine(0, options={"SEC_BS": 0} if bs == "off" else {})
     rng = random.Random(96)
     chunks, km = [], []
     for k, m in [(64, 96), (32, 48), (16, 24), (64, 96), (32, 48)]:

@@ -107,7 +107,7 @@ def test_piece_api_ids():
 
 
 @pytest.mark.parametrize("split", ["1", "0"])
-def test_sha1_split_kernel_forced(split, monkeypatch):
+def test_sha1_split_kernel_forced(split):
     """The two-wave SHA-1 kernel (schedule wave + rounds wave, kernels.hip
     sec_sha1_split_kernel), forced on (SEC_SHA1_SPLIT=1) and off, on messages of every length
     class: empty, sub-block, exact blocks, long, zero tails past avail, ragged workgroups (more
@@ -115,8 +115,7 @@ def test_sha1_split_kernel_forced(split, monkeypatch):
     host path, and fused after an encode; against hashlib."""
     from storb_amd.engine import Engine
 
-    monkeypatch.setenv("SEC_SHA1_SPLIT", split)
-    eng = Engine(0)  # its own plan cache: the choice is made when a plan is built
+    eng = Engine(0, options={"SEC_SHA1_SPLIT": int(split)})
     rng = np.random.default_rng(11)
     buf = torch.from_numpy(rng.integers(0, 256, 1 << 22, dtype=np.uint8)).cuda()
     host = buf.cpu().numpy().tobytes()

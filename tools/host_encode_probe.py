@@ -29,10 +29,8 @@ def main():
     rng = np.random.default_rng(1)
     base = rng.integers(0, 256, 64 * cs, dtype=np.uint8).tobytes()
     res = {"chunk_bytes": cs, "k": k, "m": m, "unit": "ms per call, median of 40"}
-    for label, env in (("lock", {}), ("staged", {"SEC_REGISTER_MIN": "0"})):
-        os.environ.pop("SEC_REGISTER_MIN", None)
-        os.environ.update(env)
-        eng = Engine(0)
+    for label, env in (("lock", {}), ("staged", {"SEC_REGISTER_MIN": 0})):
+        eng = Engine(0, options=env)
         for mode in ("fresh", "reused"):
             ts, ks = [], []
             same = base[:cs]
@@ -50,7 +48,6 @@ def main():
             res[f"{label}_{mode}"] = round(statistics.median(ts) * 1e3, 3)
             res[f"{label}_{mode}_kernel"] = round(statistics.median(ks), 3)
         eng.close()
-    os.environ.pop("SEC_REGISTER_MIN", None)
     t0 = time.perf_counter()
     for i in range(8):
         bytes(base[i * cs:(i + 1) * cs])

@@ -43,18 +43,15 @@ def main():
         bufs[(nm, ln)] = (buf, msgs, {})
     engs = {}
     for mode in ("1", "0"):
-        os.environ["SEC_SHA1_SPLIT"] = mode
-        e = engs[mode] = Engine(0)
+        e = engs[mode] = Engine(0, options={"SEC_SHA1_SPLIT": int(mode)})
         for s in SHAPES:  # one engine per mode; each shape's plan is built here with that mode
             _, msgs, dig = bufs[s]
             dig[mode] = torch.empty(s[0] * 20, dtype=torch.uint8, device="cuda")
-    os.environ.pop("SEC_SHA1_SPLIT")
     samples = {(s, m): [] for s in SHAPES for m in engs}
     for _ in range(rounds):
         for s in SHAPES:
             _, msgs, dig = bufs[s]
             for m, e in engs.items():
-                os.environ["SEC_SHA1_SPLIT"] = m  # a plan rebuilt for another shape keeps the mode
                 e.sha1_batch(msgs, dig[m])
                 e.set_timing(True)
                 for _ in range(5):
@@ -63,7 +60,6 @@ def main():
                 e.set_timing(False)
                 ms, n = e.collect_timing("sha1")
                 samples[(s, m)].append(ms / n)
-    os.environ.pop("SEC_SHA1_SPLIT", None)
     for s in SHAPES:
         _, _, dig = bufs[s]
         assert torch.equal(dig["1"], dig["0"]), s

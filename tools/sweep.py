@@ -123,7 +123,8 @@ def main():
     ap.add_argument("--recover", action="store_true", help="also time recover-only decodes (not c5)")
     ap.add_argument("--erased", default="", help="erased block numbers, e.g. 1,3 (not c5; default per workload)")
     a = ap.parse_args()
-    # a variant is TAG or TAG@ENV=VALUE: the TAG build, with ENV set while its plan is built
+    # a variant is TAG or TAG@OPT=VALUE[+OPT2=V2]: the TAG build, with those context options
+    # (sec_ctx_set_option) on its engine
     specs = a.variants.split(",")
     tags = sorted({v.split("@")[0] for v in specs})
     libs = build(tags)
@@ -176,13 +177,11 @@ def main():
     engines = {}
     for v, u in configs:
         t, _, env = v.partition("@")
-        os.environ["SEC_TILE_U"] = str(u)
-        if env:
-            os.environ[env.split("=")[0]] = env.split("=")[1]
-        e = Engine(0, lib_path=libs[t])
-        # builds + caches this engine's plans with U (and env).  The flags are part of the
-        # plan key, so these calls must be asynchronous like the timed ones: a synchronous
-        # call here would leave the timed calls to rebuild their plan without the overrides.
+        # the variant's options hold on its own engine (sec_ctx_set_option) for every call
+        opts = {"SEC_TILE_U": u}
+        for kv in filter(None, env.split("+")):
+            opts[kv.split("=")[0]] = int(kv.split("=")[1])
+        e = Engine(0, lib_path=libs[t], options=opts)
         out.zero_()
         e.encode_batch(ed, src, par, asynchronous=True)
         e.decode_batch(dd, sn, offs, 0, out, block_avail=av, asynchronous=True)
@@ -191,26 +190,11 @@ def main():
         e.sync()
         assert torch.equal(out, src), (v, u)
         engines[(v, u)] = e
-        if env:
-            os.environ.pop(env.split("=")[0])
-    os.environ.pop("SEC_TILE_U", None)
     samples = {c: ([], [], []) for c in configs}
-    def set_env(v, on):
-        # a config's ENV=VALUE stays set while its calls run: a ctx caches one plan per kind, so
-        # a workload that alternates decode modes rebuilds plans inside the timed loop, and those
-        # rebuilds must see the config's knobs too
-        env = v[0].partition("@")[2]
-        if env:
-            if on:
-                os.environ[env.split("=")[0]] = env.split("=")[1]
-            else:
-                os.environ.pop(env.split("=")[0], None)
 
     for _ in range(a.rounds):
         for c in configs:
             e = engines[c]
-            set_env(c, True)
-            os.environ["SEC_TILE_U"] = str(c[1])
             e.set_timing(True)
             for _ in range(a.reps):
                 e.encode_batch(ed, src, par, asynchronous=True)
@@ -230,8 +214,6 @@ def main():
                 e.set_timing(False)
                 ms, nl = e.collect_timing("decode")
                 samples[c][2].append(ms / nl)
-            set_env(c, False)
-    os.environ.pop("SEC_TILE_U", None)
     # the timed calls must have produced the same bytes (a fast wrong kernel is not a result)
     ref_par = par.clone()
     engines[configs[0]].encode_batch(ed, src, ref_par, asynchronous=True)

@@ -63,7 +63,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="direct@SEC_SYN=0,syn@SEC_SYN=1,auto",
-                    help="name@ENV=V+ENV2=V2[/tag]: environment per variant, optionally a prebuilt variant library "
+                    help="name@OPT=V+OPT2=V2[/tag]: context options per variant, optionally a prebuilt variant library "
                          "storb_amd/lib/libstorbec_<tag>.so (storb_amd._build.build(defines=..., tag=...))")
     ap.add_argument("--cases", default="")
     a = ap.parse_args()
@@ -72,7 +72,7 @@ def main():
         v, _, tag = v.partition("/")
         name, _, env = v.partition("@")
         lib = os.path.join(ROOT, "storb_amd", "lib", f"libstorbec_{tag}.so") if tag else None
-        variants.append((name, dict(kv.split("=") for kv in env.split("+")) if env else {}, lib))
+        variants.append((name, {kv.split("=")[0]: int(kv.split("=")[1]) for kv in env.split("+")} if env else {}, lib))
     sel = [c for c in CASES if not a.cases or any(t in c[0] for t in a.cases.split(";"))]
     for name, k, m, n, nch, e, *seed in sel:
         src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
@@ -91,39 +91,29 @@ def main():
         paths = {}
         for _ in range(a.rounds):
             for vname, env, lib in variants:
-                old = {key: os.environ.get(key) for key in env}
-                os.environ.pop("SEC_SYN", None) if not env else None
-                os.environ.update(env)
-                try:
-                    eng = Engine(0, lib_path=lib)
-                    for mode, args in (("reassemble", (dd, sn, offs, av, out, False)),
-                                       ("recover_only", (rd, rsn, roffs, rav, rec, True))):
-                        d_, s_, o_, a_, dst, recov = args
-                        dst.zero_()
-                        eng.decode_batch(d_, s_, o_, 0, dst, block_avail=a_, recover_only=recov)
-                        if not recov:
-                            assert torch.equal(out, src), (name, vname)
-                        else:  # recovered rows against the (zero-padded) source blocks
-                            r3 = rec.view(nch, e, B)
-                            s3 = torch.nn.functional.pad(src.view(nch, n), (0, k * B - n)).view(nch, k, B)
-                            for j, blk in enumerate(lost):
-                                assert torch.equal(r3[:, j], s3[:, blk]), (name, vname, blk)
-                        eng.set_timing(True)
-                        for _ in range(a.reps):
-                            eng.decode_batch(d_, s_, o_, 0, dst, block_avail=a_, recover_only=recov, asynchronous=True)
-                        eng.sync()
-                        eng.set_timing(False)
-                        ms, nl = eng.collect_timing("decode")
-                        alg = nch * (k * B + (e * B if recov else n))
-                        res[vname][mode].append(alg / (ms / 1e3 / a.reps) / 1e12)
-                    paths[vname] = eng.decode_paths()
-                    eng.close()
-                finally:
-                    for key, val in old.items():
-                        if val is None:
-                            os.environ.pop(key, None)
-                        else:
-                            os.environ[key] = val
+                eng = Engine(0, lib_path=lib, options=env)  # the variant's options (sec_ctx_set_option)
+                for mode, args in (("reassemble", (dd, sn, offs, av, out, False)),
+                                   ("recover_only", (rd, rsn, roffs, rav, rec, True))):
+                    d_, s_, o_, a_, dst, recov = args
+                    dst.zero_()
+                    eng.decode_batch(d_, s_, o_, 0, dst, block_avail=a_, recover_only=recov)
+                    if not recov:
+                        assert torch.equal(out, src), (name, vname)
+                    else:  # recovered rows against the (zero-padded) source blocks
+                        r3 = rec.view(nch, e, B)
+                        s3 = torch.nn.functional.pad(src.view(nch, n), (0, k * B - n)).view(nch, k, B)
+                        for j, blk in enumerate(lost):
+                            assert torch.equal(r3[:, j], s3[:, blk]), (name, vname, blk)
+                    eng.set_timing(True)
+                    for _ in range(a.reps):
+                        eng.decode_batch(d_, s_, o_, 0, dst, block_avail=a_, recover_only=recov, asynchronous=True)
+                    eng.sync()
+                    eng.set_timing(False)
+                    ms, nl = eng.collect_timing("decode")
+                    alg = nch * (k * B + (e * B if recov else n))
+                    res[vname][mode].append(alg / (ms / 1e3 / a.reps) / 1e12)
+                paths[vname] = eng.decode_paths()
+                eng.close()
         row = {"case": name, "k": k, "m": m, "chunk": n, "chunks": nch, "lost": list(lost),
                "parity_kept": [s for s in sn[:k].tolist() if s >= k]}
         for vname, r in res.items():
