@@ -67,8 +67,8 @@ enum sec_status {
                           encode / decode lies in pinned memory mapped at the same address
                           on the device (sec_host_alloc, sec_host_register, hipHostMalloc),
                           the kernels read and write it directly over PCIe: no staging
-                          copy.  Pageable buffers of a large call (SEC_REGISTER_MIN bytes,
-                          default 4 MiB, in ranges of >= 1 MiB on average) are page-locked
+                          copy.  Pageable buffers of a large call (context option SEC_REGISTER_MIN
+                          bytes, default 4 MiB, in ranges of >= 1 MiB on average) are page-locked
                           for the call and used the same way; otherwise (or if locking
                           fails) they are staged through pinned slabs and device scratch.
                           sec_ctx_host_paths counts which path each call took        */
@@ -145,6 +145,16 @@ int sec_ctx_set_option(sec_ctx *ctx, const char *name, int64_t value);
 /* The context's value (NULL ctx: the library default). */
 int sec_ctx_get_option(sec_ctx *ctx, const char *name, int64_t *value);
 const char *sec_option_name(int index);
+
+/* ---- choosing the blocks to decode from (host logic, no device needed) ---------------
+ * A caller holding n > k blocks of a chunk (storb's validator fetches every data and parity
+ * piece: validator.py:1556-1604, 1631) passes their sharenums; pick[0..k) receives the
+ * positions of the k blocks to hand to sec_decode_batch(_ex): every present primary, then
+ * parity rows from as few of the decode kernels' row groups as possible (the cheapest decode;
+ * any k distinct blocks give the same bytes).  Replaces the reference's `pieces[:k]`
+ * (storb/util/piece.py:189-191).  Out-of-range and repeated sharenums are never chosen;
+ * SEC_ENBLOCKS when fewer than k distinct valid ones are present. */
+int sec_decode_choose(int k, int m, int64_t n, const int32_t *sharenums, int32_t *pick);
 
 /* ---- matrices (host arithmetic, no device needed) ------------------------ */
 /* Rows k..m-1 of zfec's systematic encode matrix ((m-k)*k bytes, row-major). */

@@ -84,6 +84,7 @@ _SIGS = {
     "sec_ctx_set_option": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int64]),
     "sec_ctx_get_option": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "sec_option_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "sec_decode_choose": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int64, _vp, _vp]),
     "sec_encode_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp]),
     "sec_decode_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp]),
     "sec_encode_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_uint]),

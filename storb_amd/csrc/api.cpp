@@ -126,7 +126,6 @@ enum Opt {
     O_SYN,               // syndrome decodes: -1 cost rule, 0 off, 1 wherever they apply
     O_SYN_FUSED,         // 0: never the one-wave fused kernel
     O_SYN_RATIO,         // syndrome path taken under this many per mille of the direct estimate
-    O_SYN_SUBSET,        // decodes handed more than k blocks choose the syndrome-friendly subset (0: first k)
     O_BS,                // bit-sliced encode: -1 rule (bs_shape), 0 off, 1 every shape it has
     O_BS_LANES,          // lanes of a bit-sliced / syndrome tile (64, 128, 256)
     O_BS_SPLIT,          // 1: one launch per 16-row group (64,96)
@@ -158,7 +157,6 @@ constexpr OptSpec kOpts[O_COUNT] = {
     {"SEC_SYN", -1, -1, 1},
     {"SEC_SYN_FUSED", 1, 0, 1},
     {"SEC_SYN_RATIO", 900, 1, 1000000},
-    {"SEC_SYN_SUBSET", 1, 0, 1},
     {"SEC_BS", -1, -1, 1},
     {"SEC_BS_LANES", 256, 64, 256},
     {"SEC_BS_SPLIT", 0, 0, 1},
@@ -1847,6 +1845,79 @@ int sec_timing_collect(sec_ctx *ctx, int kind, double *total_ms, int64_t *launch
     *launches = (int64_t)ctx->pending[kind].size();
     *total_ms = tot;
     ctx->pending[kind].clear();
+    return SEC_OK;
+}
+
+// Which k of the n blocks a caller holds to decode from (storb's validator fetches every data and
+// parity piece of a chunk, /root/reference/storb/validator/validator.py:1556-1604, 1631; the
+// reference then takes the first k in piece order, storb/util/piece.py:189-191).  Any k distinct
+// blocks give the same bytes, so the choice is free, and it decides the decode's cost:
+//   * every present primary (its bytes are copied, not computed);
+//   * the e = k - primaries parity rows from as few bit-sliced row groups as possible
+//     (sec_bs_rows(sec_syn_shape(k, m)) rows each: 16 for the policy's wide shapes): one group
+//     holding e present rows lets an e <= 16 decode take the fused one-wave syndrome kernel
+//     (api.cpp syn_choice), where rows spread over both groups of zfec(64,96) read the data once
+//     per group; groups with the most present rows first, lowest rows first within a group.
+// Entries that are out of range or repeat an earlier sharenum are never chosen.  pick[0..k) =
+// positions in `sharenums`, in ascending sharenum order.  SEC_ENBLOCKS when fewer than k
+// distinct valid blocks are present.
+int sec_decode_choose(int k, int m, int64_t n, const int32_t *sharenums, int32_t *pick)
+{
+    if (!pick || n < 0 || (n > 0 && !sharenums))
+        return SEC_EINVAL;
+    if (k < 1 || m < k || m > 256)
+        return SEC_EKM;
+    int pos[256];
+    for (int j = 0; j < 256; ++j)
+        pos[j] = -1;
+    int distinct = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int s = sharenums[i];
+        if (s >= 0 && s < m && pos[s] < 0) {
+            pos[s] = (int)i;
+            ++distinct;
+        }
+    }
+    if (distinct < k)
+        return SEC_ENBLOCKS;
+    bool take[256] = {false};
+    int have = 0;
+    for (int j = 0; j < k; ++j)
+        if (pos[j] >= 0) {
+            take[j] = true;
+            ++have;
+        }
+    const int e = k - have, p = m - k;
+    if (e > 0) {
+        const int sh = sec_syn_shape(k, m);
+        const int G = sh >= 0 ? sec_bs_rows(sh) : p;
+        const int ng = (p + G - 1) / G;
+        std::vector<int> cnt((size_t)ng, 0);
+        for (int r = 0; r < p; ++r)
+            cnt[(size_t)(r / G)] += pos[k + r] >= 0;
+        std::vector<int> order((size_t)ng);
+        for (int g = 0; g < ng; ++g)
+            order[(size_t)g] = g;
+        int one = -1;  // lowest group that alone holds e present rows
+        for (int g = 0; g < ng && one < 0; ++g)
+            if (cnt[(size_t)g] >= e)
+                one = g;
+        if (one >= 0)
+            order = {one};
+        else
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cnt[(size_t)a] > cnt[(size_t)b]; });
+        int need = e;
+        for (int g : order)
+            for (int r = g * G; r < std::min(p, (g + 1) * G) && need > 0; ++r)
+                if (pos[k + r] >= 0) {
+                    take[k + r] = true;
+                    --need;
+                }
+    }
+    int o = 0;
+    for (int j = 0; j < m; ++j)
+        if (take[j])
+            pick[o++] = pos[j];
     return SEC_OK;
 }
 

@@ -436,6 +436,20 @@ def encode_matrix(k: int, m: int) -> bytes:
     return out[: (m - k) * k].tobytes()
 
 
+def choose_blocks(k: int, m: int, sharenums) -> list[int] | None:
+    """Positions (ascending sharenum) of the k blocks to decode from when more are at hand
+    (sec_decode_choose: every present primary, then parity rows from as few of the decode
+    kernels' row groups as possible), or None when fewer than k distinct valid sharenums."""
+    lib = _lib.load()
+    sn = np.ascontiguousarray([int(x) for x in sharenums], dtype=np.int32)
+    pick = np.zeros(max(k, 1), dtype=np.int32)
+    rc = lib.sec_decode_choose(int(k), int(m), sn.size, _ptr(sn), _ptr(pick))
+    if rc == _lib.SEC_ENBLOCKS:
+        return None
+    check(rc, lib)
+    return pick[:k].tolist()
+
+
 def option_names() -> list[str]:
     """Every context option the library knows (sec_option_name)."""
     lib = _lib.load()

@@ -12,6 +12,10 @@ Deliberate differences (documented in DESIGN.md §Boundary):
   reproduces the reference's behaviour exactly.
 * ``reconstruct_data`` decodes all chunks in ONE batched GPU call instead of one zfec call
   per chunk (same output; the "not enough pieces" ValueError is raised before any decode).
+* handed more than k pieces, ``decode_chunk`` decodes from the k the library picks
+  (``sec_decode_choose``: every present primary, then parity pieces from as few of the decode
+  kernels' row groups as possible) instead of the first k (piece.py:189-191); any k distinct
+  pieces give the same bytes, the choice only sets the decode's cost.
 * the two ``print()`` calls per piece in ``encode_chunk`` (piece.py:140,151) are debug
   logs here.
 * extra batch entry points ``encode_chunks`` / ``decode_chunks`` for callers that can hand
@@ -46,7 +50,7 @@ from pydantic import BaseModel, ConfigDict, Field
 
 from .constants import MAX_PIECE_SIZE, MIN_PIECE_SIZE, PIECE_LENGTH_OFFSET, PIECE_LENGTH_SCALING
 from .easyfec import Decoder, Encoder, Error
-from .engine import check_decode_item, get_engine
+from .engine import check_decode_item, choose_blocks, get_engine
 
 logger = logging.getLogger(__name__)
 
@@ -58,6 +62,9 @@ __all__ = [
 ]
 
 PREFETCH_PIECE_IDS = True  # encode_chunk hashes its pieces on a thread pool (see module doc)
+# decode_chunk & co. handed more than k pieces decode from the k that sec_decode_choose picks
+# (False: the first k in piece order, as the reference's piece.py:189-191; same bytes either way)
+CHOOSE_BLOCKS = True
 # ... for chunks of at least this many bytes.  The validator's pattern (encode_chunk, then
 # piece_hash of every piece; tools/prefetch_study.py, profiles/r02_prefetch_study.json), us per
 # chunk without / with: 256 KiB 217 / 217, 512 KiB 395 / 303, 1 MiB 744 / 411, 4 MiB 2754 / 918.
@@ -536,6 +543,14 @@ def _sharenums(encoded_chunk: EncodedChunk, positional: bool):
             use = pieces[:k]
             return [p.data for p in use], list(range(k))
         return [p.data for p in pieces], list(range(len(pieces)))
+    if len(pieces) > k and CHOOSE_BLOCKS:
+        # the validator hands over every piece it fetched (validator.py:1556-1604, 1631): decode
+        # from the k the library picks (every present primary, then parity rows of one decode
+        # row group where possible: the fused syndrome kernel), not the first k; same bytes
+        pick = choose_blocks(k, encoded_chunk.m, [p.piece_idx for p in pieces])
+        if pick is not None:
+            use = [pieces[i] for i in pick]
+            return [p.data for p in use], [p.piece_idx for p in use]
     use = pieces[:k] if len(pieces) > k else pieces
     return [p.data for p in use], [p.piece_idx for p in use]
 

@@ -36,7 +36,37 @@ CASES = [
     ("zfec(64,96) 1MiB x1024, 24 lost (random, parity random)", 64, 96, 1 << 20, 1024, 24, 2),
     ("zfec(32,48) 1MiB x1024, 12 lost (random, parity random)", 32, 48, 1 << 20, 1024, 12, 3),
     ("zfec(32,48) 1MiB x1024, 16 lost (random)", 32, 48, 1 << 20, 1024, 16, 4),
+    # every one of the m blocks fetched, a random 10-30 % of them lost (data and parity): the decode
+    # from the first k present in block order (the reference's pieces[:k], piece.py:189-191) and
+    # from the k sec_decode_choose picks; e = 0 is the lost-data count then
+    ("zfec(64,96) 1MiB x1024, 20 % of blocks lost, first k", 64, 96, 1 << 20, 1024, 0, 11, 0.2, "first"),
+    ("zfec(64,96) 1MiB x1024, 20 % of blocks lost, chosen k", 64, 96, 1 << 20, 1024, 0, 11, 0.2, "choose"),
+    ("zfec(64,96) 1MiB x1024, 15 % of blocks lost, first k", 64, 96, 1 << 20, 1024, 0, 12, 0.15, "first"),
+    ("zfec(64,96) 1MiB x1024, 15 % of blocks lost, chosen k", 64, 96, 1 << 20, 1024, 0, 12, 0.15, "choose"),
+    ("zfec(64,96) 1MiB x1024, 30 % of blocks lost, first k", 64, 96, 1 << 20, 1024, 0, 13, 0.3, "first"),
+    ("zfec(64,96) 1MiB x1024, 30 % of blocks lost, chosen k", 64, 96, 1 << 20, 1024, 0, 13, 0.3, "choose"),
+    ("zfec(32,48) 1MiB x1024, 20 % of blocks lost, first k", 32, 48, 1 << 20, 1024, 0, 14, 0.2, "first"),
+    ("zfec(32,48) 1MiB x1024, 20 % of blocks lost, chosen k", 32, 48, 1 << 20, 1024, 0, 14, 0.2, "choose"),
 ]
+
+
+def lost_fraction(k, m, seed, frac, how):
+    """(lost data blocks, erased block numbers) for `frac` of the m blocks lost (seeded; each
+    pattern holds >= k blocks), the decoder keeping the first k present ("first") or
+    sec_decode_choose's k ("choose")."""
+    import random
+
+    from storb_amd.engine import choose_blocks
+
+    rng = random.Random(seed)
+    while True:
+        gone = set(rng.sample(range(m), int(round(frac * m))))
+        present = [j for j in range(m) if j not in gone]
+        if len(present) >= k:
+            break
+    keep = present[:k] if how == "first" else [present[i] for i in choose_blocks(k, m, present)]
+    lost = tuple(j for j in range(k) if j not in keep)
+    return lost, tuple(j for j in range(m) if j not in keep)
 
 
 def erased_of(k, m, e, seed):
@@ -75,11 +105,15 @@ def main():
         variants.append((name, {kv.split("=")[0]: int(kv.split("=")[1]) for kv in env.split("+")} if env else {}, lib))
     sel = [c for c in CASES if not a.cases or any(t in c[0] for t in a.cases.split(";"))]
     for name, k, m, n, nch, e, *seed in sel:
+        if len(seed) == 3:  # a fraction of all m blocks lost, first or chosen k
+            lost, erased = lost_fraction(k, m, *seed)
+            e = len(lost)
+        else:
+            lost, erased = erased_of(k, m, e, seed[0] if seed else 0)
         src = torch.randint(0, 256, (nch * n,), dtype=torch.uint8, device="cuda")
         B = -(-n // k)
         ed, _ = bench.enc_descs(nch, n, k, m)
         par = torch.empty(nch * (m - k) * B, dtype=torch.uint8, device="cuda")
-        lost, erased = erased_of(k, m, e, seed[0] if seed else 0)
         eng0 = Engine(0)
         eng0.encode_batch(ed, src, par)
         eng0.close()
