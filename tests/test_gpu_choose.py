@@ -1,0 +1,96 @@
+"""GPU: decodes handed every fetched piece choose their k.
+
+storb's validator fetches all m pieces of a chunk and hands the survivors to
+reconstruct_data_stream (/root/reference/storb/validator/validator.py:1556-1604, 1631); the
+reference decodes from the first k (storb/util/piece.py:189-191).  storb_amd.piece decodes from
+the k that sec_decode_choose picks.  Pieces here are the ORACLE's blocks (oracle/fec_oracle.c) of
+seeded chunks of the policy's wide shapes; with 10-30 % of the m pieces lost (low parity rows
+included) the drop-in's bytes must equal the source chunk (= the oracle's decode) whichever k it
+uses, and the kernel counters show which decode ran."""
+
+import random
+
+import pytest
+
+from oracle import cfec
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _chunk(rng, k, m, idx, n, lost):
+    from storb_amd.piece import EncodedChunk, Piece, PieceType
+
+    data = rng.randbytes(n)
+    blocks = cfec.easy_encode(data, k, m)
+    B = len(blocks[0])
+    pieces = [Piece(chunk_idx=idx, piece_idx=j, piece_type=PieceType.Data if j < k else PieceType.Parity,
+                    data=blocks[j]) for j in range(m) if j not in lost]
+    ec = EncodedChunk(chunk_idx=idx, k=k, m=m, chunk_size=B, padlen=k * B - n, original_chunk_size=n)
+    return data, pieces, ec
+
+
+@pytest.mark.parametrize("k,m", [(32, 48), (64, 96), (16, 24)])
+def test_random_losses_all_pieces_handed_over(k, m):
+    """10-30 % of all m pieces lost at random: reconstruct_data / reconstruct_data_stream /
+    decode_chunk over every surviving piece return the chunk, with the chooser and without."""
+    from storb_amd import piece
+
+    rng = random.Random(k * 7 + m)
+    datas, pieces, chunks = [], [], []
+    for idx in range(12):
+        n = rng.randrange(k * 4096, k * 20000)
+        while True:
+            lost = set(rng.sample(range(m), int(m * rng.uniform(0.1, 0.3))))
+            if m - len(lost) >= k:
+                break
+        d, ps, ec = _chunk(rng, k, m, idx, n, lost)
+        rng.shuffle(ps)
+        datas.append(d)
+        pieces += ps
+        chunks.append(ec)
+    want = b"".join(datas)
+    for choose in (True, False):
+        piece.CHOOSE_BLOCKS = choose
+        try:
+            assert piece.reconstruct_data(pieces, chunks) == want, choose
+            assert b"".join(piece.reconstruct_data_stream(pieces, chunks, window_bytes=3 * k * 20000)) == want
+            for ec, d in zip(chunks, datas):
+                ec.pieces = sorted((p for p in pieces if p.chunk_idx == ec.chunk_idx), key=lambda p: p.piece_idx)
+                assert piece.decode_chunk(ec) == d
+        finally:
+            piece.CHOOSE_BLOCKS = True
+
+
+def test_chooser_takes_the_fused_kernel_where_first_k_cannot():
+    """zfec(64,96) chunks that lost 12-16 data pieces and the low rows of parity group 0 (so the
+    first k surviving pieces span both parity groups): the chosen k lie in group 1, so every chunk
+    decodes in the one-wave fused syndrome kernel; the first k take another kernel.  Same bytes."""
+    from storb_amd import piece
+    from storb_amd.engine import get_engine
+
+    k, m = 64, 96
+    rng = random.Random(9)
+    datas, pieces, chunks = [], [], []
+    for idx in range(8):
+        e = rng.randrange(12, 17)
+        lost = set(rng.sample(range(k), e)) | set(range(k, k + 10))  # group 0 keeps 6 < e rows
+        d, ps, ec = _chunk(rng, k, m, idx, k * 16384 + rng.randrange(-5000, 0), lost)
+        datas.append(d)
+        pieces += ps
+        chunks.append(ec)
+    want = b"".join(datas)
+    eng = get_engine(0)
+    runs = {}
+    for choose in (True, False):
+        piece.CHOOSE_BLOCKS = choose
+        try:
+            before = eng.decode_methods()
+            assert piece.reconstruct_data(pieces, chunks) == want, choose
+            after = eng.decode_methods()
+            runs[choose] = tuple(a - b for a, b in zip(after, before))
+        finally:
+            piece.CHOOSE_BLOCKS = True
+    assert runs[True] == (len(chunks), 0, 0), runs
+    assert runs[False][0] == 0 and sum(runs[False]) == len(chunks), runs
