@@ -210,7 +210,7 @@ def _stream_fixture(seed, n_chunks=10, size=600_000):
     return objs, encoded, chunks
 
 
-@pytest.mark.parametrize("fault", ["duplicate_idx", "truncated_piece", "bad_sharenum"])
+@pytest.mark.parametrize("fault", ["duplicate_idx", "truncated_piece", "bad_sharenum", "bad_sharenum_spare"])
 def test_reconstruct_stream_precondition_error_after_prefix(fault):
     """A zfec precondition failure in the middle of a window: every chunk before
     the bad one is still yielded, then the error is raised, as the reference's per-chunk loop
@@ -225,10 +225,16 @@ def test_reconstruct_stream_precondition_error_after_prefix(fault):
                 ps = [ps[0].model_copy(), *ps[:e.k - 1]]  # k pieces, two with the same piece_idx
             elif fault == "truncated_piece":
                 ps[1] = ps[1].model_copy(update={"data": ps[1].data[:-1]})
-            else:
-                ps[1] = ps[1].model_copy(update={"piece_idx": -1})  # sorts first: sharenum -1
+            elif fault == "bad_sharenum":  # exactly k pieces, one of them with sharenum -1
+                ps = ps[:e.k]
+                ps[1] = ps[1].model_copy(update={"piece_idx": -1})
+            else:  # bad_sharenum_spare: a spare valid piece beside it, which the chooser uses
+                ps[1] = ps[1].model_copy(update={"piece_idx": -1})
         pieces.extend(ps)
     got = []
+    if fault == "bad_sharenum_spare":  # sec_decode_choose never picks an invalid sharenum
+        assert b"".join(piece.reconstruct_data_stream(pieces, chunks, window_bytes=64 << 20)) == b"".join(objs)
+        return
     with pytest.raises((piece.Error, ValueError)):
         for b in piece.reconstruct_data_stream(pieces, chunks, window_bytes=64 << 20):  # one window
             got.append(b)
