@@ -130,6 +130,8 @@ enum Opt {
     O_BS_LANES,          // lanes of a bit-sliced / syndrome tile (64, 128, 256)
     O_BS_SPLIT,          // 1: one launch per 16-row group (64,96)
     O_BS_R8,             // 1: (32,48) as two interleaved groups of 8 rows
+    O_BS_LDS,            // 0: small bit-sliced chunks keep the block-stream tiles (no LDS staging)
+    O_BS_PAIR,           // 0: (64,96) encode without the shared-transpose wave pairs
     O_TILE_U,            // 0 rule (1), or 1 / 2 / 4 u-steps per lane
     O_ENC_LANES,         // 0 rule, or lanes of U = 1 encode tiles
     O_FULL_LANES,        // 0 rule, or lanes of U = 1 tiles (both kernels)
@@ -161,6 +163,8 @@ constexpr OptSpec kOpts[O_COUNT] = {
     {"SEC_BS_LANES", 256, 64, 256},
     {"SEC_BS_SPLIT", 0, 0, 1},
     {"SEC_BS_R8", 0, 0, 1},
+    {"SEC_BS_LDS", 1, 0, 1},
+    {"SEC_BS_PAIR", 1, 0, 1},
     {"SEC_TILE_U", 0, 0, 4},
     {"SEC_ENC_LANES", 0, 0, 1024},
     {"SEC_FULL_LANES", 0, 0, 1024},
@@ -204,6 +208,7 @@ struct Group {
     int rows, U, lanes, wide;  // wide: k > kBatchVecs / U, blocks loaded in several batches
     uint32_t first, count;
     int mfma = 0;              // bin kind.  Encode: 3 = sec_encode_bs_kernel of shape `rows`, row group U;
+                               // 4 = sec_encode_bs_lds_kernel of shape `rows` (one tile per chunk);
                                // decode: the small-batch variant's batch (dec_small_kb), or 0
 };
 
@@ -501,6 +506,7 @@ void add_work(const Options &o, Bins &bins, std::vector<sec::TailItem> &tail, ui
 // (then the v_perm rows), SEC_BS = 1 uses it for every shape it has; SEC_BS_R8 = 1 takes
 // (32,48) in two groups of 8 rows.
 constexpr int kBsAllGroups = 99;  // Group::U of an interleaved launch of every row group
+constexpr int kBsPair = 98;       // Group::U of a launch of two-wave workgroups (one per span, both groups)
 
 int bs_shape(const Options &o, int k, int m, uint64_t B)
 {
@@ -519,11 +525,26 @@ int bs_shape(const Options &o, int k, int m, uint64_t B)
     return sec_bs_shape(k, m);
 }
 
+// Chunks of at most sec_bs_lds_max() (64 KiB) bytes with 16 <= B <= 8192 and at most 8 parity rows
+// (C4's 64 KiB zfec(10,14) chunks) take sec_encode_bs_lds_kernel: one workgroup per chunk that
+// reads the chunk as one contiguous run into LDS instead of k unaligned block streams.  Option
+// SEC_BS_LDS = 0: the tiles below.
+bool bs_lds(const Options &o, const sec_enc_chunk &c, uint64_t B)
+{
+    return o[O_BS_LDS] && c.n <= sec_bs_lds_max() && B >= 16 && B <= 8192 && c.m - c.k <= 8;
+}
+
 void add_bs_work(const Options &o, Bins &bins, uint32_t chunk, uint64_t B, int shape)
 {
     const int lanes = o.lanes(O_BS_LANES);
     const uint64_t step = (uint64_t)sec_bs_span() * (lanes / 64);
     const int ng = sec_bs_groups(shape);
+    if (ng == 2 && o[O_BS_PAIR] && !o[O_BS_SPLIT]) {  // one two-wave workgroup per span
+        auto &bin = bins[{3, shape, kBsPair, 128, 0}];
+        for (uint64_t t0 = 0; t0 < B; t0 += sec_bs_span())
+            bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
+        return;
+    }
     if (ng > 1 && !o[O_BS_SPLIT]) {  // flatten() interleaves the groups
         auto &bin = bins[{3, shape, kBsAllGroups, lanes, 0}];
         for (uint64_t t0 = 0; t0 < B; t0 += step)
@@ -564,7 +585,7 @@ void bs_interleave(int shape, const std::vector<sec::Tile> &pos, std::vector<sec
 
 bool use_xcd_order(bool decode, const Group &g)
 {
-    if (g.mfma == 3)
+    if (g.mfma >= 3)
         return false;
     if (SEC_XCD_ORDER >= 0)
         return SEC_XCD_ORDER == 1;
@@ -959,7 +980,9 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
             const int bs = p > 0 ? bs_shape(ctx->opt, c.k, c.m, B) : -1;
-            if (bs >= 0)
+            if (bs >= 0 && bs_lds(ctx->opt, c, B))
+                bins[{4, bs, 0, 256, 0}].push_back(sec::Tile{(uint32_t)(i - c0), 0, 0, 0});
+            else if (bs >= 0)
                 add_bs_work(ctx->opt, bins, (uint32_t)(i - c0), B, bs);
             else if (p > 0)
                 add_work(ctx->opt, bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, 0, narrow);
@@ -990,11 +1013,14 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
     for (const Group &g : sp.groups) {
-        int e = g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsAllGroups ? -1 : g.U, g.lanes, in, par, dd,
-                                                   dt + g.first, g.count, s)
-                            : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
+        int e = g.mfma == 4   ? sec_launch_encode_bs_lds(g.rows, in, par, dd, dt + g.first, g.count, s)
+                : g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsAllGroups ? -1 : g.U == kBsPair ? -2 : g.U,
+                                                     g.lanes, in, par, dd, dt + g.first, g.count, s)
+                              : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
         if (e)
-            return hip_fail((hipError_t)e, g.mfma == 3 ? "sec_encode_bs_kernel" : "sec_encode_kernel");
+            return hip_fail((hipError_t)e, g.mfma == 4   ? "sec_encode_bs_lds_kernel"
+                                           : g.mfma == 3 ? "sec_encode_bs_kernel"
+                                                         : "sec_encode_kernel");
     }
     if (sp.ntail) {
         int e = sec_launch_encode_tail(in, par, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs, s);

@@ -150,13 +150,20 @@ int sec_launch_encode(int rows, int U, int wide, int lanes, const uint8_t *in, u
 // (else -1; rows = 0: the first kernel of that (k, m), else the one of `rows` rows per group):
 // all of [0, B) of chunks with B >= 16, row group `group` of sec_bs_groups(shape) (-1: every
 // group in one launch, each tile's r0 = group * sec_bs_rows(shape)), tiles of `lanes` (64..256)
-// lanes over lanes / 64 wave spans of sec_bs_span() positions
+// lanes over lanes / 64 wave spans of sec_bs_span() positions; group -2 (two-group shapes): one
+// 128-lane workgroup per span (tile t0), its two waves the two row groups sharing the transposes
 int sec_bs_shape(int k, int m, int rows = 0);
 int sec_bs_groups(int shape);
 int sec_bs_rows(int shape);
 uint32_t sec_bs_span();
 int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
                          const sec::Tile *t, uint32_t ntiles, void *stream);
+// The same rows for chunks of at most sec_bs_lds_max() bytes with 16 <= B <= 8192, one 256-lane
+// workgroup per chunk (tile t0 = 0) that reads the chunk contiguously into LDS first; for the
+// shapes of at most 8 parity rows (else hipErrorInvalidValue)
+uint32_t sec_bs_lds_max();
+int sec_launch_encode_bs_lds(int shape, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::Tile *t,
+                             uint32_t ntiles, void *stream);
 // Syndrome decode, phase 1, for the shapes sec_syn_shape knows (else -1): tiles as the bit-sliced
 // encode's (r0 = the row group's first parity row; ntail bit 0 = this tile also copies the
 // present primaries to `out`)
