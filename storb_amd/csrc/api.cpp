@@ -132,6 +132,7 @@ enum Opt {
     O_BS_R8,             // 1: (32,48) as two interleaved groups of 8 rows
     O_BS_LDS,            // 0: small bit-sliced chunks keep the block-stream tiles (no LDS staging)
     O_BS_PAIR,           // 0: (64,96) encode without the shared-transpose wave pairs
+    O_DEC_LDS,           // 0: small chunks' reassembly keeps the row-stream tiles (no LDS image)
     O_TILE_U,            // 0 rule (1), or 1 / 2 / 4 u-steps per lane
     O_ENC_LANES,         // 0 rule, or lanes of U = 1 encode tiles
     O_FULL_LANES,        // 0 rule, or lanes of U = 1 tiles (both kernels)
@@ -165,6 +166,7 @@ constexpr OptSpec kOpts[O_COUNT] = {
     {"SEC_BS_R8", 0, 0, 1},
     {"SEC_BS_LDS", 1, 0, 1},
     {"SEC_BS_PAIR", 1, 0, 1},
+    {"SEC_DEC_LDS", 1, 0, 1},
     {"SEC_TILE_U", 0, 0, 4},
     {"SEC_ENC_LANES", 0, 0, 1024},
     {"SEC_FULL_LANES", 0, 0, 1024},
@@ -381,7 +383,9 @@ int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, 
     if (o[O_SYN] == 0)
         return -1;
     const int sh = sec_syn_shape(c.k, c.m);
-    if (sh < 0 || e < 1 || c.B < 16 || c.B > 0xFFFFFFFFull - 8192 || c.padlen >= c.B)
+    // e < k - 1: the LDS-ring kernels point an absent item's loads at the first present data block
+    // other than the (possibly short) block k-1 (kernels_bs.hip item_addrs)
+    if (sh < 0 || e < 1 || e >= c.k - 1 || c.B < 16 || c.B > 0xFFFFFFFFull - 8192 || c.padlen >= c.B)
         return -1;
     const int k = c.k, NR = sec_bs_rows(sh), NR2 = sec_solve_rows(sh);
     uint64_t touched = 0, g8 = 0, g16 = 0;  // parity groups with a present row, data groups with a lost one
@@ -507,6 +511,7 @@ void add_work(const Options &o, Bins &bins, std::vector<sec::TailItem> &tail, ui
 // (32,48) in two groups of 8 rows.
 constexpr int kBsAllGroups = 99;  // Group::U of an interleaved launch of every row group
 constexpr int kBsPair = 98;       // Group::U of a launch of two-wave workgroups (one per span, both groups)
+constexpr int kDecLds = 16;       // decode bin kind of sec_decode_lds_kernel (one tile per chunk)
 
 int bs_shape(const Options &o, int k, int m, uint64_t B)
 {
@@ -1315,6 +1320,10 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                     for (int g : gl)
                         for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
                             vt.push_back(sec::Tile{vi, (uint32_t)t, (uint32_t)(g * NR2), 0u});
+            } else if (nout > 0 && !recover && !nocopy && ctx->opt[O_DEC_LDS] && c.B >= 16 && c.B <= 8192 &&
+                       nout <= sec_dec_lds_max() && e_of[i] <= (uint32_t)sec::kMaxRows) {
+                // small chunk: reassembled in LDS, written out as one run (sec_decode_lds_kernel)
+                bins[{kDecLds, (int)e_of[i], 0, 256, 0}].push_back(sec::Tile{(uint32_t)(i - c0), 0, 0, 0});
             } else if (nout > 0 && !(nocopy && e_of[i] == 0)) {
                 add_work(ctx->opt, bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true, 0, false,
                          recover || nocopy ? dec_small_kb(ctx->opt, c.k) : dec_copy_kb(ctx->opt, c.k));
@@ -1368,10 +1377,12 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::DecSlots sl{plan.meta.as<uint64_t>(sp.off_soff), plan.meta.as<uint32_t>(sp.off_srow),
                            plan.meta.as<uint32_t>(sp.off_mrow), plan.meta.as<uint32_t>(sp.off_savail)};
     for (const Group &g : sp.groups) {
-        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, blocks, out, dd, dt + g.first, g.count, tabs, sl, s,
-                                  g.mfma);  // decode groups: the bin kind is the small-batch variant (or 0)
+        // decode groups: the bin kind is the small-batch variant (or 0), or kDecLds
+        int e = g.mfma == kDecLds ? sec_launch_decode_lds(g.rows, blocks, out, dd, dt + g.first, g.count, tabs, sl, s)
+                                  : sec_launch_decode(g.rows, g.U, g.wide, g.lanes, blocks, out, dd, dt + g.first,
+                                                      g.count, tabs, sl, s, g.mfma);
         if (e)
-            return hip_fail((hipError_t)e, "sec_decode_kernel");
+            return hip_fail((hipError_t)e, g.mfma == kDecLds ? "sec_decode_lds_kernel" : "sec_decode_kernel");
     }
     if (sp.ntail) {
         int e = sec_launch_decode_tail(blocks, out, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs,

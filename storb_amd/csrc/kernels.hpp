@@ -190,6 +190,12 @@ int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *block
 // one lane per message
 int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDesc *msgs, uint32_t nmsgs,
                     uint8_t *digests, void *stream, int split = 0);
+// Reassembly of chunks of at most sec_dec_lds_max() bytes with 16 <= B <= 8192 and rows = e <= 8
+// lost primaries (every one recovered here), one 256-lane workgroup per chunk (tile t0 = 0): the
+// chunk is put together in LDS and written out as one contiguous run
+uint32_t sec_dec_lds_max();
+int sec_launch_decode_lds(int rows, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
+                          const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, sec::DecSlots sl, void *stream);
 int sec_launch_decode_tail(const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
                            const sec::TailItem *items, uint32_t nitems, const uint32_t *tabs, sec::DecSlots slots,
                            void *stream);

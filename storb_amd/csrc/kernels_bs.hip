@@ -906,10 +906,23 @@ __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__re
     }
 }
 
+// SEC_SYN_WAVES / SEC_SOLVE_WAVES (build knobs, A/B): minimum waves per SIMD of the syndrome /
+// solve kernels (amdgpu_waves_per_eu, a register cap); 0 = the compiler's choice.
+#if defined(SEC_SYN_WAVES) && SEC_SYN_WAVES > 0
+#define SEC_SYN_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SEC_SYN_WAVES)))
+#else
+#define SEC_SYN_WAVES_ATTR
+#endif
+#if defined(SEC_SOLVE_WAVES) && SEC_SOLVE_WAVES > 0
+#define SEC_SOLVE_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SEC_SOLVE_WAVES)))
+#else
+#define SEC_SOLVE_WAVES_ATTR
+#endif
+
 // The scaled syndromes go to `syn` as bit planes; sec_solve_bs_kernel then solves for the lost
 // blocks.
 template <int K, int M, int NR, int D>
-__global__ __launch_bounds__(256) void sec_syndrome_bs_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+__global__ __launch_bounds__(256) SEC_SYN_WAVES_ATTR void sec_syndrome_bs_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                               u8 *__restrict__ syn,
                                                               const sec::SynDesc *__restrict__ descs,
                                                               const sec::Tile *__restrict__ tiles,
@@ -1056,9 +1069,17 @@ __device__ __forceinline__ void solve_span(const u8 *__restrict__ syn, u8 *__res
     solve_outs<K, R0, NR>(std::make_integer_sequence<int, NR>{}, acc, o);
 }
 
+template <int K, int M, int NR, int D, int... Gs>
+__device__ __forceinline__ void solve_group(std::integer_sequence<int, Gs...>, u32 r0, const u8 *__restrict__ syn,
+                                            u8 *__restrict__ out, const sec::SolveDesc &d,
+                                            const uint64_t *__restrict__ masks, u32 s)
+{
+    ((r0 == (u32)(Gs * NR) ? solve_span<K, M, Gs * NR, NR, D>(syn, out, d, masks, s) : void()), ...);
+}
+
 // Tiles carry the row group's first data row in r0 (groups of NR rows).
 template <int K, int M, int NR, int D>
-__global__ __launch_bounds__(256) void sec_solve_bs_kernel(const u8 *__restrict__ syn, u8 *__restrict__ out,
+__global__ __launch_bounds__(256) SEC_SOLVE_WAVES_ATTR void sec_solve_bs_kernel(const u8 *__restrict__ syn, u8 *__restrict__ out,
                                                            const sec::SolveDesc *__restrict__ descs,
                                                            const sec::Tile *__restrict__ tiles,
                                                            const uint64_t *__restrict__ masks)
@@ -1068,18 +1089,8 @@ __global__ __launch_bounds__(256) void sec_solve_bs_kernel(const u8 *__restrict_
     const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
     if (s >= d.B)
         return;
-    static_assert(K % NR == 0 && K / NR <= 4, "row groups");
-    if (tl.r0 == 0)
-        solve_span<K, M, 0, NR, D>(syn, out, d, masks, s);
-    if constexpr (K / NR > 1)
-        if (tl.r0 == NR)
-            solve_span<K, M, NR, NR, D>(syn, out, d, masks, s);
-    if constexpr (K / NR > 2)
-        if (tl.r0 == 2 * NR)
-            solve_span<K, M, 2 * NR, NR, D>(syn, out, d, masks, s);
-    if constexpr (K / NR > 3)
-        if (tl.r0 == 3 * NR)
-            solve_span<K, M, 3 * NR, NR, D>(syn, out, d, masks, s);
+    static_assert(K % NR == 0 && K / NR <= 8, "row groups");
+    solve_group<K, M, NR, D>(std::make_integer_sequence<int, K / NR>{}, tl.r0, syn, out, d, masks, s);
 }
 
 // ---- decode, both phases in one wave (e <= 16, the present parity rows in one group) ---------
@@ -1353,6 +1364,7 @@ int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uin
     case 17: return launch_bs<64, 96, 0, 16, RING_K(64, 2)>(lanes, in, par, descs, t, ntiles, s);
     case 18: return launch_bs<64, 96, 16, 16, RING_K(64, 2)>(lanes, in, par, descs, t, ntiles, s);
     case 21: return launch_bs<8, 11, 0, 3, RING_K(8, 4)>(lanes, in, par, descs, t, ntiles, s);
+    case 23: return launch_bs<32, 48, -2, 8, RING_K(16, 2)>(lanes, in, par, descs, t, ntiles, s);
     case 24: return launch_bs<32, 48, -1, 8, RING_K(32, 4)>(lanes, in, par, descs, t, ntiles, s);
     case 25: return launch_bs<32, 48, 0, 8, RING_K(32, 4)>(lanes, in, par, descs, t, ntiles, s);
     case 26: return launch_bs<32, 48, 8, 8, RING_K(32, 4)>(lanes, in, par, descs, t, ntiles, s);
@@ -1402,7 +1414,11 @@ hipError_t launch_syn(int lanes, const u8 *blocks, u8 *out, u8 *syn, const sec::
 }
 
 // phase-2 rows per group: (10,14) 10, (8,*) 8, the rest 16
-constexpr int solve_nr(int k) { return k <= 16 ? k : 16; }
+// SEC_SOLVE_NR (build knob, A/B): rows per phase-2 group of the k >= 32 shapes (16 or 8)
+#ifndef SEC_SOLVE_NR
+#define SEC_SOLVE_NR 16
+#endif
+constexpr int solve_nr(int k) { return k <= 16 ? k : SEC_SOLVE_NR; }
 
 template <int K, int M, int D>
 hipError_t launch_solve(int lanes, const u8 *syn, u8 *out, const sec::SolveDesc *d, const sec::Tile *t, u32 nt,

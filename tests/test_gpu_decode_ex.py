@@ -400,3 +400,69 @@ def test_fuzz_host_reassembly_join(mode):
         assert {"pinned": z, "locked": r, "staged": st}[mode] >= 2, (mode, z, r, st)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("opts", [{}, {"SEC_DEC_LDS": 0}, {"SEC_HOST_JOIN": 0}])
+def test_small_chunks_reassembled_in_lds(opts):
+    """Chunks of at most 64 KiB with B <= 8192 and e <= 8 reassemble through LDS
+    (sec_decode_lds_kernel: the chunk put together in LDS, written out as one run); against the
+    source bytes and the oracle's decode, B of every residue mod 16 (odd B: byte writes into the
+    image), e = 0 .. 8, block k-1 in place with its short avail, device buffers; with
+    SEC_HOST_JOIN = 0 the same blocks from host buffers (staged, the kernels write every byte);
+    SEC_DEC_LDS = 0 is the row-stream tile path."""
+    from storb_amd.engine import Engine
+
+    eng = Engine(0, options=opts)
+    try:
+        rng = random.Random(404)
+        shapes, sizes = [], []
+        while len(shapes) < 96:
+            k = rng.choice([1, 2, 4, 8, 10, 13, 16])
+            m = k + rng.randrange(1, 9)
+            n = rng.choice([65536, 16 * k + 3, rng.randrange(16 * k, 65537)])
+            B = -(-n // k)
+            if n <= (k - 1) * B or B > 8192 or B < 16:
+                continue
+            shapes.append((k, m))
+            sizes.append(n)
+        src_h = np.random.default_rng(404).integers(0, 256, sum(sizes), dtype=np.uint8)
+        in_off = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+        host = "SEC_HOST_JOIN" in opts
+        blocks_all, keeps = [], []
+        for (k, m), n, o in zip(shapes, sizes, in_off):
+            blocks_all.append(cfec.easy_encode(src_h[int(o):int(o) + n].tobytes(), k, m))
+            keeps.append(rng.sample(range(m), k))
+        par_h = np.frombuffer(b"".join(b"".join(bl[k:]) for bl, (k, m) in zip(blocks_all, shapes)), np.uint8)
+        src, par = torch.from_numpy(src_h).cuda(), torch.from_numpy(par_h.copy()).cuda()
+        nslots = sum(k for k, _ in shapes)
+        dd = np.zeros(len(sizes), dtype=DEC_DTYPE)
+        sn, offs, avail = np.zeros(nslots, np.int32), np.zeros(nslots, np.uint64), np.zeros(nslots, np.uint64)
+        hostbuf, want, o, slot, po = bytearray(), [], 0, 0, 0
+        for i, ((k, m), n, keep) in enumerate(zip(shapes, sizes, keeps)):
+            b = -(-n // k)
+            dd[i] = (o, b, b * k - n, slot, k, m)
+            want.append(cfec.easy_decode([blocks_all[i][s] for s in keep], keep, b * k - n, k, m))
+            o += n
+            for s in keep:
+                sn[slot] = s
+                if host:
+                    offs[slot], avail[slot] = len(hostbuf), b
+                    hostbuf += blocks_all[i][s]
+                elif s < k:
+                    offs[slot] = src.data_ptr() + int(in_off[i]) + s * b
+                    avail[slot] = n - s * b if s == k - 1 else b
+                else:
+                    offs[slot], avail[slot] = par.data_ptr() + po + (s - k) * b, b
+                slot += 1
+            po += (m - k) * b
+        assert b"".join(want) == src_h.tobytes()  # the oracle's decode is the chunk
+        if host:
+            got = np.zeros(o, np.uint8)
+            eng.decode_batch(dd, sn, offs, np.frombuffer(bytes(hostbuf), np.uint8).copy(), got, host=True)
+            assert got.tobytes() == src_h.tobytes()
+        else:
+            out = torch.zeros(o, dtype=torch.uint8, device="cuda")
+            eng.decode_batch(dd, sn, offs, 0, out, block_avail=avail)
+            assert torch.equal(out, src)
+    finally:
+        eng.close()

@@ -45,6 +45,9 @@ CASES = [
     ("zfec(64,96) 1MiB x1024, 15 % of blocks lost, chosen k", 64, 96, 1 << 20, 1024, 0, 12, 0.15, "choose"),
     ("zfec(64,96) 1MiB x1024, 30 % of blocks lost, first k", 64, 96, 1 << 20, 1024, 0, 13, 0.3, "first"),
     ("zfec(64,96) 1MiB x1024, 30 % of blocks lost, chosen k", 64, 96, 1 << 20, 1024, 0, 13, 0.3, "choose"),
+    # parity group 0's low rows lost too (the first k present then span both groups)
+    ("zfec(64,96) 1MiB x1024, 14 data + parity rows 64..73 lost, first k", 64, 96, 1 << 20, 1024, 0, 21, "g0low", "first"),
+    ("zfec(64,96) 1MiB x1024, 14 data + parity rows 64..73 lost, chosen k", 64, 96, 1 << 20, 1024, 0, 21, "g0low", "choose"),
     ("zfec(32,48) 1MiB x1024, 20 % of blocks lost, first k", 32, 48, 1 << 20, 1024, 0, 14, 0.2, "first"),
     ("zfec(32,48) 1MiB x1024, 20 % of blocks lost, chosen k", 32, 48, 1 << 20, 1024, 0, 14, 0.2, "choose"),
 ]
@@ -52,18 +55,21 @@ CASES = [
 
 def lost_fraction(k, m, seed, frac, how):
     """(lost data blocks, erased block numbers) for `frac` of the m blocks lost (seeded; each
-    pattern holds >= k blocks), the decoder keeping the first k present ("first") or
-    sec_decode_choose's k ("choose")."""
+    pattern holds >= k blocks), or (frac "g0low") 14 random data blocks and parity rows k .. k+9
+    lost; the decoder keeps the first k present ("first") or sec_decode_choose's k ("choose")."""
     import random
 
     from storb_amd.engine import choose_blocks
 
     rng = random.Random(seed)
-    while True:
-        gone = set(rng.sample(range(m), int(round(frac * m))))
-        present = [j for j in range(m) if j not in gone]
-        if len(present) >= k:
-            break
+    if frac == "g0low":
+        gone = set(rng.sample(range(k), 14)) | set(range(k, k + 10))
+    else:
+        while True:
+            gone = set(rng.sample(range(m), int(round(frac * m))))
+            if m - len(gone) >= k:
+                break
+    present = [j for j in range(m) if j not in gone]
     keep = present[:k] if how == "first" else [present[i] for i in choose_blocks(k, m, present)]
     lost = tuple(j for j in range(k) if j not in keep)
     return lost, tuple(j for j in range(m) if j not in keep)
