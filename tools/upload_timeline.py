@@ -78,12 +78,11 @@ def main():
     piece._pieces_parallel, piece._build = orig_pp, orig_build
     med = {k: round(statistics.median(r[k] for r in rows) * 1e3, 3) for k in rows[0]}
     k, m, B, _ = piece.chunk_shape(cs)
-    print(json.dumps({"STORB_AMD_MALLOC_TUNE": os.environ.get("STORB_AMD_MALLOC_TUNE", ""), "unit": "ms from the call's start, median", "chunk_bytes": cs, "k": k, "m": m, "B": B,
+    print(json.dumps({"MALLOC_TRIM_THRESHOLD_": os.environ.get("MALLOC_TRIM_THRESHOLD_", ""), "unit": "ms from the call's start, median", "chunk_bytes": cs, "k": k, "m": m, "B": B,
                       "chunks": len(rows), **med,
                       "GiB_per_s": round(cs / (med["hash_done"] / 1e3) / 2**30, 3),
                       "cpus": piece._usable_cpus(), "hash_workers": piece.HASH_WORKERS,
-                      "pool_threads": piece._pool("hash")._max_workers,
-                      "SEC_REGISTER_MIN": os.environ.get("SEC_REGISTER_MIN", "")}))
+                      "pool_threads": piece._pool("hash")._max_workers}))
 
 
 if __name__ == "__main__":
