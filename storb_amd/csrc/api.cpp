@@ -125,14 +125,15 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 enum Opt {
     O_SYN,               // syndrome decodes: -1 cost rule, 0 off, 1 wherever they apply
     O_SYN_FUSED,         // 0: never the one-wave fused kernel
+    O_SYN_PAIR,          // 0: never the two-wave kernel (parity rows in both groups, e <= 16)
     O_SYN_RATIO,         // syndrome path taken under this many per mille of the direct estimate
     O_BS,                // bit-sliced encode: -1 rule (bs_shape), 0 off, 1 every shape it has
     O_BS_LANES,          // lanes of a bit-sliced / syndrome tile (64, 128, 256)
     O_BS_SPLIT,          // 1: one launch per 16-row group (64,96)
     O_BS_R8,             // 1: (32,48) as two interleaved groups of 8 rows
-    O_BS_LDS,            // 0: small bit-sliced chunks keep the block-stream tiles (no LDS staging)
-    O_BS_PAIR,           // 0: (64,96) encode without the shared-transpose wave pairs
-    O_DEC_LDS,           // 0: small chunks' reassembly keeps the row-stream tiles (no LDS image)
+    O_BS_LDS,            // 1: small bit-sliced chunks LDS-staged whole (default 0: measured slower)
+    O_BS_PAIR,           // 1: (64,96) encode in shared-transpose wave pairs (default 0: measured slower)
+    O_DEC_LDS,           // 1: small chunks' reassembly through an LDS image (default 0: measured slower)
     O_TILE_U,            // 0 rule (1), or 1 / 2 / 4 u-steps per lane
     O_ENC_LANES,         // 0 rule, or lanes of U = 1 encode tiles
     O_FULL_LANES,        // 0 rule, or lanes of U = 1 tiles (both kernels)
@@ -159,14 +160,15 @@ struct OptSpec {
 constexpr OptSpec kOpts[O_COUNT] = {
     {"SEC_SYN", -1, -1, 1},
     {"SEC_SYN_FUSED", 1, 0, 1},
+    {"SEC_SYN_PAIR", 1, 0, 1},
     {"SEC_SYN_RATIO", 900, 1, 1000000},
     {"SEC_BS", -1, -1, 1},
     {"SEC_BS_LANES", 256, 64, 256},
     {"SEC_BS_SPLIT", 0, 0, 1},
     {"SEC_BS_R8", 0, 0, 1},
-    {"SEC_BS_LDS", 1, 0, 1},
-    {"SEC_BS_PAIR", 1, 0, 1},
-    {"SEC_DEC_LDS", 1, 0, 1},
+    {"SEC_BS_LDS", 0, 0, 1},
+    {"SEC_BS_PAIR", 0, 0, 1},
+    {"SEC_DEC_LDS", 0, 0, 1},
     {"SEC_TILE_U", 0, 0, 4},
     {"SEC_ENC_LANES", 0, 0, 1024},
     {"SEC_FULL_LANES", 0, 0, 1024},
@@ -231,9 +233,9 @@ struct SubPlan {
     // syndrome decodes (decode): phase 1 launches (bit-sliced syndromes) and phase 2 launches
     // (the Cauchy solve), one each per shape
     // (shape, (first, count)) in tiles; synf: the fused kernel (both phases in one wave)
-    std::vector<std::pair<int, std::pair<uint32_t, uint32_t>>> syn1, syn2, synf;
+    std::vector<std::pair<int, std::pair<uint32_t, uint32_t>>> syn1, syn2, synf, synp;  // synp: the wave pairs
     size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_vdesc = 0, off_vtiles = 0,
-           off_masks = 0, off_ftiles = 0;
+           off_masks = 0, off_ftiles = 0, off_ptiles = 0;
     uint64_t syn_bytes = 0;  // syndrome scratch of this unit
     int syn_lanes = 256;     // lanes of the syndrome kernels' tiles (their span per tile)
 };
@@ -376,10 +378,15 @@ double vperm_ops(int rows, int slots)
     return v * slots;
 }
 
-// shape of the syndrome kernels for this chunk, or -1 (direct); `fused`: the one-wave kernel
-int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, bool copies, bool &fused)
+// Syndrome methods of a chunk (syn_choice)
+enum SynMethod { kSynTwo = 0, kSynFused = 1, kSynPair = 2 };
+
+// shape of the syndrome kernels for this chunk, or -1 (direct); `method`: two kernels, the one-wave
+// fused kernel, or the two-wave kernel (sec_decode_bs_pair_kernel: e <= 16 present parity rows in
+// both groups of zfec(64,96); its estimate is the fused kernel's with the transposes halved)
+int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, bool copies, int &method)
 {
-    fused = false;
+    method = kSynTwo;
     if (o[O_SYN] == 0)
         return -1;
     const int sh = sec_syn_shape(c.k, c.m);
@@ -397,8 +404,9 @@ int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, 
         }
     const int P = __builtin_popcountll(touched);
     const bool can_fuse = P == 1 && e <= 16 && o[O_SYN_FUSED] != 0;
+    const bool can_pair = P == 2 && e <= 16 && sec_syn_pair(sh) && o[O_SYN_PAIR] != 0;
     if (o[O_SYN] == 1) {
-        fused = can_fuse;
+        method = can_fuse ? kSynFused : can_pair ? kSynPair : kSynTwo;
         return sh;
     }
     auto t = [](double ops, double R, double bytes, double bw) { return std::max(ops / R, bytes / bw); };
@@ -411,10 +419,14 @@ int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, 
     const double fuse = can_fuse ? t(KE * (8.75 + E) + 15 * E + 2.75 * E * __builtin_popcountll(g8) + E * E + 14 * E,
                                      17, 4.0 * (k + out), 5.0)
                                  : 1e30;
+    const double pair = can_pair ? t(KE * (6.25 + E) + 15 * E + 2.75 * E * __builtin_popcountll(g8) + E * E + 14 * E,
+                                     17, 4.0 * (k + out), 5.0)
+                                 : 1e30;
     const double lim = (double)o[O_SYN_RATIO] / 1000.0 * direct;
-    if (std::min(two, fuse) >= lim)
+    const double best = std::min(two, std::min(fuse, pair));
+    if (best >= lim)
         return -1;
-    fused = fuse <= two;
+    method = best == fuse ? kSynFused : best == pair ? kSynPair : kSynTwo;
     return sh;
 }
 
@@ -532,8 +544,8 @@ int bs_shape(const Options &o, int k, int m, uint64_t B)
 
 // Chunks of at most sec_bs_lds_max() (64 KiB) bytes with 16 <= B <= 8192 and at most 8 parity rows
 // (C4's 64 KiB zfec(10,14) chunks) take sec_encode_bs_lds_kernel: one workgroup per chunk that
-// reads the chunk as one contiguous run into LDS instead of k unaligned block streams.  Option
-// SEC_BS_LDS = 0: the tiles below.
+// reads the chunk as one contiguous run into LDS instead of k unaligned block streams.  Opt-in
+// (SEC_BS_LDS = 1): on C4 it measured 5193 GB/s against the tiles' 5680 (profiles/r04_c4_lds_ab.jsonl).
 bool bs_lds(const Options &o, const sec_enc_chunk &c, uint64_t B)
 {
     return o[O_BS_LDS] && c.n <= sec_bs_lds_max() && B >= 16 && B <= 8192 && c.m - c.k <= 8;
@@ -1093,7 +1105,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
     std::vector<PendingExpand> pending;
     std::vector<uint32_t> tab_of((size_t)nchunks, 0), e_of((size_t)nchunks, 0);
     std::vector<int> syn_of((size_t)nchunks, -1);  // syndrome-decode shape, or -1 (syn_choice)
-    std::vector<char> fuse_of((size_t)nchunks, 0);  // ... in the one-wave kernel
+    std::vector<char> fuse_of((size_t)nchunks, 0);  // ... its SynMethod
     for (int attempt = 0;; ++attempt) {
         pending.clear();
         size_t need = 0;
@@ -1114,7 +1126,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             bool whole = true;
             for (int s = 0; s < k && whole && !host; ++s)
                 whole = idx[s] == k - 1 || slot_avail(c, block_avail, L.perm[L.first[i] + s]) >= c.B;
-            bool fz = false;
+            int fz = kSynTwo;
             const int sh = syn_of[i] =
                 whole ? syn_choice(ctx->opt, c, idx, (int)miss.size(), !recover && !nocopy, fz) : -1;
             fuse_of[i] = fz;
@@ -1160,7 +1172,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         if (e_of[i])
         {
             ++(syn_of[i] >= 0 ? plan.nsyn : plan.ndirect);
-            plan.nfused += syn_of[i] >= 0 && fuse_of[i];
+            plan.nfused += syn_of[i] >= 0 && fuse_of[i] != kSynTwo;
         }
     std::vector<std::pair<int64_t, int64_t>> ranges;
     if (host) {
@@ -1189,7 +1201,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         std::vector<sec::SynDesc> sdescs;
         std::vector<uint64_t> ssoff;
         std::vector<uint32_t> ssavail;
-        std::map<int, std::vector<sec::Tile>> stiles, vtiles, ftiles;
+        std::map<int, std::vector<sec::Tile>> stiles, vtiles, ftiles, ptiles;
         std::vector<sec::SolveDesc> vdescs;
         std::vector<uint64_t> masks;                                    // w / z scalings (scale_mask)
         std::map<std::string, std::pair<uint32_t, uint32_t>> mask_of;  // pattern -> (wq0, zq0)
@@ -1252,8 +1264,8 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 for (int g = 0; g * NR < p; ++g)
                     if ((sd.pmask >> (g * NR)) & ((NR >= 64 ? ~0ull : (1ull << NR) - 1)))
                         gs.push_back(g);
-                const bool fused = fuse_of[i];  // both phases in one wave (syn_choice)
-                if (!fused)
+                const int method = fuse_of[i];  // syn_choice: both phases in one kernel unless kSynTwo
+                if (method == kSynTwo)
                     sp.syn_bytes += (uint64_t)e * sec::syn_stride(c.B);
                 // the scalings of this erasure pattern (shared by the chunks that have it)
                 uint64_t lost = 0;
@@ -1287,10 +1299,16 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 const uint32_t si = (uint32_t)sdescs.size();
                 sdescs.push_back(sd);
                 const uint64_t step = (uint64_t)sec_bs_span() * (syn_lanes / 64);
-                if (fused) {
+                if (method == kSynFused) {
                     auto &ft = ftiles[sh];
                     for (uint64_t t = 0; t < c.B; t += step)
                         ft.push_back(sec::Tile{si, (uint32_t)t, (uint32_t)(gs[0] * NR), copies ? 1u : 0u});
+                    continue;
+                }
+                if (method == kSynPair) {  // one two-wave workgroup per span
+                    auto &pt = ptiles[sh];
+                    for (uint64_t t = 0; t < c.B; t += sec_bs_span())
+                        pt.push_back(sec::Tile{si, (uint32_t)t, 0u, copies ? 1u : 0u});
                     continue;
                 }
                 auto &st = stiles[sh];
@@ -1345,6 +1363,12 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             ftl.insert(ftl.end(), kv.second.begin(), kv.second.end());
         }
         sp.off_ftiles = img.put(ftl.data(), ftl.size() * sizeof(sec::Tile));
+        std::vector<sec::Tile> ptl;
+        for (auto &kv : ptiles) {
+            sp.synp.push_back({kv.first, {(uint32_t)ptl.size(), (uint32_t)kv.second.size()}});
+            ptl.insert(ptl.end(), kv.second.begin(), kv.second.end());
+        }
+        sp.off_ptiles = img.put(ptl.data(), ptl.size() * sizeof(sec::Tile));
         sp.off_sdesc = img.put(sdescs.data(), sdescs.size() * sizeof(sec::SynDesc));
         sp.off_stiles = img.put(stl.data(), stl.size() * sizeof(sec::Tile));
         sp.off_ssoff = img.put(ssoff.data(), ssoff.size() * 8);
@@ -1390,7 +1414,7 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_tail");
     }
-    if (sp.syn1.empty() && sp.synf.empty())
+    if (sp.syn1.empty() && sp.synf.empty() && sp.synp.empty())
         return SEC_OK;
     if (!syn && !sp.syn1.empty())
         return SEC_EINVAL;
@@ -1406,6 +1430,12 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
         int e = sec_launch_decode_bs(g.first, lanes, blocks, out, sd, ft + g.second.first, g.second.second, ss, s);
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_bs_kernel");
+    }
+    const sec::Tile *pt = plan.meta.as<sec::Tile>(sp.off_ptiles);
+    for (const auto &g : sp.synp) {
+        int e = sec_launch_decode_bs_pair(g.first, blocks, out, sd, pt + g.second.first, g.second.second, ss, s);
+        if (e)
+            return hip_fail((hipError_t)e, "sec_decode_bs_pair_kernel");
     }
     for (const auto &g : sp.syn1) {
         int e = sec_launch_syndrome_bs(g.first, lanes, blocks, out, syn, sd, st + g.second.first, g.second.second, ss, s);

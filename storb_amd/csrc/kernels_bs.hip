@@ -1188,6 +1188,206 @@ __global__ __launch_bounds__(256) void sec_decode_bs_kernel(const u8 *__restrict
     }
 }
 
+// ---- both phases for parity rows in BOTH groups: a wave pair (zfec(64,96), e <= 16) ------------
+// A chunk whose e <= 16 present parity rows lie in both 16-row groups has no place in the one-wave
+// kernel above (16 accumulator slots, one group's compile-time rows) and took the two kernels,
+// which read the data once per group and send the syndromes through HBM.  Here a workgroup is two
+// waves over the same span, wave g holding group g's syndromes:
+//   phase 1  wave g loads, copies and transposes the present data blocks j = g mod 2 and hands
+//            their bit planes to the other wave through LDS (one s_barrier per block pair), so
+//            every block is read and transposed once; each wave applies its group's present
+//            rows to every block, then its parity rows: scaled syndromes in its registers, and a
+//            copy in LDS by global rank q;
+//   phase 2  wave g solves the lost rows of 8-row groups G = g mod 2 over all e syndromes: its
+//            own from registers, the other wave's from LDS.
+// The syndromes never leave the CU: traffic is the decode's own.
+template <int K, int M, int R0, int NRP, int J>
+__device__ __forceinline__ void pd_rows(u32 (&acc)[NRP * 8], const u32 *v, uint64_t pmask)
+{
+    u32 lo[16], hi[16];
+    subsets(v[0], v[1], v[2], v[3], lo);
+    subsets(v[4], v[5], v[6], v[7], hi);
+    syn_rows<K, M, R0, J>(std::make_integer_sequence<int, NRP>{}, acc, lo, hi, pmask);
+}
+
+template <int K, int M, int R0, int NRP, int D, int P>
+__device__ __forceinline__ void pd_step(u32 (&acc)[NRP * 8], u32 (&ring)[D][8], const SynCtx &c,
+                                        u32x4 (*planes)[2][2][64], u8 *orow0, u32 B, u32 last, bool copies, u32 lane)
+{
+    constexpr int G = R0 / NRP, JO = 2 * P + G, JT = 2 * P + 1 - G, JN = 2 * (P + D) + G;
+    u32 x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        x[i] = ring[P % D][i];
+    if constexpr (JN < K)
+        if ((c.dmask >> JN) & 1)
+            load_syn_item<K, NRP, R0, JN>(ring[P % D], c);
+    const bool own = (c.dmask >> JO) & 1, other = (c.dmask >> JT) & 1;
+    if (own) {
+        if (copies) {  // the present primary's bytes to its output row (row K-1 clamps to `last`)
+            u8 *o = orow0 + (u64)JO * B;
+            if constexpr (JO == K - 1) {
+                st16_clamped(o, c.pa, last, x[0], x[1], x[2], x[3]);
+                st16_clamped(o, c.pb, last, x[4], x[5], x[6], x[7]);
+            } else {
+                st16(o + c.pa, x[0], x[1], x[2], x[3]);
+                st16(o + c.pb, x[4], x[5], x[6], x[7]);
+            }
+        }
+        transpose8(x);
+        planes[P & 1][G][0][lane] = u32x4{x[0], x[1], x[2], x[3]};
+        planes[P & 1][G][1][lane] = u32x4{x[4], x[5], x[6], x[7]};
+    }
+    __syncthreads();
+    if (own)
+        pd_rows<K, M, R0, NRP, JO>(acc, x, c.pmask);
+    __builtin_amdgcn_sched_barrier(0);
+    if (other) {
+        const u32x4 t0 = planes[P & 1][1 - G][0][lane], t1 = planes[P & 1][1 - G][1][lane];
+        const u32 y[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+        pd_rows<K, M, R0, NRP, JT>(acc, y, c.pmask);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int K, int M, int R0, int NRP, int D, int... Ps>
+__device__ __forceinline__ void pd_steps(std::integer_sequence<int, Ps...>, u32 (&acc)[NRP * 8], u32 (&ring)[D][8],
+                                         const SynCtx &c, u32x4 (*planes)[2][2][64], u8 *orow0, u32 B, u32 last,
+                                         bool copies, u32 lane)
+{
+    (pd_step<K, M, R0, NRP, D, Ps>(acc, ring, c, planes, orow0, B, last, copies, lane), ...);
+}
+
+// parity row R0 + r of this wave's group: syndrome = its planes ^ the data's contribution, * w_q;
+// kept in the accumulators and copied to LDS slot q (its rank among all present rows)
+template <int K, int R0, int NRP, int r>
+__device__ __forceinline__ void pd_parity(u32 (&acc)[NRP * 8], const SynCtx &c, u32x4 (*syl)[2][64], u32 lane)
+{
+    if (!((c.pmask >> (R0 + r)) & 1))
+        return;
+    u32 x[8];
+    load_syn_item<K, NRP, R0, K + r>(x, c);
+    transpose8(x);
+    const u32 q = (u32)__builtin_popcountll(c.pmask & ((1ull << (R0 + r)) - 1ull));
+    u32 y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        y[i] = acc[r * 8 + i] ^ x[i];
+    scale_planes(y, c.wmask[q]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        acc[r * 8 + i] = y[i];
+    syl[q][0][lane] = u32x4{y[0], y[1], y[2], y[3]};
+    syl[q][1][lane] = u32x4{y[4], y[5], y[6], y[7]};
+}
+
+template <int K, int R0, int NRP, int... Rs>
+__device__ __forceinline__ void pd_parities(std::integer_sequence<int, Rs...>, u32 (&acc)[NRP * 8], const SynCtx &c,
+                                            u32x4 (*syl)[2][64], u32 lane)
+{
+    (pd_parity<K, R0, NRP, Rs>(acc, c, syl, lane), ...);
+}
+
+// phase 2, lost rows [G2 * NR2, G2 * NR2 + NR2): parity row PR's syndrome (own group: the
+// registers; else LDS) times c[PR][lost rows]
+template <int K, int M, int R0, int NRP, int NR2, int G2, int PR>
+__device__ __forceinline__ void pd_solve_one(u32 (&acc2)[NR2 * 8], const u32 (&sy)[NRP * 8], const SynCtx &c,
+                                             const OutCtx &o, u32x4 (*syl)[2][64], u32 lane)
+{
+    if (!((c.pmask >> PR) & 1))
+        return;
+    u32 v[8];
+    if constexpr (PR >= R0 && PR < R0 + NRP) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            v[i] = sy[(PR - R0) * 8 + i];
+    } else {
+        const u32 q = (u32)__builtin_popcountll(c.pmask & ((1ull << PR) - 1ull));
+        const u32x4 a = syl[q][0][lane], b = syl[q][1][lane];
+        v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+    }
+    u32 lo[16], hi[16];
+    subsets(v[0], v[1], v[2], v[3], lo);
+    subsets(v[4], v[5], v[6], v[7], hi);
+    solve_rows<K, M, G2 * NR2, NR2, PR>(std::make_integer_sequence<int, NR2>{}, acc2, lo, hi, o.lost);
+}
+
+template <int K, int M, int R0, int NRP, int NR2, int G2, int... PRs>
+__device__ __forceinline__ void pd_solve_group(std::integer_sequence<int, PRs...>, const u32 (&sy)[NRP * 8],
+                                               const SynCtx &c, const OutCtx &o, u32x4 (*syl)[2][64], u32 lane)
+{
+    if (!((o.lost >> (G2 * NR2)) & ((1ull << NR2) - 1ull)))
+        return;
+    u32 acc2[NR2 * 8];
+#pragma unroll
+    for (int i = 0; i < NR2 * 8; ++i)
+        acc2[i] = 0;
+    (pd_solve_one<K, M, R0, NRP, NR2, G2, PRs>(acc2, sy, c, o, syl, lane), ...);
+    solve_outs<K, G2 * NR2, NR2>(std::make_integer_sequence<int, NR2>{}, acc2, o);
+}
+
+template <int K, int M, int R0, int NRP, int NR2, int... G2s>
+__device__ __forceinline__ void pd_solve(std::integer_sequence<int, G2s...>, const u32 (&sy)[NRP * 8], const SynCtx &c,
+                                         const OutCtx &o, u32x4 (*syl)[2][64], u32 lane)
+{
+    // this wave's lost-row groups: every other one, from its own index
+    ((G2s % 2 == R0 / NRP ? pd_solve_group<K, M, R0, NRP, NR2, G2s>(std::make_integer_sequence<int, M - K>{}, sy, c, o,
+                                                                     syl, lane)
+                          : void()),
+     ...);
+}
+
+// the first D own data blocks of wave R0 / NRP (blocks 2 j + g) into the ring
+template <int K, int R0, int NRP, int D, int... Js>
+__device__ __forceinline__ void pd_first(std::integer_sequence<int, Js...>, u32 (&ring)[D][8], const SynCtx &c)
+{
+    constexpr int G = R0 / NRP;
+    ((((c.dmask >> (2 * Js + G)) & 1) ? load_syn_item<K, NRP, R0, 2 * Js + G>(ring[Js], c) : void()), ...);
+}
+
+template <int K, int M, int R0, int NRP, int NR2, int D>
+__device__ __forceinline__ void pd_span(const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::SynDesc &d,
+                                        const sec::SynSlots &sl, u32 s, bool copies, u32x4 (*planes)[2][2][64],
+                                        u32x4 (*syl)[2][64])
+{
+    const u32 B = d.B, lane = threadIdx.x & 63;
+    const SynCtx c{blocks,  sl.off,     sl.avail, sl.masks + d.wq0,     d.slot0,         min(s + 16 * lane, B - 16),
+                   min(s + 1024 + 16 * lane, B - 16), s + 16 * lane, s + 1024 + 16 * lane, d.dmask, d.pmask, 0};
+    u32 ring[D][8];
+    pd_first<K, R0, NRP, D>(std::make_integer_sequence<int, D>{}, ring, c);
+    u32 acc[NRP * 8];
+#pragma unroll
+    for (int i = 0; i < NRP * 8; ++i)
+        acc[i] = 0;
+    pd_steps<K, M, R0, NRP, D>(std::make_integer_sequence<int, K / 2>{}, acc, ring, c, planes, out + d.out_off, B,
+                               d.last, copies, lane);
+    pd_parities<K, R0, NRP>(std::make_integer_sequence<int, NRP>{}, acc, c, syl, lane);
+    __syncthreads();  // both waves' syndromes in LDS
+    const uint64_t lost = ~d.dmask & (K >= 64 ? ~0ull : (1ull << K) - 1ull);
+    const OutCtx o{out + d.out_off, sl.masks + d.zq0, lost, B, d.last, d.flags & 2u ? 1u : 0u, c.pa, c.pb};
+    pd_solve<K, M, R0, NRP, NR2>(std::make_integer_sequence<int, K / NR2>{}, acc, c, o, syl, lane);
+}
+
+// 128 lanes per span (tile t0), wave g = parity group g; ntail bit 0 = copy the present primaries
+template <int K, int M, int NRP, int NR2, int D>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void sec_decode_bs_pair_kernel(
+    const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::SynDesc *__restrict__ descs,
+    const sec::Tile *__restrict__ tiles, const sec::SynSlots sl)
+{
+    static_assert(K % 2 == 0 && M - K == 2 * NRP && K % NR2 == 0, "two parity groups over an even K");
+    __shared__ u32x4 planes[2][2][2][64];  // [pair parity][wave][planes 0-3 | 4-7][lane]: 8 KiB
+    __shared__ u32x4 syl[16][2][64];       // scaled syndrome q: 32 KiB (e <= 16)
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::SynDesc d = descs[tl.chunk];
+    if (tl.t0 >= d.B)
+        return;
+    const bool copies = tl.ntail & 1;
+    if (threadIdx.x < 64)
+        pd_span<K, M, 0, NRP, NR2, D>(blocks, out, d, sl, tl.t0, copies, planes, syl);
+    else
+        pd_span<K, M, NRP, NRP, NR2, D>(blocks, out, d, sl, tl.t0, copies, planes, syl);
+}
+
 // ---- two row groups sharing each block's transpose (zfec(64,96)) ------------------------------
 // sec_encode_bs2_kernel's two groups of 16 rows each load and transpose all K blocks (the
 // transposes are 27 % of its VALU, and it runs at the VALU issue rate).  Here a workgroup is two
@@ -1416,7 +1616,7 @@ hipError_t launch_syn(int lanes, const u8 *blocks, u8 *out, u8 *syn, const sec::
 // phase-2 rows per group: (10,14) 10, (8,*) 8, the rest 16
 // SEC_SOLVE_NR (build knob, A/B): rows per phase-2 group of the k >= 32 shapes (16 or 8)
 #ifndef SEC_SOLVE_NR
-#define SEC_SOLVE_NR 16
+#define SEC_SOLVE_NR 8
 #endif
 constexpr int solve_nr(int k) { return k <= 16 ? k : SEC_SOLVE_NR; }
 
@@ -1498,6 +1698,26 @@ int sec_launch_decode_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *o
     case 5: return launch_fused<8, 11, 3, R>(lanes, blocks, out, descs, t, ntiles, sl, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+int sec_syn_pair(int shape) { return shape == 4; }  // zfec(64,96)
+
+// SEC_PAIR_RING (build knob): own data blocks in flight per wave of the pair decode
+#ifndef SEC_PAIR_RING
+#define SEC_PAIR_RING 2
+#endif
+int sec_launch_decode_bs_pair(int shape, const uint8_t *blocks, uint8_t *out, const sec::SynDesc *descs,
+                              const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    if (shape != 4)
+        return hipErrorInvalidValue;
+    void *a = nullptr, *b = nullptr;
+    sec_next_launch_events(&a, &b);
+    hipExtLaunchKernelGGL((sec_decode_bs_pair_kernel<64, 96, 16, 8, SEC_PAIR_RING>), dim3(ntiles), dim3(128), 0,
+                          (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
+    return hipGetLastError();
 }
 
 #ifndef SEC_SYN_RING

@@ -46,8 +46,8 @@ MODES = {
     "split": {"SEC_BS": 1, "SEC_BS_SPLIT": 1},  # (64,96): one launch per row group
     "r8": {"SEC_BS": 1, "SEC_BS_R8": 1},  # (32,48) in two interleaved groups of 8 rows
     "off": {"SEC_BS": 0},
-    "nolds": {"SEC_BS": 1, "SEC_BS_LDS": 0},  # small chunks on the block-stream tiles, not LDS-staged
-    "nopair": {"SEC_BS": 1, "SEC_BS_PAIR": 0},  # (64,96): both groups interleaved, each wave all blocks
+    "lds": {"SEC_BS": 1, "SEC_BS_LDS": 1},  # small chunks LDS-staged whole (opt-in; default is the block-stream tiles)
+    "pair": {"SEC_BS": 1, "SEC_BS_PAIR": 1},  # (64,96): shared-transpose wave pairs (opt-in)
 }
 
 

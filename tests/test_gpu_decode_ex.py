@@ -402,14 +402,15 @@ def test_fuzz_host_reassembly_join(mode):
         eng.close()
 
 
-@pytest.mark.parametrize("opts", [{}, {"SEC_DEC_LDS": 0}, {"SEC_HOST_JOIN": 0}])
+@pytest.mark.parametrize("opts", [{}, {"SEC_DEC_LDS": 1}, {"SEC_HOST_JOIN": 0}])
 def test_small_chunks_reassembled_in_lds(opts):
-    """Chunks of at most 64 KiB with B <= 8192 and e <= 8 reassemble through LDS
+    """With SEC_DEC_LDS = 1 (opt-in: measured slower than the tiles on C4, profiles/r04_c4_lds_ab.jsonl)
+    chunks of at most 64 KiB with B <= 8192 and e <= 8 reassemble through LDS
     (sec_decode_lds_kernel: the chunk put together in LDS, written out as one run); against the
     source bytes and the oracle's decode, B of every residue mod 16 (odd B: byte writes into the
     image), e = 0 .. 8, block k-1 in place with its short avail, device buffers; with
     SEC_HOST_JOIN = 0 the same blocks from host buffers (staged, the kernels write every byte);
-    SEC_DEC_LDS = 0 is the row-stream tile path."""
+    the default is the row-stream tile path."""
     from storb_amd.engine import Engine
 
     eng = Engine(0, options=opts)

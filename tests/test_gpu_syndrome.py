@@ -14,8 +14,10 @@ with the oracle's own decode of exactly the blocks the kernels were given, for:
   k-1 present and read in place (avail = B - padlen) or lost;
 * reassemble and recover-only; device buffers, staged host buffers and pinned host buffers;
 * syndrome chunks mixed with direct-path chunks and other shapes in one call;
-* the path actually taken (sec_ctx_decode_paths) under SEC_SYN=1 (forced) and the default
-  cost rule, with SEC_SYN=0 (the direct decode) giving the same bytes.
+* the path actually taken (sec_ctx_decode_paths / _methods) under SEC_SYN=1 (forced) and the
+  default cost rule, with SEC_SYN=0 (the direct decode) giving the same bytes;
+* zfec(64,96) with e <= 16 present parity rows in BOTH groups: the two-wave kernel
+  (sec_decode_bs_pair_kernel), against the two kernels (SEC_SYN_PAIR = 0).
 """
 
 import random
@@ -35,14 +37,15 @@ SHAPES = [(16, 24), (32, 48), (64, 96), (10, 14), (8, 12), (8, 11)]
 
 
 def _engine(syn=None, fused=None):
-    """A fresh context with the syndrome options forced (None: the library default)."""
+    """A fresh context with the syndrome options forced (None: the library default).  fused = 0:
+    neither one-kernel method (the one-wave kernel, the wave pair), i.e. the two kernels."""
     from storb_amd.engine import Engine
 
     opts = {}
     if syn is not None:
         opts["SEC_SYN"] = int(syn)
     if fused is not None:
-        opts["SEC_SYN_FUSED"] = int(fused)
+        opts["SEC_SYN_FUSED"] = opts["SEC_SYN_PAIR"] = int(fused)
     return Engine(0, options=opts)
 
 
@@ -288,5 +291,42 @@ def test_syndrome_lanes_option_and_replan(lanes):
             _run(eng, k, m, cases, recover=True)
             eng.set_option("SEC_BS_LANES", 256)
             _run(eng, k, m, cases, recover=True)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("recover", [False, True])
+def test_syndrome_wave_pair_both_groups(recover):
+    """zfec(64,96), e = 1 .. 16 lost data blocks with present parity rows drawn from both 16-row
+    groups (rows r and r + 16 both present included): the two-wave kernel decodes every chunk
+    (decode_methods counts it with the one-kernel methods), equal to the oracle's decode; then the
+    same chunks with the wave pair off (the two kernels), same bytes."""
+    k, m = 64, 96
+    rng = random.Random(96 + recover)
+    cases = []
+    for n in (16 * k, 2048 * k + 5 * k, 4099 * k - 1, 1 << 20, rng.randrange(70000, 400000)):
+        for e in (1, 2, 7, 12, 16):
+            lost = sorted(rng.sample(range(k), e))
+            g0 = rng.randrange(1, e) if e > 1 else 0
+            par = sorted(rng.sample(range(k, k + 16), g0) + rng.sample(range(k + 16, m), e - g0))
+            if e == 1:
+                par = [k + 16 + rng.randrange(16)]  # one row, group 1 only: the one-wave kernel
+            keep = [j for j in range(k) if j not in lost] + par
+            rng.shuffle(keep)
+            cases.append((n, keep))
+    both = sum(1 for _, keep in cases if {(s - k) // 16 for s in keep if s >= k} == {0, 1})
+    eng = _engine(1)
+    try:
+        _run(eng, k, m, cases, recover=recover)
+        one, two, direct = eng.decode_methods()
+        assert one == len(cases) and two == 0 and direct == 0, (one, two, direct)
+    finally:
+        eng.close()
+    eng = _engine(1)
+    eng.set_option("SEC_SYN_PAIR", 0)
+    try:
+        _run(eng, k, m, cases, recover=recover)
+        one, two, direct = eng.decode_methods()
+        assert two == both and one == len(cases) - both, (one, two, both)
     finally:
         eng.close()
