@@ -294,12 +294,13 @@ int sec_ctx_host_paths(sec_ctx *ctx, int64_t *zero_copy, int64_t *registered, in
 /* Chunks with a lost data block decoded so far on this context, by method: `syndrome` (the
  * wide-decode path: bit-sliced syndromes of the present parity rows, then the e x e solve) and
  * `direct` (the decode matrix rows over all k blocks).  Which one a chunk takes is the library's
- * choice (cost estimate; SEC_SYN=0 / 1 in the environment turns the syndrome path off / forces
+ * choice (cost estimate; context option SEC_SYN = 0 / 1 turns the syndrome path off / forces
  * it where it applies); the bytes are the same. */
 int sec_ctx_decode_paths(sec_ctx *ctx, int64_t *syndrome, int64_t *direct);
-/* The same chunks by kernel: the one-wave fused syndrome kernel, the two syndrome kernels
- * (syndromes through device scratch), the direct decode (syndrome = fused + two_kernel). */
-int sec_ctx_decode_methods(sec_ctx *ctx, int64_t *fused, int64_t *two_kernel, int64_t *direct);
+/* The same chunks by kernel: the one-wave fused syndrome kernel, the two-wave kernel (parity
+ * rows of both groups of zfec(64,96)), the two syndrome kernels (syndromes through device
+ * scratch), the direct decode (syndrome = fused + pair + two_kernel). */
+int sec_ctx_decode_methods(sec_ctx *ctx, int64_t *fused, int64_t *pair, int64_t *two_kernel, int64_t *direct);
 /* kind: 0 host->device, 1 device->host, 2 device->device; synchronous on the ctx stream */
 int sec_memcpy(sec_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
 int sec_memset(sec_ctx *ctx, void *dptr, int value, size_t bytes);

@@ -114,7 +114,7 @@ _SIGS = {
                                           ctypes.POINTER(ctypes.c_int64)]),
     "sec_ctx_decode_paths": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "sec_ctx_decode_methods": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
-                                              ctypes.POINTER(ctypes.c_int64)]),
+                                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "sec_memcpy": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_int]),
     "sec_memset": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t]),
 }

@@ -246,7 +246,7 @@ struct Plan {
     std::vector<SubPlan> subs;
     DevBuf meta;  // device copy of the metadata image of every sub-plan
     bool valid = false;
-    int64_t nsyn = 0, ndirect = 0, nfused = 0;  // decode: chunks with a lost primary, by method
+    int64_t nsyn = 0, ndirect = 0, nfused = 0, npair = 0;  // decode: chunks with a lost primary, by method
 };
 
 // Device-resident GF coefficient tables (5 dwords per coefficient), keyed by
@@ -698,7 +698,7 @@ struct sec_ctx {
     std::unique_ptr<sec::CopyPool> pool;
     // SEC_F_HOST encode / decode calls by path (sec_ctx_host_paths)
     int64_t zero_copy_calls = 0, registered_calls = 0, staged_calls = 0;
-    int64_t syn_chunks = 0, direct_chunks = 0, fused_chunks = 0;  // decodes by method (sec_ctx_decode_paths)
+    int64_t syn_chunks = 0, direct_chunks = 0, fused_chunks = 0, pair_chunks = 0;  // decodes by method (sec_ctx_decode_paths)
 
     hipStream_t stream() const { return ext ? ext : own; }
     hipEvent_t ev()
@@ -1167,12 +1167,13 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         RC(table_reset(ctx, tc, need * 2 + ((size_t)1 << 18)));
     }
 
-    plan.nsyn = plan.ndirect = plan.nfused = 0;
+    plan.nsyn = plan.ndirect = plan.nfused = plan.npair = 0;
     for (int64_t i = 0; i < nchunks; ++i)
         if (e_of[i])
         {
             ++(syn_of[i] >= 0 ? plan.nsyn : plan.ndirect);
-            plan.nfused += syn_of[i] >= 0 && fuse_of[i] != kSynTwo;
+            plan.nfused += syn_of[i] >= 0 && fuse_of[i] == kSynFused;
+            plan.npair += syn_of[i] >= 0 && fuse_of[i] == kSynPair;
         }
     std::vector<std::pair<int64_t, int64_t>> ranges;
     if (host) {
@@ -2752,6 +2753,7 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
     ctx->syn_chunks += plan.nsyn;
     ctx->direct_chunks += plan.ndirect;
     ctx->fused_chunks += plan.nfused;
+    ctx->pair_chunks += plan.npair;
 
     if (!host) {
         hipEvent_t t0 = nullptr;
@@ -2883,14 +2885,16 @@ int sec_ctx_decode_paths(sec_ctx *ctx, int64_t *syndrome, int64_t *direct)
     return SEC_OK;
 }
 
-int sec_ctx_decode_methods(sec_ctx *ctx, int64_t *fused, int64_t *two_kernel, int64_t *direct)
+int sec_ctx_decode_methods(sec_ctx *ctx, int64_t *fused, int64_t *pair, int64_t *two_kernel, int64_t *direct)
 {
     if (!ctx)
         return SEC_EINVAL;
     if (fused)
         *fused = ctx->fused_chunks;
+    if (pair)
+        *pair = ctx->pair_chunks;
     if (two_kernel)
-        *two_kernel = ctx->syn_chunks - ctx->fused_chunks;
+        *two_kernel = ctx->syn_chunks - ctx->fused_chunks - ctx->pair_chunks;
     if (direct)
         *direct = ctx->direct_chunks;
     return SEC_OK;

@@ -235,12 +235,13 @@ class Engine:
         self._check(self.lib.sec_ctx_decode_paths(self._ctx, ctypes.byref(syn), ctypes.byref(direct)))
         return syn.value, direct.value
 
-    def decode_methods(self) -> tuple[int, int, int]:
-        """(fused syndrome kernel, two syndrome kernels, direct): chunks with a lost data block
-        decoded so far, by kernel."""
-        f, t, d = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
-        self._check(self.lib.sec_ctx_decode_methods(self._ctx, ctypes.byref(f), ctypes.byref(t), ctypes.byref(d)))
-        return f.value, t.value, d.value
+    def decode_methods(self) -> tuple[int, int, int, int]:
+        """(fused one-wave syndrome kernel, two-wave kernel, two syndrome kernels, direct): chunks
+        with a lost data block decoded so far, by kernel."""
+        f, p, t, d = (ctypes.c_int64(0) for _ in range(4))
+        self._check(self.lib.sec_ctx_decode_methods(self._ctx, ctypes.byref(f), ctypes.byref(p), ctypes.byref(t),
+                                                    ctypes.byref(d)))
+        return f.value, p.value, t.value, d.value
 
     _SCRATCH_CAP = 256 << 20  # largest result staged in the reusable pinned scratch
 

@@ -66,7 +66,8 @@ def test_random_losses_all_pieces_handed_over(k, m):
 def test_chooser_takes_the_fused_kernel_where_first_k_cannot():
     """zfec(64,96) chunks that lost 12-16 data pieces and the low rows of parity group 0 (so the
     first k surviving pieces span both parity groups): the chosen k lie in group 1, so every chunk
-    decodes in the one-wave fused syndrome kernel; the first k take another kernel.  Same bytes."""
+    decodes in the one-wave fused syndrome kernel; the first k take another kernel (the two-wave
+    kernel for parity rows of both groups, or the direct decode).  Same bytes."""
     from storb_amd import piece
     from storb_amd.engine import get_engine
 
@@ -92,5 +93,5 @@ def test_chooser_takes_the_fused_kernel_where_first_k_cannot():
             runs[choose] = tuple(a - b for a, b in zip(after, before))
         finally:
             piece.CHOOSE_BLOCKS = True
-    assert runs[True] == (len(chunks), 0, 0), runs
+    assert runs[True] == (len(chunks), 0, 0, 0), runs
     assert runs[False][0] == 0 and sum(runs[False]) == len(chunks), runs

@@ -299,8 +299,8 @@ def test_syndrome_lanes_option_and_replan(lanes):
 def test_syndrome_wave_pair_both_groups(recover):
     """zfec(64,96), e = 1 .. 16 lost data blocks with present parity rows drawn from both 16-row
     groups (rows r and r + 16 both present included): the two-wave kernel decodes every chunk
-    (decode_methods counts it with the one-kernel methods), equal to the oracle's decode; then the
-    same chunks with the wave pair off (the two kernels), same bytes."""
+    (decode_methods' pair count; e = 1 with one row takes the one-wave kernel), equal to the
+    oracle's decode; then the same chunks with the wave pair off (the two kernels), same bytes."""
     k, m = 64, 96
     rng = random.Random(96 + recover)
     cases = []
@@ -318,15 +318,15 @@ def test_syndrome_wave_pair_both_groups(recover):
     eng = _engine(1)
     try:
         _run(eng, k, m, cases, recover=recover)
-        one, two, direct = eng.decode_methods()
-        assert one == len(cases) and two == 0 and direct == 0, (one, two, direct)
+        one, pair, two, direct = eng.decode_methods()
+        assert pair == both and one == len(cases) - both and two == 0 and direct == 0, (one, pair, two, direct)
     finally:
         eng.close()
     eng = _engine(1)
     eng.set_option("SEC_SYN_PAIR", 0)
     try:
         _run(eng, k, m, cases, recover=recover)
-        one, two, direct = eng.decode_methods()
-        assert two == both and one == len(cases) - both, (one, two, both)
+        one, pair, two, direct = eng.decode_methods()
+        assert pair == 0 and two == both and one == len(cases) - both, (one, pair, two, both)
     finally:
         eng.close()
