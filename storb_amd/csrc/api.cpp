@@ -382,7 +382,7 @@ double vperm_ops(int rows, int slots)
 enum SynMethod { kSynTwo = 0, kSynFused = 1, kSynPair = 2 };
 
 // shape of the syndrome kernels for this chunk, or -1 (direct); `method`: two kernels, the one-wave
-// fused kernel, or the two-wave kernel (sec_decode_bs_pair_kernel: e <= 16 present parity rows in
+// fused kernel, or the two-wave kernel (sec_decode_bs_pair_kernel: e <= 32 present parity rows in
 // both groups of zfec(64,96); its estimate is the fused kernel's with the transposes halved)
 int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, bool copies, int &method)
 {
@@ -404,7 +404,7 @@ int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, 
         }
     const int P = __builtin_popcountll(touched);
     const bool can_fuse = P == 1 && e <= 16 && o[O_SYN_FUSED] != 0;
-    const bool can_pair = P == 2 && e <= 16 && sec_syn_pair(sh) && o[O_SYN_PAIR] != 0;
+    const bool can_pair = P == 2 && e <= 32 && sec_syn_pair(sh) && o[O_SYN_PAIR] != 0;
     if (o[O_SYN] == 1) {
         method = can_fuse ? kSynFused : can_pair ? kSynPair : kSynTwo;
         return sh;
@@ -1306,8 +1306,8 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                         ft.push_back(sec::Tile{si, (uint32_t)t, (uint32_t)(gs[0] * NR), copies ? 1u : 0u});
                     continue;
                 }
-                if (method == kSynPair) {  // one two-wave workgroup per span
-                    auto &pt = ptiles[sh];
+                if (method == kSynPair) {  // one two-wave workgroup per span; launches by LDS size
+                    auto &pt = ptiles[sh * 64 + (e <= 16 ? 16 : 32)];
                     for (uint64_t t = 0; t < c.B; t += sec_bs_span())
                         pt.push_back(sec::Tile{si, (uint32_t)t, 0u, copies ? 1u : 0u});
                     continue;
@@ -1434,7 +1434,8 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     }
     const sec::Tile *pt = plan.meta.as<sec::Tile>(sp.off_ptiles);
     for (const auto &g : sp.synp) {
-        int e = sec_launch_decode_bs_pair(g.first, blocks, out, sd, pt + g.second.first, g.second.second, ss, s);
+        int e = sec_launch_decode_bs_pair(g.first / 64, g.first % 64, blocks, out, sd, pt + g.second.first,
+                                          g.second.second, ss, s);
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_bs_pair_kernel");
     }

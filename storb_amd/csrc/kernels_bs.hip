@@ -1188,10 +1188,10 @@ __global__ __launch_bounds__(256) void sec_decode_bs_kernel(const u8 *__restrict
     }
 }
 
-// ---- both phases for parity rows in BOTH groups: a wave pair (zfec(64,96), e <= 16) ------------
-// A chunk whose e <= 16 present parity rows lie in both 16-row groups has no place in the one-wave
-// kernel above (16 accumulator slots, one group's compile-time rows) and took the two kernels,
-// which read the data once per group and send the syndromes through HBM.  Here a workgroup is two
+// ---- both phases for parity rows in BOTH groups: a wave pair (zfec(64,96), e <= 32) ------------
+// A chunk whose e present parity rows lie in both 16-row groups (or e > 16) has no place in the
+// one-wave kernel above (16 accumulator slots, one group's compile-time rows) and took the two
+// kernels, which read the data once per group and send the syndromes through HBM.  Here a workgroup is two
 // waves over the same span, wave g holding group g's syndromes:
 //   phase 1  wave g loads, copies and transposes the present data blocks j = g mod 2 and hands
 //            their bit planes to the other wave through LDS (one s_barrier per block pair), so
@@ -1368,15 +1368,16 @@ __device__ __forceinline__ void pd_span(const u8 *__restrict__ blocks, u8 *__res
     pd_solve<K, M, R0, NRP, NR2>(std::make_integer_sequence<int, K / NR2>{}, acc, c, o, syl, lane);
 }
 
-// 128 lanes per span (tile t0), wave g = parity group g; ntail bit 0 = copy the present primaries
-template <int K, int M, int NRP, int NR2, int D>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void sec_decode_bs_pair_kernel(
+// 128 lanes per span (tile t0), wave g = parity group g; ntail bit 0 = copy the present primaries.
+// SL syndrome slots in LDS: 16 (40 KiB, 4 workgroups per CU) or 32 (72 KiB, e > 16: 2 per CU).
+template <int K, int M, int NRP, int NR2, int D, int SL>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SL <= 16 ? 2 : 1))) void sec_decode_bs_pair_kernel(
     const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::SynDesc *__restrict__ descs,
     const sec::Tile *__restrict__ tiles, const sec::SynSlots sl)
 {
     static_assert(K % 2 == 0 && M - K == 2 * NRP && K % NR2 == 0, "two parity groups over an even K");
     __shared__ u32x4 planes[2][2][2][64];  // [pair parity][wave][planes 0-3 | 4-7][lane]: 8 KiB
-    __shared__ u32x4 syl[16][2][64];       // scaled syndrome q: 32 KiB (e <= 16)
+    __shared__ u32x4 syl[SL][2][64];       // scaled syndrome q: 2 KiB each
     const sec::Tile tl = tiles[blockIdx.x];
     const sec::SynDesc d = descs[tl.chunk];
     if (tl.t0 >= d.B)
@@ -1706,17 +1707,21 @@ int sec_syn_pair(int shape) { return shape == 4; }  // zfec(64,96)
 #ifndef SEC_PAIR_RING
 #define SEC_PAIR_RING 2
 #endif
-int sec_launch_decode_bs_pair(int shape, const uint8_t *blocks, uint8_t *out, const sec::SynDesc *descs,
+int sec_launch_decode_bs_pair(int shape, int e_max, const uint8_t *blocks, uint8_t *out, const sec::SynDesc *descs,
                               const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream)
 {
     if (ntiles == 0)
         return hipSuccess;
-    if (shape != 4)
+    if (shape != 4 || e_max < 1 || e_max > 32)
         return hipErrorInvalidValue;
     void *a = nullptr, *b = nullptr;
     sec_next_launch_events(&a, &b);
-    hipExtLaunchKernelGGL((sec_decode_bs_pair_kernel<64, 96, 16, 8, SEC_PAIR_RING>), dim3(ntiles), dim3(128), 0,
-                          (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
+    if (e_max <= 16)
+        hipExtLaunchKernelGGL((sec_decode_bs_pair_kernel<64, 96, 16, 8, SEC_PAIR_RING, 16>), dim3(ntiles), dim3(128),
+                              0, (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
+    else
+        hipExtLaunchKernelGGL((sec_decode_bs_pair_kernel<64, 96, 16, 8, SEC_PAIR_RING, 32>), dim3(ntiles), dim3(128),
+                              0, (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
     return hipGetLastError();
 }
 
