@@ -250,9 +250,9 @@ __device__ __forceinline__ void all_blocks(std::integer_sequence<int, Js...>, u3
 #define SEC_FUSED_LDS_RING 8
 #endif
 
-template <int D>
+template <int D, int W = 4>
 struct LdsRing {
-    u32x4 v[4][D][2][64];  // [wave of a 256-lane workgroup][slot][half][lane]
+    u32x4 v[W][D][2][64];  // [wave of the workgroup][slot][half][lane]
 };
 
 template <int N>
@@ -792,8 +792,8 @@ __device__ __forceinline__ void syn_items(std::integer_sequence<int, Js...>, u32
 // measured +0-5 % reassembling and +7-16 % recover-only over the register ring; the small-k
 // shapes keep the register ring (LDS ring -8 % on (32,48) with 8 lost, -9 % (16,24), -20 % C4;
 // the direct decode is chosen there anyway), r03_syn_ab_lds.jsonl.
-template <int K, int NR, int R0, int D, int J>
-__device__ __forceinline__ void lds_issue(LdsRing<D> &ring, u32 w, u32 (&xs)[8], const SynCtx &c, const ItemAddrs &ia)
+template <int K, int NR, int R0, int D, int J, class Ring>
+__device__ __forceinline__ void lds_issue(Ring &ring, u32 w, u32 (&xs)[8], const SynCtx &c, const ItemAddrs &ia)
 {
     const bool here = item_present<K, NR, R0>(c, J);
     if constexpr (J == K - 1) {  // register path (short block k-1)
@@ -808,15 +808,15 @@ __device__ __forceinline__ void lds_issue(LdsRing<D> &ring, u32 w, u32 (&xs)[8],
     }
 }
 
-template <int K, int NR, int R0, int D, int... Js>
-__device__ __forceinline__ void lds_first(std::integer_sequence<int, Js...>, LdsRing<D> &ring, u32 w, u32 (&xs)[8],
+template <int K, int NR, int R0, int D, class Ring, int... Js>
+__device__ __forceinline__ void lds_first(std::integer_sequence<int, Js...>, Ring &ring, u32 w, u32 (&xs)[8],
                                           const SynCtx &c, const ItemAddrs &ia)
 {
     (lds_issue<K, NR, R0, D, Js>(ring, w, xs, c, ia), ...);
 }
 
-template <int K, int M, int R0, int NR, int D, bool FUSED, int J>
-__device__ __forceinline__ void syn_item_lds(u32 (&acc)[NR * 8], LdsRing<D> &ring, u32 w, u32 (&xs)[8],
+template <int K, int M, int R0, int NR, int D, bool FUSED, int J, class Ring>
+__device__ __forceinline__ void syn_item_lds(u32 (&acc)[NR * 8], Ring &ring, u32 w, u32 (&xs)[8],
                                              const SynCtx &c, const ItemAddrs &ia, u8 *orow0, u32 B, u32 last,
                                              bool copies, u8 *syn, u32 &q)
 {
@@ -846,8 +846,8 @@ __device__ __forceinline__ void syn_item_lds(u32 (&acc)[NR * 8], LdsRing<D> &rin
     syn_process<K, M, R0, NR, FUSED, J>(acc, x, c, orow0, B, last, copies, syn, q);
 }
 
-template <int K, int M, int R0, int NR, int D, bool FUSED, int... Js>
-__device__ __forceinline__ void syn_items_lds(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], LdsRing<D> &ring,
+template <int K, int M, int R0, int NR, int D, bool FUSED, class Ring, int... Js>
+__device__ __forceinline__ void syn_items_lds(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], Ring &ring,
                                               u32 w, u32 (&xs)[8], const SynCtx &c, const ItemAddrs &ia, u8 *orow0,
                                               u32 B, u32 last, bool copies, u8 *syn, u32 &q)
 {
@@ -1389,6 +1389,84 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SL <= 16 ? 
         pd_span<K, M, NRP, NRP, NR2, D>(blocks, out, d, sl, tl.t0, copies, planes, syl);
 }
 
+// The same wave pair with each wave's phase 1 on its own (the default; SEC_PAIR_SHARED = 1 builds
+// the shared-transpose phase 1 above instead).  Measured, the shared transposes cost more than
+// they save: one s_barrier per block pair lockstepped the waves and the register ring held only
+// 2 blocks in flight (2.8 TB/s at e = 16, against 4.2 for the one-wave kernel).  Here wave g runs
+// the one-wave kernel's phase 1 for group g -- every present data block through a per-wave LDS
+// ring filled by global_load_lds, its own transposes, no barrier -- the two waves reading the
+// same blocks at the same time (the second read an L2 hit).  Then the ring's LDS becomes the
+// syndrome exchange: each wave stores its scaled syndromes at their global rank, one barrier,
+// and phase 2 as above.  LDS: max(ring, SL slots) = 32 KiB for e <= 16, 64 KiB for e <= 32.
+template <int SL>
+union PairLds {
+    LdsRing<SEC_FUSED_LDS_RING, 2> ring;  // phase 1: 8 blocks in flight per wave
+    u32x4 syl[SL][2][64];                 // phase 2: scaled syndrome q
+};
+
+template <int NRP, int r>
+__device__ __forceinline__ void pf_put(const u32 (&acc)[NRP * 8], uint64_t pm, u32 &q, u32x4 (*syl)[2][64], u32 lane)
+{
+    if (!((pm >> r) & 1))
+        return;
+    syl[q][0][lane] = u32x4{acc[r * 8 + 0], acc[r * 8 + 1], acc[r * 8 + 2], acc[r * 8 + 3]};
+    syl[q][1][lane] = u32x4{acc[r * 8 + 4], acc[r * 8 + 5], acc[r * 8 + 6], acc[r * 8 + 7]};
+    ++q;
+}
+
+template <int NRP, int... Rs>
+__device__ __forceinline__ void pf_puts(std::integer_sequence<int, Rs...>, const u32 (&acc)[NRP * 8], uint64_t pm,
+                                        u32 q, u32x4 (*syl)[2][64], u32 lane)
+{
+    (pf_put<NRP, Rs>(acc, pm, q, syl, lane), ...);
+}
+
+template <int K, int M, int R0, int NRP, int NR2, int SL>
+__device__ __forceinline__ void pf_span(const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::SynDesc &d,
+                                        const sec::SynSlots &sl, u32 s, bool copies, PairLds<SL> &lds)
+{
+    constexpr u32 w = R0 / NRP;
+    constexpr int DL = SEC_FUSED_LDS_RING;
+    const u32 B = d.B, lane = threadIdx.x & 63;
+    const SynCtx c{blocks,  sl.off,     sl.avail, sl.masks + d.wq0,     d.slot0,         min(s + 16 * lane, B - 16),
+                   min(s + 1024 + 16 * lane, B - 16), s + 16 * lane, s + 1024 + 16 * lane, d.dmask, d.pmask, 0};
+    u32 acc[NRP * 8];
+#pragma unroll
+    for (int i = 0; i < NRP * 8; ++i)
+        acc[i] = 0;
+    const u32 q0 = (u32)__builtin_popcountll(d.pmask & ((1ull << R0) - 1ull));  // this group's first rank
+    u32 q = q0;
+    u32 xs[8];
+    const ItemAddrs ia = item_addrs<K, NRP, R0>(c);
+    lds_first<K, NRP, R0, DL>(std::make_integer_sequence<int, DL>{}, lds.ring, w, xs, c, ia);
+    syn_items_lds<K, M, R0, NRP, DL, true>(std::make_integer_sequence<int, K + NRP>{}, acc, lds.ring, w, xs, c, ia,
+                                           out + d.out_off, B, d.last, copies && w == 0, nullptr, q);
+    __syncthreads();  // both rings drained: the LDS becomes the syndrome slots
+    pf_puts<NRP>(std::make_integer_sequence<int, NRP>{}, acc, d.pmask >> R0, q0, lds.syl, lane);
+    __syncthreads();
+    const uint64_t lost = ~d.dmask & (K >= 64 ? ~0ull : (1ull << K) - 1ull);
+    const OutCtx o{out + d.out_off, sl.masks + d.zq0, lost, B, d.last, d.flags & 2u ? 1u : 0u, c.pa, c.pb};
+    pd_solve<K, M, R0, NRP, NR2>(std::make_integer_sequence<int, K / NR2>{}, acc, c, o, lds.syl, lane);
+}
+
+template <int K, int M, int NRP, int NR2, int SL>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void sec_decode_bs_pair2_kernel(
+    const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::SynDesc *__restrict__ descs,
+    const sec::Tile *__restrict__ tiles, const sec::SynSlots sl)
+{
+    static_assert(K >= 32 && M - K == 2 * NRP && K % NR2 == 0, "two parity groups, the LDS ring's k");
+    __shared__ PairLds<SL> lds;
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::SynDesc d = descs[tl.chunk];
+    if (tl.t0 >= d.B)
+        return;
+    const bool copies = tl.ntail & 1;
+    if (threadIdx.x < 64)
+        pf_span<K, M, 0, NRP, NR2, SL>(blocks, out, d, sl, tl.t0, copies, lds);
+    else
+        pf_span<K, M, NRP, NRP, NR2, SL>(blocks, out, d, sl, tl.t0, copies, lds);
+}
+
 // ---- two row groups sharing each block's transpose (zfec(64,96)) ------------------------------
 // sec_encode_bs2_kernel's two groups of 16 rows each load and transpose all K blocks (the
 // transposes are 27 % of its VALU, and it runs at the VALU issue rate).  Here a workgroup is two
@@ -1703,7 +1781,11 @@ int sec_launch_decode_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *o
 
 int sec_syn_pair(int shape) { return shape == 4; }  // zfec(64,96)
 
-// SEC_PAIR_RING (build knob): own data blocks in flight per wave of the pair decode
+// SEC_PAIR_SHARED (build knob, A/B): 1 = the shared-transpose pair decode, SEC_PAIR_RING own data
+// blocks in flight per wave; 0 (default) = each wave's phase 1 on its own LDS ring
+#ifndef SEC_PAIR_SHARED
+#define SEC_PAIR_SHARED 0
+#endif
 #ifndef SEC_PAIR_RING
 #define SEC_PAIR_RING 2
 #endif
@@ -1716,12 +1798,21 @@ int sec_launch_decode_bs_pair(int shape, int e_max, const uint8_t *blocks, uint8
         return hipErrorInvalidValue;
     void *a = nullptr, *b = nullptr;
     sec_next_launch_events(&a, &b);
+#if SEC_PAIR_SHARED
     if (e_max <= 16)
         hipExtLaunchKernelGGL((sec_decode_bs_pair_kernel<64, 96, 16, 8, SEC_PAIR_RING, 16>), dim3(ntiles), dim3(128),
                               0, (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
     else
         hipExtLaunchKernelGGL((sec_decode_bs_pair_kernel<64, 96, 16, 8, SEC_PAIR_RING, 32>), dim3(ntiles), dim3(128),
                               0, (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
+#else
+    if (e_max <= 16)
+        hipExtLaunchKernelGGL((sec_decode_bs_pair2_kernel<64, 96, 16, 8, 16>), dim3(ntiles), dim3(128), 0,
+                              (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
+    else
+        hipExtLaunchKernelGGL((sec_decode_bs_pair2_kernel<64, 96, 16, 8, 32>), dim3(ntiles), dim3(128), 0,
+                              (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
+#endif
     return hipGetLastError();
 }
 
