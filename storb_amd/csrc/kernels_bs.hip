@@ -1440,7 +1440,7 @@ __device__ __forceinline__ void pf_span(const u8 *__restrict__ blocks, u8 *__res
     const ItemAddrs ia = item_addrs<K, NRP, R0>(c);
     lds_first<K, NRP, R0, DL>(std::make_integer_sequence<int, DL>{}, lds.ring, w, xs, c, ia);
     syn_items_lds<K, M, R0, NRP, DL, true>(std::make_integer_sequence<int, K + NRP>{}, acc, lds.ring, w, xs, c, ia,
-                                           out + d.out_off, B, d.last, copies && w == 0, nullptr, q);
+                                           out + d.out_off, B, d.last, copies, nullptr, q);
     __syncthreads();  // both rings drained: the LDS becomes the syndrome slots
     pf_puts<NRP>(std::make_integer_sequence<int, NRP>{}, acc, d.pmask >> R0, q0, lds.syl, lane);
     __syncthreads();
@@ -1450,7 +1450,7 @@ __device__ __forceinline__ void pf_span(const u8 *__restrict__ blocks, u8 *__res
 }
 
 template <int K, int M, int NRP, int NR2, int SL>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void sec_decode_bs_pair2_kernel(
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SL <= 16 ? 2 : 1))) void sec_decode_bs_pair2_kernel(
     const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::SynDesc *__restrict__ descs,
     const sec::Tile *__restrict__ tiles, const sec::SynSlots sl)
 {
@@ -1460,8 +1460,10 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1))) void s
     const sec::SynDesc d = descs[tl.chunk];
     if (tl.t0 >= d.B)
         return;
-    const bool copies = tl.ntail & 1;
-    if (threadIdx.x < 64)
+    // wave 0 copies the present primaries (a run-time flag for both waves: with a constant false
+    // the compiler drops wave 1's stores and hoists its transposes, 1600+ spilled registers)
+    const bool first = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64, copies = (tl.ntail & 1) && first;
+    if (first)  // a scalar branch
         pf_span<K, M, 0, NRP, NR2, SL>(blocks, out, d, sl, tl.t0, copies, lds);
     else
         pf_span<K, M, NRP, NRP, NR2, SL>(blocks, out, d, sl, tl.t0, copies, lds);
