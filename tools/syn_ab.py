@@ -102,6 +102,7 @@ def main():
                     help="name@OPT=V+OPT2=V2[/tag]: context options per variant, optionally a prebuilt variant library "
                          "storb_amd/lib/libstorbec_<tag>.so (storb_amd._build.build(defines=..., tag=...))")
     ap.add_argument("--cases", default="")
+    ap.add_argument("--modes", default="reassemble,recover_only", help="decode modes to run (PMC passes: one)")
     a = ap.parse_args()
     variants = []  # (name, env, lib path or None); "name@ENV=V+ENV2=V2/tag": storb_amd/lib/libstorbec_<tag>.so
     for v in a.variants.split(","):
@@ -134,6 +135,8 @@ def main():
                 eng = Engine(0, lib_path=lib, options=env)  # the variant's options (sec_ctx_set_option)
                 for mode, args in (("reassemble", (dd, sn, offs, av, out, False)),
                                    ("recover_only", (rd, rsn, roffs, rav, rec, True))):
+                    if mode not in a.modes.split(","):
+                        continue
                     d_, s_, o_, a_, dst, recov = args
                     dst.zero_()
                     eng.decode_batch(d_, s_, o_, 0, dst, block_avail=a_, recover_only=recov)
@@ -157,7 +160,7 @@ def main():
         row = {"case": name, "k": k, "m": m, "chunk": n, "chunks": nch, "lost": list(lost),
                "parity_kept": [s for s in sn[:k].tolist() if s >= k]}
         for vname, r in res.items():
-            row[vname] = {mode: round(float(np.median(v)), 3) for mode, v in r.items()}
+            row[vname] = {mode: round(float(np.median(v)), 3) for mode, v in r.items() if v}
             row[vname]["paths(syn,direct)"] = paths.get(vname)
         print(json.dumps(row), flush=True)
         del src, par, out, rec
