@@ -125,7 +125,7 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 enum Opt {
     O_SYN,               // syndrome decodes: -1 cost rule, 0 off, 1 wherever they apply
     O_SYN_FUSED,         // 0: never the one-wave fused kernel
-    O_SYN_PAIR,          // 0: never the two-wave kernel (parity rows in both groups, e <= 16)
+    O_SYN_PAIR,          // 1: the two-wave kernel where it applies (default 0: ties the direct decode)
     O_SYN_RATIO,         // syndrome path taken under this many per mille of the direct estimate
     O_BS,                // bit-sliced encode: -1 rule (bs_shape), 0 off, 1 every shape it has
     O_BS_LANES,          // lanes of a bit-sliced / syndrome tile (64, 128, 256)
@@ -160,7 +160,7 @@ struct OptSpec {
 constexpr OptSpec kOpts[O_COUNT] = {
     {"SEC_SYN", -1, -1, 1},
     {"SEC_SYN_FUSED", 1, 0, 1},
-    {"SEC_SYN_PAIR", 1, 0, 1},
+    {"SEC_SYN_PAIR", 0, 0, 1},
     {"SEC_SYN_RATIO", 900, 1, 1000000},
     {"SEC_BS", -1, -1, 1},
     {"SEC_BS_LANES", 256, 64, 256},
@@ -382,8 +382,9 @@ double vperm_ops(int rows, int slots)
 enum SynMethod { kSynTwo = 0, kSynFused = 1, kSynPair = 2 };
 
 // shape of the syndrome kernels for this chunk, or -1 (direct); `method`: two kernels, the one-wave
-// fused kernel, or the two-wave kernel (sec_decode_bs_pair_kernel: e <= 32 present parity rows in
-// both groups of zfec(64,96); its estimate is the fused kernel's with the transposes halved)
+// fused kernel, or (option SEC_SYN_PAIR = 1) the two-wave kernel (sec_decode_bs_pair_kernel: e <= 16
+// present parity rows in both groups of zfec(64,96); its estimate is the fused kernel's with the
+// transposes halved)
 int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, bool copies, int &method)
 {
     method = kSynTwo;
@@ -404,7 +405,7 @@ int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, 
         }
     const int P = __builtin_popcountll(touched);
     const bool can_fuse = P == 1 && e <= 16 && o[O_SYN_FUSED] != 0;
-    const bool can_pair = P == 2 && e <= 32 && sec_syn_pair(sh) && o[O_SYN_PAIR] != 0;
+    const bool can_pair = P == 2 && e <= 16 && sec_syn_pair(sh) && o[O_SYN_PAIR] != 0;
     if (o[O_SYN] == 1) {
         method = can_fuse ? kSynFused : can_pair ? kSynPair : kSynTwo;
         return sh;
@@ -1307,7 +1308,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                     continue;
                 }
                 if (method == kSynPair) {  // one two-wave workgroup per span; launches by LDS size
-                    auto &pt = ptiles[sh * 64 + (e <= 16 ? 16 : 32)];
+                    auto &pt = ptiles[sh * 64 + 16];
                     for (uint64_t t = 0; t < c.B; t += sec_bs_span())
                         pt.push_back(sec::Tile{si, (uint32_t)t, 0u, copies ? 1u : 0u});
                     continue;

@@ -176,8 +176,8 @@ int sec_launch_syndrome_bs(int shape, int lanes, const uint8_t *blocks, uint8_t 
 int sec_launch_decode_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, const sec::SynDesc *descs,
                          const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream);
 // Both phases in a two-wave workgroup per span (tile t0; ntail bit 0 as above) for chunks whose
-// e <= 32 present parity rows lie in both 16-row groups, on the shapes sec_syn_pair accepts
-// (e_max: the largest e among the tiles' chunks, which sizes the kernel's LDS)
+// e <= 16 present parity rows lie in both 16-row groups, on the shapes sec_syn_pair accepts
+// (e_max: the largest e among the tiles' chunks, at most 16)
 int sec_syn_pair(int shape);
 int sec_launch_decode_bs_pair(int shape, int e_max, const uint8_t *blocks, uint8_t *out, const sec::SynDesc *descs,
                               const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream);

@@ -1188,10 +1188,10 @@ __global__ __launch_bounds__(256) void sec_decode_bs_kernel(const u8 *__restrict
     }
 }
 
-// ---- both phases for parity rows in BOTH groups: a wave pair (zfec(64,96), e <= 32) ------------
-// A chunk whose e present parity rows lie in both 16-row groups (or e > 16) has no place in the
-// one-wave kernel above (16 accumulator slots, one group's compile-time rows) and took the two
-// kernels, which read the data once per group and send the syndromes through HBM.  Here a workgroup is two
+// ---- both phases for parity rows in BOTH groups: a wave pair (zfec(64,96), e <= 16) ------------
+// A chunk whose e <= 16 present parity rows lie in both 16-row groups has no place in the one-wave
+// kernel above (16 accumulator slots, one group's compile-time rows) and took the two kernels,
+// which read the data once per group and send the syndromes through HBM.  Here a workgroup is two
 // waves over the same span, wave g holding group g's syndromes:
 //   phase 1  wave g loads, copies and transposes the present data blocks j = g mod 2 and hands
 //            their bit planes to the other wave through LDS (one s_barrier per block pair), so
@@ -1200,7 +1200,13 @@ __global__ __launch_bounds__(256) void sec_decode_bs_kernel(const u8 *__restrict
 //            copy in LDS by global rank q;
 //   phase 2  wave g solves the lost rows of 8-row groups G = g mod 2 over all e syndromes: its
 //            own from registers, the other wave's from LDS.
-// The syndromes never leave the CU: traffic is the decode's own.
+// The syndromes never leave the CU: traffic is the decode's own (1.02x, profiles/r04_syn_pmc.json).
+// Opt-in (context option SEC_SYN_PAIR = 1): on random 16-lost patterns it ties the direct decode
+// (0.78 ms per GiB, 2.75-2.83 TB/s) -- its waves wait on memory 60 % of their cycles (2-block register
+// ring, one barrier per block pair).  Also measured and dropped (r04_syn_ab_pair.jsonl): each wave
+// running the one-wave kernel's phase 1 for its own group on an LDS DMA ring (0.85 ms: every block's
+// transposes and subsets twice), and e <= 32 with 32 syndrome slots (64-72 KiB of LDS, one wave per
+// SIMD: 1.62-1.66 ms against 0.80 for the two kernels).
 template <int K, int M, int R0, int NRP, int J>
 __device__ __forceinline__ void pd_rows(u32 (&acc)[NRP * 8], const u32 *v, uint64_t pmask)
 {
@@ -1368,16 +1374,15 @@ __device__ __forceinline__ void pd_span(const u8 *__restrict__ blocks, u8 *__res
     pd_solve<K, M, R0, NRP, NR2>(std::make_integer_sequence<int, K / NR2>{}, acc, c, o, syl, lane);
 }
 
-// 128 lanes per span (tile t0), wave g = parity group g; ntail bit 0 = copy the present primaries.
-// SL syndrome slots in LDS: 16 (40 KiB, 4 workgroups per CU) or 32 (72 KiB, e > 16: 2 per CU).
-template <int K, int M, int NRP, int NR2, int D, int SL>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SL <= 16 ? 2 : 1))) void sec_decode_bs_pair_kernel(
+// 128 lanes per span (tile t0), wave g = parity group g; ntail bit 0 = copy the present primaries
+template <int K, int M, int NRP, int NR2, int D>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void sec_decode_bs_pair_kernel(
     const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::SynDesc *__restrict__ descs,
     const sec::Tile *__restrict__ tiles, const sec::SynSlots sl)
 {
     static_assert(K % 2 == 0 && M - K == 2 * NRP && K % NR2 == 0, "two parity groups over an even K");
     __shared__ u32x4 planes[2][2][2][64];  // [pair parity][wave][planes 0-3 | 4-7][lane]: 8 KiB
-    __shared__ u32x4 syl[SL][2][64];       // scaled syndrome q: 2 KiB each
+    __shared__ u32x4 syl[16][2][64];       // scaled syndrome q: 32 KiB (e <= 16)
     const sec::Tile tl = tiles[blockIdx.x];
     const sec::SynDesc d = descs[tl.chunk];
     if (tl.t0 >= d.B)
@@ -1387,86 +1392,6 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SL <= 16 ? 
         pd_span<K, M, 0, NRP, NR2, D>(blocks, out, d, sl, tl.t0, copies, planes, syl);
     else
         pd_span<K, M, NRP, NRP, NR2, D>(blocks, out, d, sl, tl.t0, copies, planes, syl);
-}
-
-// The same wave pair with each wave's phase 1 on its own (the default; SEC_PAIR_SHARED = 1 builds
-// the shared-transpose phase 1 above instead).  Measured, the shared transposes cost more than
-// they save: one s_barrier per block pair lockstepped the waves and the register ring held only
-// 2 blocks in flight (2.8 TB/s at e = 16, against 4.2 for the one-wave kernel).  Here wave g runs
-// the one-wave kernel's phase 1 for group g -- every present data block through a per-wave LDS
-// ring filled by global_load_lds, its own transposes, no barrier -- the two waves reading the
-// same blocks at the same time (the second read an L2 hit).  Then the ring's LDS becomes the
-// syndrome exchange: each wave stores its scaled syndromes at their global rank, one barrier,
-// and phase 2 as above.  LDS: max(ring, SL slots) = 32 KiB for e <= 16, 64 KiB for e <= 32.
-template <int SL>
-union PairLds {
-    LdsRing<SEC_FUSED_LDS_RING, 2> ring;  // phase 1: 8 blocks in flight per wave
-    u32x4 syl[SL][2][64];                 // phase 2: scaled syndrome q
-};
-
-template <int NRP, int r>
-__device__ __forceinline__ void pf_put(const u32 (&acc)[NRP * 8], uint64_t pm, u32 &q, u32x4 (*syl)[2][64], u32 lane)
-{
-    if (!((pm >> r) & 1))
-        return;
-    syl[q][0][lane] = u32x4{acc[r * 8 + 0], acc[r * 8 + 1], acc[r * 8 + 2], acc[r * 8 + 3]};
-    syl[q][1][lane] = u32x4{acc[r * 8 + 4], acc[r * 8 + 5], acc[r * 8 + 6], acc[r * 8 + 7]};
-    ++q;
-}
-
-template <int NRP, int... Rs>
-__device__ __forceinline__ void pf_puts(std::integer_sequence<int, Rs...>, const u32 (&acc)[NRP * 8], uint64_t pm,
-                                        u32 q, u32x4 (*syl)[2][64], u32 lane)
-{
-    (pf_put<NRP, Rs>(acc, pm, q, syl, lane), ...);
-}
-
-template <int K, int M, int R0, int NRP, int NR2, int SL>
-__device__ __forceinline__ void pf_span(const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::SynDesc &d,
-                                        const sec::SynSlots &sl, u32 s, bool copies, PairLds<SL> &lds)
-{
-    constexpr u32 w = R0 / NRP;
-    constexpr int DL = SEC_FUSED_LDS_RING;
-    const u32 B = d.B, lane = threadIdx.x & 63;
-    const SynCtx c{blocks,  sl.off,     sl.avail, sl.masks + d.wq0,     d.slot0,         min(s + 16 * lane, B - 16),
-                   min(s + 1024 + 16 * lane, B - 16), s + 16 * lane, s + 1024 + 16 * lane, d.dmask, d.pmask, 0};
-    u32 acc[NRP * 8];
-#pragma unroll
-    for (int i = 0; i < NRP * 8; ++i)
-        acc[i] = 0;
-    const u32 q0 = (u32)__builtin_popcountll(d.pmask & ((1ull << R0) - 1ull));  // this group's first rank
-    u32 q = q0;
-    u32 xs[8];
-    const ItemAddrs ia = item_addrs<K, NRP, R0>(c);
-    lds_first<K, NRP, R0, DL>(std::make_integer_sequence<int, DL>{}, lds.ring, w, xs, c, ia);
-    syn_items_lds<K, M, R0, NRP, DL, true>(std::make_integer_sequence<int, K + NRP>{}, acc, lds.ring, w, xs, c, ia,
-                                           out + d.out_off, B, d.last, copies, nullptr, q);
-    __syncthreads();  // both rings drained: the LDS becomes the syndrome slots
-    pf_puts<NRP>(std::make_integer_sequence<int, NRP>{}, acc, d.pmask >> R0, q0, lds.syl, lane);
-    __syncthreads();
-    const uint64_t lost = ~d.dmask & (K >= 64 ? ~0ull : (1ull << K) - 1ull);
-    const OutCtx o{out + d.out_off, sl.masks + d.zq0, lost, B, d.last, d.flags & 2u ? 1u : 0u, c.pa, c.pb};
-    pd_solve<K, M, R0, NRP, NR2>(std::make_integer_sequence<int, K / NR2>{}, acc, c, o, lds.syl, lane);
-}
-
-template <int K, int M, int NRP, int NR2, int SL>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(SL <= 16 ? 2 : 1))) void sec_decode_bs_pair2_kernel(
-    const u8 *__restrict__ blocks, u8 *__restrict__ out, const sec::SynDesc *__restrict__ descs,
-    const sec::Tile *__restrict__ tiles, const sec::SynSlots sl)
-{
-    static_assert(K >= 32 && M - K == 2 * NRP && K % NR2 == 0, "two parity groups, the LDS ring's k");
-    __shared__ PairLds<SL> lds;
-    const sec::Tile tl = tiles[blockIdx.x];
-    const sec::SynDesc d = descs[tl.chunk];
-    if (tl.t0 >= d.B)
-        return;
-    // wave 0 copies the present primaries (a run-time flag for both waves: with a constant false
-    // the compiler drops wave 1's stores and hoists its transposes, 1600+ spilled registers)
-    const bool first = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64, copies = (tl.ntail & 1) && first;
-    if (first)  // a scalar branch
-        pf_span<K, M, 0, NRP, NR2, SL>(blocks, out, d, sl, tl.t0, copies, lds);
-    else
-        pf_span<K, M, NRP, NRP, NR2, SL>(blocks, out, d, sl, tl.t0, copies, lds);
 }
 
 // ---- two row groups sharing each block's transpose (zfec(64,96)) ------------------------------
@@ -1783,11 +1708,7 @@ int sec_launch_decode_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *o
 
 int sec_syn_pair(int shape) { return shape == 4; }  // zfec(64,96)
 
-// SEC_PAIR_SHARED (build knob, A/B): 1 = the shared-transpose pair decode, SEC_PAIR_RING own data
-// blocks in flight per wave; 0 (default) = each wave's phase 1 on its own LDS ring
-#ifndef SEC_PAIR_SHARED
-#define SEC_PAIR_SHARED 0
-#endif
+// SEC_PAIR_RING (build knob): own data blocks in flight per wave of the pair decode
 #ifndef SEC_PAIR_RING
 #define SEC_PAIR_RING 2
 #endif
@@ -1796,25 +1717,12 @@ int sec_launch_decode_bs_pair(int shape, int e_max, const uint8_t *blocks, uint8
 {
     if (ntiles == 0)
         return hipSuccess;
-    if (shape != 4 || e_max < 1 || e_max > 32)
+    if (shape != 4 || e_max < 1 || e_max > 16)
         return hipErrorInvalidValue;
     void *a = nullptr, *b = nullptr;
     sec_next_launch_events(&a, &b);
-#if SEC_PAIR_SHARED
-    if (e_max <= 16)
-        hipExtLaunchKernelGGL((sec_decode_bs_pair_kernel<64, 96, 16, 8, SEC_PAIR_RING, 16>), dim3(ntiles), dim3(128),
-                              0, (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
-    else
-        hipExtLaunchKernelGGL((sec_decode_bs_pair_kernel<64, 96, 16, 8, SEC_PAIR_RING, 32>), dim3(ntiles), dim3(128),
-                              0, (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
-#else
-    if (e_max <= 16)
-        hipExtLaunchKernelGGL((sec_decode_bs_pair2_kernel<64, 96, 16, 8, 16>), dim3(ntiles), dim3(128), 0,
-                              (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
-    else
-        hipExtLaunchKernelGGL((sec_decode_bs_pair2_kernel<64, 96, 16, 8, 32>), dim3(ntiles), dim3(128), 0,
-                              (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
-#endif
+    hipExtLaunchKernelGGL((sec_decode_bs_pair_kernel<64, 96, 16, 8, SEC_PAIR_RING>), dim3(ntiles), dim3(128), 0,
+                          (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, descs, t, sl);
     return hipGetLastError();
 }
 
