@@ -127,6 +127,7 @@ enum Opt {
     O_SYN_FUSED,         // 0: never the one-wave fused kernel
     O_SYN_PAIR,          // 1: the two-wave kernel where it applies (default 0: ties the direct decode)
     O_SYN_RATIO,         // syndrome path taken under this many per mille of the direct estimate
+    O_SOLVE_LDS,         // 0: phase 2 of k >= 32 shapes in (span, row group) tiles, not LDS-staged spans
     O_BS,                // bit-sliced encode: -1 rule (bs_shape), 0 off, 1 every shape it has
     O_BS_LANES,          // lanes of a bit-sliced / syndrome tile (64, 128, 256)
     O_BS_SPLIT,          // 1: one launch per 16-row group (64,96)
@@ -162,6 +163,7 @@ constexpr OptSpec kOpts[O_COUNT] = {
     {"SEC_SYN_FUSED", 1, 0, 1},
     {"SEC_SYN_PAIR", 0, 0, 1},
     {"SEC_SYN_RATIO", 900, 1, 1000000},
+    {"SEC_SOLVE_LDS", 1, 0, 1},
     {"SEC_BS", -1, -1, 1},
     {"SEC_BS_LANES", 256, 64, 256},
     {"SEC_BS_SPLIT", 0, 0, 1},
@@ -524,6 +526,7 @@ void add_work(const Options &o, Bins &bins, std::vector<sec::TailItem> &tail, ui
 // (32,48) in two groups of 8 rows.
 constexpr int kBsAllGroups = 99;  // Group::U of an interleaved launch of every row group
 constexpr int kBsPair = 98;       // Group::U of a launch of two-wave workgroups (one per span, both groups)
+constexpr int kSolveLds = 1 << 16;  // phase-2 tile map keys of sec_solve_bs_lds_kernel launches
 constexpr int kDecLds = 16;       // decode bin kind of sec_decode_lds_kernel (one tile per chunk)
 
 int bs_shape(const Options &o, int k, int m, uint64_t B)
@@ -1330,6 +1333,12 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 vd.recover = recover ? 1u : 0u;
                 const uint32_t vi = (uint32_t)vdescs.size();
                 vdescs.push_back(vd);
+                if (ctx->opt[O_SOLVE_LDS] && sec_solve_lds(sh)) {  // one workgroup per span, syndromes in LDS
+                    auto &vt = vtiles[kSolveLds + sh * 64 + ((e + 7) / 8) * 8];
+                    for (uint64_t t = 0; t < c.B; t += sec_bs_span())
+                        vt.push_back(sec::Tile{vi, (uint32_t)t, 0u, 0u});
+                    continue;
+                }
                 const int NR2 = sec_solve_rows(sh);
                 std::vector<int> gl;
                 for (int g = 0; g * NR2 < k; ++g)
@@ -1448,9 +1457,12 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::SolveDesc *vd = plan.meta.as<sec::SolveDesc>(sp.off_vdesc);
     const sec::Tile *vt = plan.meta.as<sec::Tile>(sp.off_vtiles);
     for (const auto &g : sp.syn2) {
-        int e = sec_launch_solve_bs(g.first, lanes, syn, out, vd, vt + g.second.first, g.second.second, masks, s);
+        const bool staged = g.first >= kSolveLds;  // key kSolveLds + shape * 64 + LDS rows
+        int e = staged ? sec_launch_solve_bs_lds((g.first - kSolveLds) / 64, (g.first - kSolveLds) % 64, syn, out, vd,
+                                                 vt + g.second.first, g.second.second, masks, s)
+                       : sec_launch_solve_bs(g.first, lanes, syn, out, vd, vt + g.second.first, g.second.second, masks, s);
         if (e)
-            return hip_fail((hipError_t)e, "sec_solve_bs_kernel");
+            return hip_fail((hipError_t)e, staged ? "sec_solve_bs_lds_kernel" : "sec_solve_bs_kernel");
     }
     return SEC_OK;
 }

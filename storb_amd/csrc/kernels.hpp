@@ -183,6 +183,11 @@ int sec_launch_decode_bs_pair(int shape, int e_max, const uint8_t *blocks, uint8
                               const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream);
 // Phase 2: the lost data rows of row group r0 / sec_solve_rows(shape) of each tile's chunk
 int sec_solve_rows(int shape);
+// Phase 2, one workgroup per span (tile t0): the span's e <= slots syndrome rows staged in LDS once,
+// each wave one row group; on the shapes sec_solve_lds accepts (slots: a multiple of 8, <= 32)
+int sec_solve_lds(int shape);
+int sec_launch_solve_bs_lds(int shape, int slots, const uint8_t *syn, uint8_t *out, const sec::SolveDesc *descs,
+                            const sec::Tile *t, uint32_t ntiles, const uint64_t *masks, void *stream);
 int sec_launch_solve_bs(int shape, int lanes, const uint8_t *syn, uint8_t *out, const sec::SolveDesc *descs,
                         const sec::Tile *t, uint32_t ntiles, const uint64_t *masks, void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,

@@ -1093,6 +1093,83 @@ __global__ __launch_bounds__(256) SEC_SOLVE_WAVES_ATTR void sec_solve_bs_kernel(
     solve_group<K, M, NR, D>(std::make_integer_sequence<int, K / NR>{}, tl.r0, syn, out, d, masks, s);
 }
 
+// ---- phase 2 with each span's syndromes staged in LDS once (k >= 32) ---------------------------
+// sec_solve_bs_kernel's tiles are (span, 8-row group) pairs, each re-reading all e syndrome rows
+// of its span: with e = 32 spread over 8 groups its PMC showed 1.44 GB read per GiB decoded where
+// the syndromes are 0.54 (profiles/r04_syn_pmc.json).  Here a workgroup is one span and K / NR
+// waves, wave w solving 8-row group w: the e rows (2 KiB each) come into LDS once by
+// global_load_lds (spread over the waves), then every wave reads them from LDS.  LDS = e rounded
+// up to 8 rows x 2 KiB (dynamic), at most 64 KiB.
+template <int K, int M, int R0, int NR, int J>
+__device__ __forceinline__ void solve_item_lds(u32 (&acc)[NR * 8], const u32x4 (*sy)[2][64], uint64_t pmask,
+                                               uint64_t lost, u32 lane)
+{
+    if (!((pmask >> J) & 1))
+        return;
+    const u32 q = (u32)__builtin_popcountll(pmask & ((1ull << J) - 1ull));
+    const u32x4 a = sy[q][0][lane], b = sy[q][1][lane];
+    u32 lo[16], hi[16];
+    subsets(a.x, a.y, a.z, a.w, lo);
+    subsets(b.x, b.y, b.z, b.w, hi);
+    solve_rows<K, M, R0, NR, J>(std::make_integer_sequence<int, NR>{}, acc, lo, hi, lost);
+}
+
+template <int K, int M, int R0, int NR, int... Js>
+__device__ __forceinline__ void solve_span_lds(std::integer_sequence<int, Js...>, const u32x4 (*sy)[2][64],
+                                               const sec::SolveDesc &d, const uint64_t *__restrict__ masks,
+                                               u8 *__restrict__ out, u32 s, u32 lane)
+{
+    if (!((d.lost >> R0) & ((1ull << NR) - 1ull)))
+        return;
+    u32 acc[NR * 8];
+#pragma unroll
+    for (int i = 0; i < NR * 8; ++i)
+        acc[i] = 0;
+    (solve_item_lds<K, M, R0, NR, Js>(acc, sy, d.pmask, d.lost, lane), ...);
+    const OutCtx o{out + d.out_off, masks + d.zq0, d.lost, d.B, d.last, d.recover, min(s + 16 * lane, d.B - 16),
+                   min(s + 1024 + 16 * lane, d.B - 16)};
+    solve_outs<K, R0, NR>(std::make_integer_sequence<int, NR>{}, acc, o);
+}
+
+template <int K, int M, int NR, int... Gs>
+__device__ __forceinline__ void solve_groups_lds(std::integer_sequence<int, Gs...>, u32 w, const u32x4 (*sy)[2][64],
+                                                 const sec::SolveDesc &d, const uint64_t *__restrict__ masks,
+                                                 u8 *__restrict__ out, u32 s, u32 lane)
+{
+    ((w == (u32)Gs ? solve_span_lds<K, M, Gs * NR, NR>(std::make_integer_sequence<int, M - K>{}, sy, d, masks, out,
+                                                        s, lane)
+                   : void()),
+     ...);
+}
+
+template <int K, int M, int NR>
+__global__ __launch_bounds__(64 * (K / NR)) void sec_solve_bs_lds_kernel(const u8 *__restrict__ syn,
+                                                                         u8 *__restrict__ out,
+                                                                         const sec::SolveDesc *__restrict__ descs,
+                                                                         const sec::Tile *__restrict__ tiles,
+                                                                         const uint64_t *__restrict__ masks)
+{
+    static_assert(K % NR == 0 && NR <= 16, "row groups");
+    extern __shared__ u32x4 sy_dyn[];
+    auto sy = reinterpret_cast<u32x4 (*)[2][64]>(sy_dyn);
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::SolveDesc d = descs[tl.chunk];
+    const u32 s = tl.t0;
+    if (s >= d.B)  // the whole workgroup (one span)
+        return;
+    constexpr u32 W = K / NR;
+    const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const u8 *base = syn + d.syn_off + s + 16 * lane;  // rows hold whole spans: no clamping
+    const u64 stride = sec::syn_stride(d.B);
+    const u32 n = 2 * (u32)__builtin_popcountll(d.pmask);  // 1 KiB halves of the e rows
+    for (u32 i = w; i < n; i += W)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(base + (u64)(i >> 1) * stride + (i & 1) * 1024),
+                                         (__attribute__((address_space(3))) void *)&sy[i >> 1][i & 1][0], 16, 0, 0);
+    wait_vm<0>();
+    __syncthreads();
+    solve_groups_lds<K, M, NR>(std::make_integer_sequence<int, W>{}, w, sy, d, masks, out, s, lane);
+}
+
 // ---- decode, both phases in one wave (e <= 16, the present parity rows in one group) ---------
 // The scaled syndromes stay in the phase-1 accumulators (the compiler parks what does not fit
 // in the 256 VGPRs in AGPRs: one wave per SIMD), so they never go through HBM: traffic is the
@@ -1704,6 +1781,35 @@ int sec_launch_decode_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *o
     case 5: return launch_fused<8, 11, 3, R>(lanes, blocks, out, descs, t, ntiles, sl, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+int sec_solve_lds(int shape) { return shape == 3 || shape == 4; }  // zfec(32,48), (64,96)
+
+int sec_launch_solve_bs_lds(int shape, int slots, const uint8_t *syn, uint8_t *out, const sec::SolveDesc *descs,
+                            const sec::Tile *t, uint32_t ntiles, const uint64_t *masks, void *stream)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    if (slots < 1 || slots > 32)
+        return hipErrorInvalidValue;
+    const size_t lds = (size_t)slots * 2048;
+    void *a = nullptr, *b = nullptr;
+    sec_next_launch_events(&a, &b);
+    hipStream_t s = (hipStream_t)stream;
+    switch (shape) {
+    case 3:
+        if (slots > 16)
+            return hipErrorInvalidValue;
+        hipExtLaunchKernelGGL((sec_solve_bs_lds_kernel<32, 48, solve_nr(32)>), dim3(ntiles), dim3(64 * (32 / solve_nr(32))),
+                              lds, s, (hipEvent_t)a, (hipEvent_t)b, 0, syn, out, descs, t, masks);
+        break;
+    case 4:
+        hipExtLaunchKernelGGL((sec_solve_bs_lds_kernel<64, 96, solve_nr(64)>), dim3(ntiles), dim3(64 * (64 / solve_nr(64))),
+                              lds, s, (hipEvent_t)a, (hipEvent_t)b, 0, syn, out, descs, t, masks);
+        break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 int sec_syn_pair(int shape) { return shape == 4; }  // zfec(64,96)

@@ -38,10 +38,14 @@ SHAPES = [(16, 24), (32, 48), (64, 96), (10, 14), (8, 12), (8, 11)]
 
 def _engine(syn=None, fused=None):
     """A fresh context with the syndrome options forced (None: the library default).  fused = 0:
-    neither one-kernel method (the one-wave kernel, the wave pair), i.e. the two kernels."""
+    neither one-kernel method (the one-wave kernel, the wave pair), i.e. the two kernels, phase 2
+    of k >= 32 with each span's syndromes staged in LDS (sec_solve_bs_lds_kernel); "tiles": the
+    two kernels with phase 2 in (span, row group) tiles (SEC_SOLVE_LDS = 0)."""
     from storb_amd.engine import Engine
 
     opts = {}
+    if fused == "tiles":
+        fused, opts["SEC_SOLVE_LDS"] = 0, 0
     if syn is not None:
         opts["SEC_SYN"] = int(syn)
     if fused is not None:
@@ -151,10 +155,10 @@ def _run(eng, k, m, cases, recover=False, host=None):
 
 @pytest.mark.parametrize("k,m", SHAPES)
 @pytest.mark.parametrize("recover", [False, True])
-@pytest.mark.parametrize("fused", [None, 0])
+@pytest.mark.parametrize("fused", [None, 0, "tiles"])
 def test_syndrome_decode_forced_device(k, m, recover, fused):
     """SEC_SYN=1: every chunk on the syndrome path (the one-wave kernel where it applies, or with
-    SEC_SYN_FUSED=0 always the two kernels with the syndromes in HBM)."""
+    SEC_SYN_FUSED=0 always the two kernels with the syndromes in HBM; both phase-2 layouts)."""
     rng = random.Random(k * 1000 + m + recover)
     sizes = [16 * k, 17 * k - 3, 2048 * k + 5 * k, 6554 * k - 4 if k == 10 else 4099 * k - 1, 65536 * k,
              rng.randrange(20000, 300000)]
@@ -252,8 +256,9 @@ def test_syndrome_mixed_batch_with_direct_chunks():
         eng.close()
 
 
-@pytest.mark.parametrize("k,m,e,fused", [(64, 96, 32, 0), (64, 96, 24, None), (64, 96, 16, None), (64, 96, 9, None),
-                                         (64, 96, 16, 0), (32, 48, 12, None), (16, 24, 6, None)])
+@pytest.mark.parametrize("k,m,e,fused", [(64, 96, 32, 0), (64, 96, 32, "tiles"), (64, 96, 24, None),
+                                         (64, 96, 24, "tiles"), (64, 96, 16, None), (64, 96, 9, None),
+                                         (64, 96, 16, 0), (32, 48, 12, None), (32, 48, 16, 0), (16, 24, 6, None)])
 def test_syndrome_random_patterns(k, m, e, fused):
     """Random lost data blocks and random present parity rows (both parity groups of (64,96): the
     two kernels), forced onto the syndrome path, reassembled and recover-only, against the
