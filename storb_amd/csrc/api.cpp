@@ -397,13 +397,16 @@ int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, 
     // other than the (possibly short) block k-1 (kernels_bs.hip item_addrs)
     if (sh < 0 || e < 1 || e >= c.k - 1 || c.B < 16 || c.B > 0xFFFFFFFFull - 8192 || c.padlen >= c.B)
         return -1;
-    const int k = c.k, NR = sec_bs_rows(sh), NR2 = sec_solve_rows(sh);
+    // g16: 16-row data groups with a lost row, the grouping the two-kernel estimate was fitted on
+    // (r03); phase 2 now runs 8-row groups (SEC_SOLVE_NR), which measured faster, not slower, so
+    // counting its groups would steer e > 16 chunks to the direct decode (r04_syn_ab_solve.jsonl)
+    const int k = c.k, NR = sec_bs_rows(sh);
     uint64_t touched = 0, g8 = 0, g16 = 0;  // parity groups with a present row, data groups with a lost one
     for (int s = 0; s < k; ++s)
         if (idx[s] >= k) {
             touched |= 1ull << ((idx[s] - k) / NR);
             g8 |= 1ull << (s / 8);
-            g16 |= 1ull << (s / NR2);
+            g16 |= 1ull << (s / 16);
         }
     const int P = __builtin_popcountll(touched);
     const bool can_fuse = P == 1 && e <= 16 && o[O_SYN_FUSED] != 0;
