@@ -128,6 +128,7 @@ enum Opt {
     O_SYN_PAIR,          // 1: the two-wave kernel where it applies (default 0: ties the direct decode)
     O_SYN_RATIO,         // syndrome path taken under this many per mille of the direct estimate
     O_SOLVE_LDS,         // 0: phase 2 of k >= 32 shapes in (span, row group) tiles, not LDS-staged spans
+    O_SYN_WG2,           // 0: phase 1 of parity rows in both groups as one workgroup per (span, group)
     O_BS,                // bit-sliced encode: -1 rule (bs_shape), 0 off, 1 every shape it has
     O_BS_LANES,          // lanes of a bit-sliced / syndrome tile (64, 128, 256)
     O_BS_SPLIT,          // 1: one launch per 16-row group (64,96)
@@ -164,6 +165,7 @@ constexpr OptSpec kOpts[O_COUNT] = {
     {"SEC_SYN_PAIR", 0, 0, 1},
     {"SEC_SYN_RATIO", 900, 1, 1000000},
     {"SEC_SOLVE_LDS", 1, 0, 1},
+    {"SEC_SYN_WG2", 1, 0, 1},
     {"SEC_BS", -1, -1, 1},
     {"SEC_BS_LANES", 256, 64, 256},
     {"SEC_BS_SPLIT", 0, 0, 1},
@@ -530,6 +532,7 @@ void add_work(const Options &o, Bins &bins, std::vector<sec::TailItem> &tail, ui
 constexpr int kBsAllGroups = 99;  // Group::U of an interleaved launch of every row group
 constexpr int kBsPair = 98;       // Group::U of a launch of two-wave workgroups (one per span, both groups)
 constexpr int kSolveLds = 1 << 16;  // phase-2 tile map keys of sec_solve_bs_lds_kernel launches
+constexpr int kSynWg2 = 1 << 16;    // phase-1 tile map keys of sec_syndrome_bs_pair_kernel launches
 constexpr int kDecLds = 16;       // decode bin kind of sec_decode_lds_kernel (one tile per chunk)
 
 int bs_shape(const Options &o, int k, int m, uint64_t B)
@@ -1319,11 +1322,17 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                         pt.push_back(sec::Tile{si, (uint32_t)t, 0u, copies ? 1u : 0u});
                     continue;
                 }
+                if (gs.size() == 2 && sec_syn_pair(sh) && ctx->opt[O_SYN_WG2]) {  // both groups, one workgroup
+                    auto &st2 = stiles[kSynWg2 + sh];
+                    for (uint64_t t = 0; t < c.B; t += sec_bs_span())
+                        st2.push_back(sec::Tile{si, (uint32_t)t, 0u, copies ? 1u : 0u});
+                } else {
                 auto &st = stiles[sh];
                 for (uint64_t t0 = 0; t0 < c.B; t0 += 8 * step)  // runs of 8 positions per group: one XCD
                     for (int g : gs)
                         for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
                             st.push_back(sec::Tile{si, (uint32_t)t, (uint32_t)(g * NR), copies && g == gs[0] ? 1u : 0u});
+                }
                 // phase 2: the groups of lost rows, their tiles interleaved as phase 1's
                 sec::SolveDesc vd{};
                 vd.out_off = d.out_off;
@@ -1453,9 +1462,13 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
             return hip_fail((hipError_t)e, "sec_decode_bs_pair_kernel");
     }
     for (const auto &g : sp.syn1) {
-        int e = sec_launch_syndrome_bs(g.first, lanes, blocks, out, syn, sd, st + g.second.first, g.second.second, ss, s);
+        const bool wg2 = g.first >= kSynWg2;  // key kSynWg2 + shape: two-wave workgroups, both groups
+        int e = wg2 ? sec_launch_syndrome_bs_pair(g.first - kSynWg2, blocks, out, syn, sd, st + g.second.first,
+                                                  g.second.second, ss, s)
+                    : sec_launch_syndrome_bs(g.first, lanes, blocks, out, syn, sd, st + g.second.first,
+                                             g.second.second, ss, s);
         if (e)
-            return hip_fail((hipError_t)e, "sec_syndrome_bs_kernel");
+            return hip_fail((hipError_t)e, wg2 ? "sec_syndrome_bs_pair_kernel" : "sec_syndrome_bs_kernel");
     }
     const sec::SolveDesc *vd = plan.meta.as<sec::SolveDesc>(sp.off_vdesc);
     const sec::Tile *vt = plan.meta.as<sec::Tile>(sp.off_vtiles);

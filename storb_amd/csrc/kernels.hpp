@@ -171,6 +171,10 @@ int sec_syn_shape(int k, int m);
 int sec_launch_syndrome_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, uint8_t *syn,
                            const sec::SynDesc *descs, const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl,
                            void *stream);
+// Phase 1 of zfec(64,96) chunks with present parity rows in both groups: one two-wave workgroup per
+// span (tile t0; ntail bit 0 = copy the present primaries), wave g group g (sec_syn_pair shapes)
+int sec_launch_syndrome_bs_pair(int shape, const uint8_t *blocks, uint8_t *out, uint8_t *syn, const sec::SynDesc *descs,
+                                const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream);
 // Both phases in one kernel (e <= 16 and every present parity row in the tile's row group r0):
 // the syndromes stay in registers
 int sec_launch_decode_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, const sec::SynDesc *descs,

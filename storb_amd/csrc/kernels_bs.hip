@@ -872,10 +872,10 @@ __device__ __forceinline__ ItemAddrs item_addrs(const SynCtx &c)
     return ItemAddrs{addr(t), NI > 64 ? addr(64 + t) : 0};
 }
 
-template <int K, int M, int R0, int NR, int D>
+template <int K, int M, int R0, int NR, int D, class Ring>
 __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__restrict__ out, u8 *__restrict__ syn,
                                          const sec::SynDesc &d, const sec::SynSlots &sl, u32 s, bool copies,
-                                         Phase1Lds<K> &lring)
+                                         Ring &lring)
 {
     const u32 B = d.B;
     const u32 lane = (threadIdx.x & 63) * 16;
@@ -944,6 +944,31 @@ __global__ __launch_bounds__(256) SEC_SYN_WAVES_ATTR void sec_syndrome_bs_kernel
         else
             syn_span<K, M, NR, NR, D>(blocks, out, syn, d, sl, s, copies, lring);
     }
+}
+
+// Phase 1 of a chunk whose present parity rows lie in both groups (zfec(64,96)), both groups of a
+// span in one workgroup of two waves (wave g: group g, one 8-slot LDS ring each, 32 KiB).  The
+// tiles above run the groups as separate workgroups, so each group reads the span's data blocks
+// from HBM (1.55 GB read per GiB decoded at e = 32 where the blocks are 1.07,
+// profiles/r04_syn_pmc.json); here the two waves read them together and the second read hits L2.
+template <int K, int M, int NR, int D>
+__global__ __launch_bounds__(128) SEC_SYN_WAVES_ATTR void sec_syndrome_bs_pair_kernel(
+    const u8 *__restrict__ blocks, u8 *__restrict__ out, u8 *__restrict__ syn, const sec::SynDesc *__restrict__ descs,
+    const sec::Tile *__restrict__ tiles, const sec::SynSlots sl)
+{
+    static_assert(K >= 32 && M - K == 2 * NR, "two row groups on the LDS ring");
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::SynDesc d = descs[tl.chunk];
+    if (tl.t0 >= d.B)
+        return;
+    // wave 0 copies the primaries (a run-time flag in both waves: a constant false lets the
+    // compiler hoist wave 1's transposes and spill)
+    const bool first = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64, copies = (tl.ntail & 1) && first;
+    __shared__ LdsRing<SEC_FUSED_LDS_RING, 2> lring;
+    if (first)
+        syn_span<K, M, 0, NR, D>(blocks, out, syn, d, sl, tl.t0, copies, lring);
+    else
+        syn_span<K, M, NR, NR, D>(blocks, out, syn, d, sl, tl.t0, copies, lring);
 }
 
 // ---- decode, phase 2: lost row l = z_l * XOR_{r in S} c[r][l] * (w_r s_r) ----------------------
@@ -1860,5 +1885,19 @@ int sec_launch_syndrome_bs(int shape, int lanes, const uint8_t *blocks, uint8_t 
     case 5: return launch_syn<8, 11, 3, RING_K(8, 4)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+int sec_launch_syndrome_bs_pair(int shape, const uint8_t *blocks, uint8_t *out, uint8_t *syn, const sec::SynDesc *descs,
+                                const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream)
+{
+    if (ntiles == 0)
+        return hipSuccess;
+    if (shape != 4)
+        return hipErrorInvalidValue;
+    void *a = nullptr, *b = nullptr;
+    sec_next_launch_events(&a, &b);
+    hipExtLaunchKernelGGL((sec_syndrome_bs_pair_kernel<64, 96, 16, SEC_SYN_RING>), dim3(ntiles), dim3(128), 0,
+                          (hipStream_t)stream, (hipEvent_t)a, (hipEvent_t)b, 0, blocks, out, syn, descs, t, sl);
+    return hipGetLastError();
 }
 

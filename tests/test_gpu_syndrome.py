@@ -39,13 +39,15 @@ SHAPES = [(16, 24), (32, 48), (64, 96), (10, 14), (8, 12), (8, 11)]
 def _engine(syn=None, fused=None):
     """A fresh context with the syndrome options forced (None: the library default).  fused = 0:
     neither one-kernel method (the one-wave kernel, the wave pair), i.e. the two kernels, phase 2
-    of k >= 32 with each span's syndromes staged in LDS (sec_solve_bs_lds_kernel); "tiles": the
-    two kernels with phase 2 in (span, row group) tiles (SEC_SOLVE_LDS = 0)."""
+    of k >= 32 with each span's syndromes staged in LDS (sec_solve_bs_lds_kernel) and, for parity
+    rows in both groups of (64,96), phase 1 in two-wave workgroups (sec_syndrome_bs_pair_kernel);
+    "tiles": the two kernels with both phases in (span, row group) tiles (SEC_SOLVE_LDS = 0,
+    SEC_SYN_WG2 = 0)."""
     from storb_amd.engine import Engine
 
     opts = {}
     if fused == "tiles":
-        fused, opts["SEC_SOLVE_LDS"] = 0, 0
+        fused, opts["SEC_SOLVE_LDS"], opts["SEC_SYN_WG2"] = 0, 0, 0
     if syn is not None:
         opts["SEC_SYN"] = int(syn)
     if fused is not None:
