@@ -369,8 +369,9 @@ int dec_copy_kb(const Options &o, int k)
 //           syndrome scaling), phase 2 2.75 e per touched 8-row group + e^2 + 14 e;
 //           R 17, BW 5.0; the direct decode's bytes;
 //   two:    phase 1 P (k - e) 8.75 + (k - e) e + 15 e over P touched parity groups, the data
-//           read once per group (BW 5.0, or 4.0 when P = 2); phase 2 2.75 e per touched 16-row
-//           group + e^2 + 14 e, 2 e rows of syndrome traffic; R 14.5.
+//           read once per group (BW 5.0, or 4.0 when P = 2), or once when both groups share a
+//           workgroup (SEC_SYN_WG2: BW 5.0); phase 2 2.75 e per touched 16-row group + e^2 + 14 e,
+//           2 e rows of syndrome traffic; R 14.5.
 // A syndrome path is taken when its estimate is under SEC_SYN_RATIO (default 900 per mille) of
 // the direct one.  Options SEC_SYN = 0 / 1 turn the syndrome paths off / force them wherever they
 // apply (fused where eligible); SEC_SYN_FUSED = 0 turns the fused kernel off.
@@ -421,8 +422,11 @@ int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, 
     const double E = e, KE = k - e, out = copies ? k : e;
     const double direct = t(vperm_ops(e, k), 28, 4.0 * (k + out), 5.6);
     const double p2 = 2.75 * E * __builtin_popcountll(g16) + E * E + 14 * E;
-    const double two = t(P * KE * 8.75 + KE * E + 15 * E, 14.5, 4.0 * (k + (P - 1) * KE + (copies ? KE : 0) + E),
-                         P > 1 ? 4.0 : 5.0) +
+    // both groups in one two-wave workgroup (SEC_SYN_WG2): the data read once (1.07x at P = 2
+    // instead of 1.45x), which fits the r04 A/B as P = 1's bytes and rate (r04_syn_ab_final.jsonl)
+    const bool wg2 = P == 2 && sec_syn_pair(sh) && o[O_SYN_WG2] != 0;
+    const double two = t(P * KE * 8.75 + KE * E + 15 * E, 14.5,
+                         4.0 * (k + (wg2 ? 0 : (P - 1) * KE) + (copies ? KE : 0) + E), P > 1 && !wg2 ? 4.0 : 5.0) +
                        t(p2, 14.5, 4.0 * 2 * E, 5.0);
     const double fuse = can_fuse ? t(KE * (8.75 + E) + 15 * E + 2.75 * E * __builtin_popcountll(g8) + E * E + 14 * E,
                                      17, 4.0 * (k + out), 5.0)
