@@ -103,6 +103,10 @@ def test_options_listed_with_defaults_and_no_environment_reads():
     assert {"SEC_SYN", "SEC_BS", "SEC_BS_LANES", "SEC_REGISTER_MIN", "SEC_HOST_JOIN"} <= set(names)
     assert engine.option_default("SEC_SYN") == -1 and engine.option_default("SEC_BS_LANES") == 256
     assert engine.option_default("SEC_REGISTER_MIN") == 4 << 20
+    # the round-4 A/B outcomes: the kernels that lost are opt-in, the winners on
+    for name, want in (("SEC_BS_LDS", 0), ("SEC_DEC_LDS", 0), ("SEC_BS_PAIR", 0), ("SEC_SYN_PAIR", 0),
+                       ("SEC_SOLVE_LDS", 1), ("SEC_SYN_WG2", 1)):
+        assert engine.option_default(name) == want, name
     lib = _lib.load()
     v = ctypes.c_int64(0)
     assert lib.sec_ctx_get_option(None, b"SEC_NOPE", ctypes.byref(v)) == _lib.SEC_EINVAL
