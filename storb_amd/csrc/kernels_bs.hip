@@ -1167,51 +1167,6 @@ __device__ __forceinline__ void solve_groups_lds(std::integer_sequence<int, Gs..
      ...);
 }
 
-// SEC_SOLVE_SPLIT (build knob, A/B): the rows of the lower half of the parity rows come in first
-// (loaded by the first half of the waves), every wave applies them while the upper half's loads
-// are in flight, then one more barrier and the upper half.
-#ifndef SEC_SOLVE_SPLIT
-#define SEC_SOLVE_SPLIT 1
-#endif
-template <int K, int M, int R0, int NR, int OFF, int... Js>
-__device__ __forceinline__ void solve_part_lds(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8],
-                                               const u32x4 (*sy)[2][64], const sec::SolveDesc &d, u32 lane)
-{
-    (solve_item_lds<K, M, R0, NR, OFF + Js>(acc, sy, d.pmask, d.lost, lane), ...);
-}
-
-template <int K, int M, int R0, int NR>
-__device__ __forceinline__ void solve_span_lds2(const u32x4 (*sy)[2][64], const sec::SolveDesc &d,
-                                                const uint64_t *__restrict__ masks, u8 *__restrict__ out, u32 s,
-                                                u32 lane, bool late)
-{
-    constexpr int H = (M - K) / 2;
-    const bool any = (d.lost >> R0) & ((1ull << NR) - 1ull);  // no early return: two barriers below
-    u32 acc[NR * 8];
-#pragma unroll
-    for (int i = 0; i < NR * 8; ++i)
-        acc[i] = 0;
-    if (any)
-        solve_part_lds<K, M, R0, NR, 0>(std::make_integer_sequence<int, H>{}, acc, sy, d, lane);
-    if (late)
-        wait_vm<0>();
-    __syncthreads();  // the upper half's rows in LDS
-    if (!any)
-        return;
-    solve_part_lds<K, M, R0, NR, H>(std::make_integer_sequence<int, M - K - H>{}, acc, sy, d, lane);
-    const OutCtx o{out + d.out_off, masks + d.zq0, d.lost, d.B, d.last, d.recover, min(s + 16 * lane, d.B - 16),
-                   min(s + 1024 + 16 * lane, d.B - 16)};
-    solve_outs<K, R0, NR>(std::make_integer_sequence<int, NR>{}, acc, o);
-}
-
-template <int K, int M, int NR, int... Gs>
-__device__ __forceinline__ void solve_groups_lds2(std::integer_sequence<int, Gs...>, u32 w, const u32x4 (*sy)[2][64],
-                                                  const sec::SolveDesc &d, const uint64_t *__restrict__ masks,
-                                                  u8 *__restrict__ out, u32 s, u32 lane, bool late)
-{
-    ((w == (u32)Gs ? solve_span_lds2<K, M, Gs * NR, NR>(sy, d, masks, out, s, lane, late) : void()), ...);
-}
-
 template <int K, int M, int NR>
 __global__ __launch_bounds__(64 * (K / NR)) void sec_solve_bs_lds_kernel(const u8 *__restrict__ syn,
                                                                          u8 *__restrict__ out,
@@ -1231,22 +1186,6 @@ __global__ __launch_bounds__(64 * (K / NR)) void sec_solve_bs_lds_kernel(const u
     const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const u8 *base = syn + d.syn_off + s + 16 * lane;  // rows hold whole spans: no clamping
     const u64 stride = sec::syn_stride(d.B);
-#if SEC_SOLVE_SPLIT
-    static_assert(W % 2 == 0, "two halves of the waves");
-    constexpr int H = (M - K) / 2;
-    const u32 e = (u32)__builtin_popcountll(d.pmask), n0 = (u32)__builtin_popcountll(d.pmask & ((1ull << H) - 1ull));
-    const bool late = w >= W / 2;  // this wave loads the upper half's rows
-    const u32 q0 = late ? n0 : 0u, n = 2 * (late ? e - n0 : n0);
-    for (u32 i = w % (W / 2); i < n; i += W / 2) {
-        const u32 q = q0 + (i >> 1);
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(base + (u64)q * stride + (i & 1) * 1024),
-                                         (__attribute__((address_space(3))) void *)&sy[q][i & 1][0], 16, 0, 0);
-    }
-    if (!late)
-        wait_vm<0>();
-    __syncthreads();  // the lower half's rows in LDS
-    solve_groups_lds2<K, M, NR>(std::make_integer_sequence<int, W>{}, w, sy, d, masks, out, s, lane, late);
-#else
     const u32 n = 2 * (u32)__builtin_popcountll(d.pmask);  // 1 KiB halves of the e rows
     for (u32 i = w; i < n; i += W)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(base + (u64)(i >> 1) * stride + (i & 1) * 1024),
@@ -1254,7 +1193,6 @@ __global__ __launch_bounds__(64 * (K / NR)) void sec_solve_bs_lds_kernel(const u
     wait_vm<0>();
     __syncthreads();
     solve_groups_lds<K, M, NR>(std::make_integer_sequence<int, W>{}, w, sy, d, masks, out, s, lane);
-#endif
 }
 
 // ---- decode, both phases in one wave (e <= 16, the present parity rows in one group) ---------
