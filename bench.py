@@ -126,6 +126,15 @@ def parse(argv=None):
                     help="c5: skip the end-to-end host steps (rocprofv3 PMC passes of the device-resident kernels)")
     ap.add_argument("--no-events", action="store_true",
                     help="A/B only: no per-launch HIP events in the timed region (roofline fields then null)")
+    ap.add_argument("--in-process", action="store_true",
+                    help="drive the N devices from ONE process (engine.EngineGroup: a host thread and context per "
+                         "device) instead of one rank per GPU; the headline and C5 lines in that form")
+    ap.add_argument("--inproc-devices", default=None,
+                    help="rehearsal only: comma list of the devices the in-process form drives (default 0..N-1; "
+                         "'0,0' puts two contexts on one GPU)")
+    ap.add_argument("--no-in-process", action="store_true",
+                    help="c2c3 under N > 1 ranks: skip the nested in-process measurement rank 0 takes after the "
+                         "rank-per-GPU lines (the other ranks wait on a CPU barrier meanwhile)")
     return ap.parse_args(argv)
 
 
@@ -609,6 +618,20 @@ def main_c2c3(args, ctx):
         res["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     elif ctx.rank == 0:
         res["cpu_baseline"] = None
+    # N > 1 ranks: the same workloads from ONE process over all N devices (engine.EngineGroup),
+    # taken by rank 0 after every rank-per-GPU measurement while the other ranks wait on a CPU
+    # (gloo) barrier with their buffers freed: reported beside `value`, never as it
+    if ctx.world > 1 and not args.no_in_process and not os.environ.get("STORB_BENCH_ENGINE"):
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        cpu_grp = ctx.dmod.new_group(backend="gloo")
+        ctx.dmod.barrier(group=cpu_grp)
+        if ctx.rank == 0:
+            try:
+                res["in_process"] = inproc_results(args, ctx.world)
+            except Exception as e:  # noqa: BLE001 - the rank-per-GPU line stands on its own
+                res["in_process"] = {"error": f"{type(e).__name__}: {e}"}
+        ctx.dmod.barrier(group=cpu_grp)
     if ctx.rank == 0:
         print(json.dumps(res), flush=True)
 
@@ -948,8 +971,186 @@ def e2e_rate(eng, nchunks=1024, steps=3) -> dict:
                       f"Engine.host_empty buffers; the kernels read / write locked or pinned host memory over PCIe"}
 
 
+# ---------------------------------------------------------------- in-process multi-device (EngineGroup)
+def _inproc_timed(grp, prep, body, steps, done=None):
+    """The timed region of the in-process form: every worker prepares (warm-up, device sync) on
+    its own thread, then all start together behind a thread barrier; the clock runs from the
+    barrier until the LAST device has synchronised after its `steps` bodies.  Returns (elapsed
+    seconds, per-worker results of `done`)."""
+    import threading
+
+    n = len(grp)
+    states = [f.result() for f in [grp.submit(i, prep, i) for i in range(n)]]
+    gate = threading.Barrier(n + 1)
+
+    def run(i, st):
+        gate.wait()
+        for _ in range(steps):
+            body(st)
+        st["eng"].sync()
+        return time.perf_counter()
+
+    futs = [grp.submit(i, run, i, st) for i, st in enumerate(states)]
+    gate.wait()
+    t0 = time.perf_counter()
+    t1 = max(f.result() for f in futs)
+    res = [f.result() for f in [grp.submit(i, done, st) for i, st in enumerate(states)]] if done else None
+    return t1 - t0, res
+
+
+def inproc_c2c3(grp, steps, warmup, nchunks=N_CHUNKS) -> dict:
+    """The headline workload on every device of `grp` from ONE process and one host thread per
+    device (engine.EngineGroup): each device owns its own 1024 x 1 MiB
+    RS(4,2) chunks (weak scaling, as the torchrun form); value = all devices' chunk bytes
+    encoded + decoded / wall time of the slowest."""
+    import torch
+
+    from storb_amd.engine import get_engine
+
+    def prep(i):
+        d = grp.devices[i]
+        torch.cuda.set_device(d)
+        eng = get_engine()
+        n, k, m = CHUNK, K, M
+        g = torch.Generator(device=f"cuda:{d}")
+        g.manual_seed(1000 + i)
+        src = torch.randint(0, 256, (nchunks * n,), dtype=torch.uint8, device=f"cuda:{d}", generator=g)
+        ed, B = enc_descs(nchunks, n, k, m)
+        par = torch.empty(nchunks * (m - k) * B, dtype=torch.uint8, device=f"cuda:{d}")
+        out = torch.empty_like(src)
+        dd, sn, offs, av = dec_descs(nchunks, n, k, m, B, src.data_ptr(), par.data_ptr(), ERASED)
+        st = {"eng": eng, "ed": ed, "src": src, "par": par, "out": out, "dd": dd, "sn": sn, "offs": offs, "av": av}
+        for _ in range(max(warmup, 1)):
+            body(st)
+        eng.sync()
+        if not torch.equal(out, src):
+            raise SystemExit(f"bench in-process: device {d} (worker {i}) round trip mismatch")
+        return st
+
+    def body(st):
+        st["eng"].encode_batch(st["ed"], st["src"], st["par"], asynchronous=True)
+        st["eng"].decode_batch(st["dd"], st["sn"], st["offs"], 0, st["out"], block_avail=st["av"], asynchronous=True)
+
+    def done(st):
+        for key in ("src", "par", "out"):
+            st.pop(key)
+        torch.cuda.empty_cache()
+
+    el, _ = _inproc_timed(grp, prep, body, steps, done)
+    nbytes = len(grp) * nchunks * 2 * CHUNK
+    return {"value": round(steps * nbytes / el / GIB, 3), "unit": "GiB/s", "n_gpus": len(grp), "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 4), "scaling": "weak", "devices": list(grp.devices),
+            "workload": f"{nchunks} x 1 MiB chunks per GPU, RS(4,2): encode + {{1,3}}-erased decode/reassemble",
+            "launch": "one process, one host thread + libstorbec context per device (engine.EngineGroup)"}
+
+
+def inproc_c5(grp, steps, warmup, total=1 << 30) -> dict:
+    """BASELINE configs[4] end to end from pinned host memory over every device of `grp`, one
+    process: the job's chunks split by bytes (dist.partition), each device's share in pinned
+    buffers its own context allocated, encoded + decoded over PCIe by its own worker thread
+    (strong scaling, as the torchrun form)."""
+    from storb_amd import dist as D
+    from storb_amd.engine import get_engine
+
+    sizes_all = c5_sizes(total)
+    parts = D.partition(sizes_all, len(grp))
+    k, m = C5_K, C5_M
+
+    def prep(i):
+        eng = get_engine()
+        lo, hi = parts[i]
+        sizes = sizes_all[lo:hi]
+        nbytes = int(np.sum(sizes)) if sizes else 0
+        st = {"eng": eng, "n": hi - lo, "bytes": nbytes}
+        if not sizes:
+            return st
+        ed, B = enc_descs_var(sizes, k, m)
+        npar = int(np.sum(B)) * (m - k)
+        host = eng.host_empty(nbytes)
+        host[:] = np.random.default_rng(5_000_000 + lo).integers(0, 256, nbytes, dtype=np.uint8)
+        hpar, hout = eng.host_empty(max(npar, 1)), eng.host_empty(max(nbytes, 1))
+        dd, sn, offs, av = dec_descs_var(sizes, k, m, B, host.ctypes.data, hpar.ctypes.data, C5_ERASED)
+        st.update(ed=ed, host=host, hpar=hpar, hout=hout, dd=dd, sn=sn, offs=offs, av=av)
+        for _ in range(max(warmup, 1)):
+            body(st)
+        if not np.array_equal(hout[:nbytes], host):
+            raise SystemExit(f"bench in-process c5: worker {i} round trip mismatch")
+        return st
+
+    def body(st):
+        if st["n"]:
+            st["eng"].encode_batch(st["ed"], st["host"], st["hpar"], host=True)
+            st["eng"].decode_batch(st["dd"], st["sn"], st["offs"], 0, st["hout"], block_avail=st["av"], host=True)
+
+    def done(st):
+        ok = (not st["n"]) or np.array_equal(st["hout"][:st["bytes"]], st["host"])
+        for key in ("host", "hpar", "hout"):
+            st.pop(key, None)
+        return ok
+
+    el, oks = _inproc_timed(grp, prep, body, steps, done)
+    if not all(oks):
+        raise SystemExit("bench in-process c5: output mismatch after the timed steps")
+    job = int(np.sum(sizes_all))
+    return {"value": round(steps * 2 * job / el / GIB, 3), "unit": "GiB/s", "n_gpus": len(grp), "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 4), "scaling": "strong", "devices": list(grp.devices),
+            "per_device_chunks": [hi - lo for lo, hi in parts],
+            "workload": f"BASELINE configs[4]: {len(sizes_all)} chunks, {job} B, RS(8,3), encode + {{1,3,5}}-erased "
+                        "decode from pinned host memory (zero-copy kernels over PCIe), split by bytes",
+            "launch": "one process, one host thread + libstorbec context per device (engine.EngineGroup)"}
+
+
+def inproc_devices(args, ndev) -> list[int]:
+    if args.inproc_devices:
+        devs = [int(x) for x in args.inproc_devices.split(",")]
+        if len(devs) != ndev:
+            raise SystemExit(f"bench: --inproc-devices names {len(devs)} devices, the run has {ndev}")
+        return devs
+    return list(range(ndev))
+
+
+def inproc_results(args, ndev) -> dict:
+    from storb_amd.engine import EngineGroup
+
+    grp = EngineGroup(inproc_devices(args, ndev))
+    try:
+        res = {"c2c3": inproc_c2c3(grp, args.steps, args.warmup, args.chunks)}
+        if not args.no_c5:
+            res["c5"] = inproc_c5(grp, args.c5_steps, min(args.warmup, 2), args.c5_bytes)
+    finally:
+        grp.close()
+    return res
+
+
+def main_in_process(args) -> None:
+    """`--in-process`: the N devices from this one process (no ranks); one JSON line whose value
+    is the in-process headline, with the in-process C5 line nested."""
+    import torch
+
+    n = args.gpus
+    if max(inproc_devices(args, n)) >= torch.cuda.device_count():
+        raise SystemExit(f"bench --in-process: devices {inproc_devices(args, n)} asked, "
+                         f"{torch.cuda.device_count()} visible")
+    r = inproc_results(args, n)
+    h = r["c2c3"]
+    res = {"metric": "GiB/s device-resident RS encode+decode, 1 MiB chunks, 1/2/4/8 MI355X",
+           "value": h["value"], "unit": "GiB/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": h["ms_per_step"], "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "u8", "data": "synthetic (torch.randint uniform bytes, seeded per device), HBM-resident",
+           "config": {"workload": h["workload"], "chunks_per_gpu": args.chunks, "world_size": 1,
+                      "parallelism": f"in-process x{n} (engine.EngineGroup)", "launch": h["launch"]},
+           "lib_digest": lib_digest(), "in_process": r}
+    print(json.dumps(res), flush=True)
+
+
 def main(argv=None):
     args = parse(argv)
+    if args.in_process:
+        if os.environ.get("WORLD_SIZE", "1") != "1":
+            print("bench: --in-process runs as ONE process (not under torch.distributed.run)", file=sys.stderr)
+            sys.exit(2)
+        main_in_process(args)
+        return
     rc = spawn_ranks(args, argv)
     if rc is not None:
         sys.exit(rc)

@@ -90,8 +90,12 @@ class Engine:
         if rc:
             raise ECRuntimeError(f"cannot create HIP context on device {self.device}: {_lib.strerror(rc)}")
         self._ctx = h
-        for k, v in (options or {}).items():  # sec_ctx_set_option: forced plan choices (tests, A/B)
-            self.set_option(k, int(v))
+        try:
+            for k, v in (options or {}).items():  # sec_ctx_set_option: forced plan choices (tests, A/B)
+                self.set_option(k, int(v))
+        except BaseException:  # an unknown option or a bad value: no context left behind
+            self.close()
+            raise
 
     def _check(self, rc: int) -> None:
         check(rc, self.lib)
@@ -343,6 +347,19 @@ class Engine:
         """
         return b"".join(self._decode_parts(items, per_chunk=False))
 
+    def decode_host_into(self, items, dst: np.ndarray) -> int:
+        """``decode_host`` written into `dst` (a writable uint8 array) instead of a new bytes
+        object: the output of a share of a multi-device call lands straight in the caller's
+        result.  Returns the bytes written; ValueError when `dst` is too small."""
+        off = 0
+        for v in self._decode_parts(items, per_chunk=False):
+            n = len(v)
+            if off + n > dst.size:
+                raise ValueError("decode_host_into: destination too small")
+            dst[off:off + n] = np.frombuffer(v, dtype=np.uint8)
+            off += n
+        return off
+
     def decode_host_chunks(self, items) -> list[bytes]:
         """``decode_host``, one bytes object per chunk."""
         return self._decode_parts(items, per_chunk=True)
@@ -487,10 +504,43 @@ def decode_matrix(k: int, m: int, sharenums) -> tuple[bytes, list[int]]:
 
 
 _tls = threading.local()
+_spread = {"devices": None, "next": 0}
+_spread_lock = threading.Lock()
+
+
+def spread_threads(devices) -> None:
+    """Give each host thread that first asks for an engine without naming a device (and is not
+    an EngineGroup worker) the next device of `devices`, round robin; None: every thread uses
+    default_device().  A multi-threaded caller (the validator serves uploads and downloads on
+    executor threads) then spreads its per-chunk calls over the GPUs.  A thread keeps the
+    device it was given."""
+    with _spread_lock:
+        _spread["devices"] = None if devices is None else [int(d) for d in devices]
+        _spread["next"] = 0
+
+
+def _thread_device():
+    devs = _spread["devices"]
+    if devs is None:
+        return None
+    mine = getattr(_tls, "spread", None)
+    if mine is not None and mine[0] is devs:
+        return mine[1]
+    with _spread_lock:
+        d = devs[_spread["next"] % len(devs)]
+        _spread["next"] += 1
+    _tls.spread = (devs, d)
+    return d
 
 
 def get_engine(device: int | None = None) -> Engine:
-    """The calling thread's engine for `device` (default: STORB_EC_DEVICE / LOCAL_RANK / 0)."""
+    """The calling thread's engine for `device` (default: the engine of the EngineGroup worker
+    this thread is, else STORB_EC_DEVICE / LOCAL_RANK / 0)."""
+    if device is None:
+        bound = getattr(_tls, "bound", None)
+        if bound is not None:
+            return bound
+        device = _thread_device()
     dev = default_device() if device is None else int(device)
     engines = getattr(_tls, "engines", None)
     if engines is None:
@@ -499,3 +549,107 @@ def get_engine(device: int | None = None) -> Engine:
     if eng is None:
         eng = engines[dev] = Engine(dev)
     return eng
+
+
+class EngineGroup:
+    """Several devices driven from ONE process: one worker thread per
+    entry of `devices`, each holding its own Engine (its own libstorbec context and streams on
+    that device).  Chunks are independent (/root/reference/storb/validator/validator.py:1352-1431
+    handles them one by one), so a batch is split into contiguous ranges balanced by bytes
+    (``dist.partition``), each range runs on its worker, and the results come back in chunk
+    order.  No collective and no peer traffic: every device reads and writes only its own share.
+
+    ``devices=None`` uses every visible device.  An entry may repeat (``[0, 0]``: two contexts
+    on one GPU, each with its own worker), so the split, the threads and the reassembly can be
+    tested on a one-GPU box.  Inside a worker, ``get_engine()`` (no argument) returns that
+    worker's engine, so the piece-level batch functions run unchanged on each share.
+
+    ``engine_factory(device)`` (tests only) builds the per-worker engine instead of Engine.
+    """
+
+    def __init__(self, devices=None, engine_factory=None):
+        from concurrent.futures import ThreadPoolExecutor
+
+        if devices is None:
+            devices = list(range(device_count()))
+        self.devices = [int(d) for d in devices]
+        if not self.devices:
+            raise ECRuntimeError("EngineGroup: no HIP device available")
+        make = engine_factory or (lambda d: Engine(d))
+        self._workers = []
+        self._engines = []
+        try:
+            for i, d in enumerate(self.devices):
+                w = ThreadPoolExecutor(1, thread_name_prefix=f"storb_amd_dev{d}_{i}")
+                self._workers.append(w)
+                # the engine is created on its own worker thread and bound there
+                self._engines.append(w.submit(self._bind, make, d).result())
+        except BaseException:
+            self.close()
+            raise
+
+    @staticmethod
+    def _bind(make, d):
+        eng = make(d)
+        _tls.bound = eng
+        return eng
+
+    def __len__(self) -> int:
+        return len(self.devices)
+
+    @property
+    def engines(self) -> list:
+        return list(self._engines)
+
+    def submit(self, i: int, fn, *args, **kw):
+        """Run fn(*args, **kw) on worker i (whose ``get_engine()`` is engine i); a Future."""
+        return self._workers[i].submit(fn, *args, **kw)
+
+    def shares(self, sizes) -> list[tuple[int, int]]:
+        """Contiguous [lo, hi) ranges of the items, one per worker, balanced by `sizes`."""
+        from .dist import partition
+
+        return partition(sizes, len(self.devices))
+
+    def map_shares(self, fn, items, sizes) -> list:
+        """fn(items[lo:hi], lo) on every worker's share at once; returns the per-share results
+        in share (= item) order.  Every share runs to completion; then the error of the FIRST
+        failing share (the one holding the earliest chunk) is raised, as a single-device call
+        over the whole batch would raise for that chunk."""
+        futs = [(self.submit(i, fn, items[lo:hi], lo) if hi > lo else None)
+                for i, (lo, hi) in enumerate(self.shares(sizes))]
+        res, err = [], None
+        for f in futs:
+            if f is None:
+                res.append(None)
+                continue
+            try:
+                res.append(f.result())
+            except BaseException as e:  # noqa: BLE001 - re-raised below, in chunk order
+                res.append(None)
+                if err is None:
+                    err = e
+        if err is not None:
+            raise err
+        return res
+
+    def sync(self) -> None:
+        for f in [self.submit(i, e.sync) for i, e in enumerate(self._engines)]:
+            f.result()
+
+    def close(self) -> None:
+        for i, w in enumerate(self._workers):
+            eng = self._engines[i] if i < len(self._engines) else None
+            if eng is not None:
+                try:
+                    w.submit(eng.close).result()
+                except Exception:  # noqa: BLE001 - closing: best effort
+                    pass
+            w.shutdown(wait=True)
+        self._workers, self._engines = [], []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

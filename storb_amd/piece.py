@@ -28,6 +28,10 @@ Deliberate differences (documented in DESIGN.md §Boundary):
   that digest when ``data`` is one of those very piece objects (identity, not equality), so
   the validator's ``piece_hash`` right after ``encode_chunk`` (validator.py:1081) does not
   hash serially.  Same digests either way; ``PREFETCH_PIECE_IDS = False`` turns it off.
+* several GPUs in one process: the batch and stream functions take ``devices=`` (or the
+  module default ``use_devices(...)``) and split their chunks over those devices
+  (``engine.EngineGroup``: one worker thread and HIP context per device, chunks partitioned
+  by bytes, results in chunk order).  Same bytes as one device.
 """
 
 from __future__ import annotations
@@ -40,7 +44,7 @@ import os
 import platform
 import threading
 import typing
-from collections import OrderedDict
+from collections import OrderedDict, deque
 from collections.abc import Iterable, Iterator
 from concurrent.futures import Future, ThreadPoolExecutor
 from enum import IntEnum
@@ -50,7 +54,7 @@ from pydantic import BaseModel, ConfigDict, Field
 
 from .constants import MAX_PIECE_SIZE, MIN_PIECE_SIZE, PIECE_LENGTH_OFFSET, PIECE_LENGTH_SCALING
 from .easyfec import Decoder, Encoder, Error
-from .engine import check_decode_item, choose_blocks, get_engine
+from .engine import EngineGroup, check_decode_item, choose_blocks, device_count, get_engine, spread_threads
 
 logger = logging.getLogger(__name__)
 
@@ -58,7 +62,7 @@ __all__ = [
     "PieceType", "Piece", "EncodedChunk", "ProcessedPieceInfo", "EncodedPieces", "piece_hash", "piece_length",
     "encode_chunk", "decode_chunk", "reconstruct_data", "reconstruct_data_stream", "encode_chunks",
     "decode_chunks", "chunk_shape", "piece_hashes", "encode_chunks_with_ids", "encode_chunks_stream", "Encoder",
-    "Decoder", "Error",
+    "Decoder", "Error", "use_devices",
 ]
 
 PREFETCH_PIECE_IDS = True  # encode_chunk hashes its pieces on a thread pool (see module doc)
@@ -182,6 +186,46 @@ def _stream_pool() -> ThreadPoolExecutor:
         i = _stream_rr[0] % max(1, STREAM_WORKERS)
         _stream_rr[0] += 1
     return _pool(f"stream{i}")
+
+
+_ONE = "one"  # devices=_ONE: the calling thread's own engine (inside an EngineGroup worker: its device)
+_default_devices = None  # use_devices()
+_groups: dict = {}
+
+
+def use_devices(devices) -> None:
+    """Module default of the batch and stream functions' ``devices=``: None (one device, the
+    calling thread's engine: the default), "all" (every visible device), a list of device ids,
+    or an EngineGroup.  A single-process validator (/root/reference/storb/validator/
+    __main__.py:10-24) calls this once at start-up and then drives every GPU through the
+    unchanged names: encode_chunks / decode_chunks / reconstruct_data split each batch by bytes
+    over the devices, the *_stream pipelines send windows round robin to them, and the per-chunk
+    calls (encode_chunk, decode_chunk) of different host threads are spread over them
+    (engine.spread_threads)."""
+    global _default_devices
+    grp = _group(devices) if devices is not None else None
+    _default_devices = grp
+    spread_threads(grp.devices if grp is not None else None)
+
+
+def _group(devices):
+    """The EngineGroup for a ``devices=`` argument (None: the module default), or None for the
+    one-device path.  Groups are created once per device list and kept (each holds a HIP
+    context and a worker thread per device)."""
+    if devices is _ONE:
+        return None
+    if devices is None:
+        devices = _default_devices
+        if devices is None:
+            return None
+    if isinstance(devices, EngineGroup):
+        return devices
+    key = "all" if isinstance(devices, str) and devices == "all" else tuple(int(d) for d in devices)
+    with _pools_lock:
+        g = _groups.get(key)
+        if g is None:
+            g = _groups[key] = EngineGroup(list(range(device_count())) if key == "all" else list(key))
+    return g
 
 
 def _sha1_hex(b) -> str:
@@ -497,8 +541,11 @@ def encode_chunk(chunk: bytes, chunk_idx: int) -> EncodedChunk:
     return enc
 
 
-def encode_chunks(chunks: typing.Sequence[bytes], first_chunk_idx: int = 0) -> list[EncodedChunk]:
-    """Batched ``encode_chunk`` over many chunks in ONE GPU call; chunk i gets index first+i."""
+def encode_chunks(chunks: typing.Sequence[bytes], first_chunk_idx: int = 0, *, devices=None) -> list[EncodedChunk]:
+    """Batched ``encode_chunk`` over many chunks in ONE GPU call; chunk i gets index first+i.
+
+    devices (or the module default set by ``use_devices``): the chunks are split by bytes over
+    those devices' workers (``EngineGroup``), one GPU call per device, results in chunk order."""
     shapes = []
     for c in chunks:
         n = len(c)
@@ -506,6 +553,11 @@ def encode_chunks(chunks: typing.Sequence[bytes], first_chunk_idx: int = 0) -> l
         shapes.append(chunk_shape(n))
     if not chunks:
         return []
+    grp = _group(devices)
+    if grp is not None:
+        parts = grp.map_shares(lambda share, lo: encode_chunks(share, first_chunk_idx + lo, devices=_ONE),
+                               list(chunks), [len(c) for c in chunks])
+        return [ec for p in parts if p for ec in p]
     if min(B for (_, _, B, _) in shapes) >= PARALLEL_COPY_MIN:  # piece copies in parallel
         pieces = _pieces_parallel(list(chunks), shapes)
         return [_build(first_chunk_idx + i, k, m, B, padlen, len(c), ps)
@@ -562,8 +614,13 @@ def decode_chunk(encoded_chunk: EncodedChunk, *, positional_sharenums: bool = Fa
     return decoder.decode(blocks, sharenums, encoded_chunk.padlen)
 
 
-def decode_chunks(encoded_chunks: typing.Sequence[EncodedChunk], *, positional_sharenums: bool = False) -> bytes:
-    """Batched ``decode_chunk``: the concatenation of every chunk's bytes, one GPU call."""
+def decode_chunks(encoded_chunks: typing.Sequence[EncodedChunk], *, positional_sharenums: bool = False,
+                  devices=None) -> bytes:
+    """Batched ``decode_chunk``: the concatenation of every chunk's bytes, one GPU call.
+
+    devices (or the module default set by ``use_devices``): the chunks are split by bytes over
+    those devices' workers, each share decoded by its own device straight into its slice of the
+    result (one copy, as on one device)."""
     items = []
     for ch in encoded_chunks:
         if not (1 <= ch.k <= ch.m <= 256):
@@ -574,7 +631,22 @@ def decode_chunks(encoded_chunks: typing.Sequence[EncodedChunk], *, positional_s
             # out-of-range padlen: keep easyfec's slicing semantics on the per-chunk path
             return b"".join(decode_chunk(c, positional_sharenums=positional_sharenums) for c in encoded_chunks)
         items.append((ch.k, ch.m, blocks, sharenums, ch.padlen))
-    return get_engine().decode_host(items) if items else b""
+    if not items:
+        return b""
+    grp = _group(devices)
+    if grp is None:
+        return get_engine().decode_host(items)
+    for it in items:  # zfec's preconditions for every chunk before any device starts
+        check_decode_item(*it)
+    lens = [k * len(blocks[0]) - padlen for (k, _, blocks, _, padlen) in items]
+    starts = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    out, view = _new_bytes(int(starts[-1]))
+
+    def share(its, lo):
+        return get_engine().decode_host_into(its, view[starts[lo]:starts[lo + len(its)]])
+
+    grp.map_shares(share, items, lens)
+    return _finalize(out)
 
 
 def _relevant(pieces: list[Piece], chunk: EncodedChunk) -> list[Piece]:
@@ -585,8 +657,9 @@ def _relevant(pieces: list[Piece], chunk: EncodedChunk) -> list[Piece]:
     return relevant
 
 
-def reconstruct_data(pieces: list[Piece], chunks: list[EncodedChunk]) -> bytes:
-    """Reconstruct the original bytes from pieces (piece.py:201-236), one batched decode."""
+def reconstruct_data(pieces: list[Piece], chunks: list[EncodedChunk], *, devices=None) -> bytes:
+    """Reconstruct the original bytes from pieces (piece.py:201-236), one batched decode (per
+    device with `devices` / ``use_devices``: see decode_chunks)."""
     by_chunk: dict[int, list[Piece]] = {}
     for p in pieces:
         by_chunk.setdefault(p.chunk_idx, []).append(p)
@@ -595,7 +668,7 @@ def reconstruct_data(pieces: list[Piece], chunks: list[EncodedChunk]) -> bytes:
         if len(relevant) < chunk.k:
             raise ValueError(f"Not enough pieces to reconstruct chunk {chunk.chunk_idx}")
         chunk.pieces = relevant
-    return decode_chunks(chunks)
+    return decode_chunks(chunks, devices=devices)
 
 
 def _windows(chunks, nbytes, size_of) -> Iterator[list]:
@@ -645,36 +718,60 @@ def _decode_window(window: list, by_chunk: dict):
 
 
 def reconstruct_data_stream(pieces: list[Piece], chunks: list[EncodedChunk], *,
-                            window_bytes: int | None = None) -> Iterator[bytes]:
+                            window_bytes: int | None = None, devices=None) -> Iterator[bytes]:
     """Yield the reconstructed bytes chunk by chunk (piece.py:239-263).
 
     Chunks go in windows of about `window_bytes` (default STREAM_WINDOW_BYTES) of output; each
     window is one batched decode on a worker thread, and window w+1's decode runs while the
     caller consumes window w (the validator streams them into the HTTP response,
-    validator.py:1630-1638).  Chunks come out in order; a chunk without enough pieces raises
-    the reference's ValueError when the stream reaches it, after every earlier chunk."""
+    validator.py:1630-1638).  With `devices` (or ``use_devices``) the windows go round robin to
+    those devices' workers, two per device in flight.  Chunks come out in order; a chunk without
+    enough pieces raises the reference's ValueError when the stream reaches it, after every
+    earlier chunk."""
     by_chunk: dict[int, list[Piece]] = {}
     for p in pieces:
         by_chunk.setdefault(p.chunk_idx, []).append(p)
     wb = STREAM_WINDOW_BYTES if window_bytes is None else window_bytes
     wins = _windows(chunks, wb, lambda c: max(c.original_chunk_size, 1))
-    pool = _stream_pool()
-    nxt = next(wins, None)
-    fut = pool.submit(_decode_window, nxt, by_chunk) if nxt is not None else None
-    ahead = None
+    for outs, err in _pipeline(wins, _decode_window, (by_chunk,), _group(devices)):
+        yield from outs
+        if err is not None:
+            raise err
+
+
+def _pipeline(windows: Iterator[list], fn, args: tuple, grp) -> Iterator:
+    """fn(window, *args) of each window on the stream workers, results in window order.
+
+    One device (grp None): one _stream_pool worker, window w + 1 running while the caller
+    consumes window w.  EngineGroup: window i on worker i mod D, 2 D windows in flight.  Windows
+    are pulled from `windows` (on the caller's thread) only as slots free up; an error, or the
+    consumer closing the stream early, cancels the windows not yet started."""
+    if grp is None:
+        pool = _stream_pool()
+        depth, submit = 2, (lambda i, w: pool.submit(fn, w, *args))
+    else:
+        depth, submit = 2 * len(grp), (lambda i, w: grp.submit(i % len(grp), fn, w, *args))
+    q: deque = deque()
+    nxt = [0]
+
+    def fill():
+        while len(q) < depth:
+            w = next(windows, None)
+            if w is None:
+                return
+            q.append(submit(nxt[0], w))
+            nxt[0] += 1
+
     try:
-        while fut is not None:
-            nxt = next(wins, None)
-            ahead = pool.submit(_decode_window, nxt, by_chunk) if nxt is not None else None
-            outs, err = fut.result()
-            yield from outs
-            if err is not None:
-                raise err
-            fut, ahead = ahead, None
-    finally:  # an error, or the consumer closed the stream early: drop the look-ahead window
-        for f in (fut, ahead):
-            if f is not None:
-                f.cancel()
+        fill()
+        while q:
+            fut = q.popleft()
+            res = fut.result()
+            yield res
+            fill()
+    finally:
+        for f in q:
+            f.cancel()
 
 
 def _window_shapes(window: list):
@@ -731,43 +828,33 @@ def _encode_window(window: list, first_idx: int, piece_ids: bool):
 
 
 def encode_chunks_stream(chunks: Iterable[bytes], first_chunk_idx: int = 0, *, piece_ids: bool = False,
-                         window_bytes: int | None = None) -> Iterator:
+                         window_bytes: int | None = None, devices=None) -> Iterator:
     """``encode_chunk`` over a stream of chunks (the validator's upload loop: chunks read from
     the request, encoded, handed to the miners, validator.py:1338-1446), pipelined.
 
     Chunks are pulled from `chunks` on the caller's thread into windows of about
     `window_bytes` (default STREAM_WINDOW_BYTES); each window is one batched GPU encode on a
-    worker thread, running while the caller consumes the previous window's results.  Yields
-    ``EncodedChunk`` per chunk in order (chunk i gets index first_chunk_idx + i), or with
-    ``piece_ids=True`` ``(EncodedChunk, [piece_hash of each of its m pieces])``; those ids
+    worker thread, running while the caller consumes the previous window's results (with
+    `devices` / ``use_devices``: windows round robin over those devices, two per device in
+    flight).  Yields ``EncodedChunk`` per chunk in order (chunk i gets index first_chunk_idx + i),
+    or with ``piece_ids=True`` ``(EncodedChunk, [piece_hash of each of its m pieces])``; those ids
     come from the GPU (GPU_PIECE_IDS) for windows of large pieces, whose default window is then
     STREAM_WINDOW_IDS_BYTES."""
     wb = window_bytes
     if wb is None:
         wb = STREAM_WINDOW_IDS_BYTES if piece_ids and GPU_PIECE_IDS else STREAM_WINDOW_BYTES
-    pool = _stream_pool()
-    idx = first_chunk_idx
-    pending = fut = None
-    try:
+
+    def numbered():  # (window, index of its first chunk)
+        idx = first_chunk_idx
         for win in _windows(chunks, wb, lambda c: max(len(c), 1)):
-            fut = pool.submit(_encode_window, win, idx, piece_ids)
+            yield win, idx
             idx += len(win)
-            if pending is not None:
-                yield from _emit(pending, piece_ids)
-            pending, fut = fut, None
-        if pending is not None:
-            p, pending = pending, None
-            yield from _emit(p, piece_ids)
-    finally:  # an error, or the consumer closed the stream early: drop windows not yet started
-        for f in (pending, fut):
-            if f is not None:
-                f.cancel()
 
+    def run(wi, pid):
+        return _encode_window(wi[0], wi[1], pid)
 
-def _emit(fut: Future, piece_ids: bool):
-    """A window's results in order, then its error (raised after the chunks before it)."""
-    outs, err = fut.result()
-    for ec, ids in outs:
-        yield (ec, ids) if piece_ids else ec
-    if err is not None:
-        raise err
+    for outs, err in _pipeline(numbered(), run, (piece_ids,), _group(devices)):
+        for ec, ids in outs:
+            yield (ec, ids) if piece_ids else ec
+        if err is not None:
+            raise err

@@ -194,6 +194,60 @@ __global__ __launch_bounds__(1024) void k_c4dec(const u8 *__restrict__ in, const
     __builtin_nontemporal_store(e, (u32x4_u *)(o + 7 * BB_));
 }
 
+
+// C5-shaped (RS(8,3) = zfec(8,11), data blocks {1,3,5} erased): chunks of
+// 8 blocks of BB_ bytes back to back, 3 parity rows per chunk in their own buffer; slots = data
+// blocks {0,2,4,6,7} + the 3 parity rows; all 8 rows of the chunk written (5 copies + 3
+// "recovered", XOR only), 256-lane tiles of 4 KiB as the product's decode.  ENC: the encode's
+// traffic instead (8 blocks read, 3 rows written).
+template <u32 BB_, bool ENC>
+__global__ __launch_bounds__(256) void k_c5(const u8 *__restrict__ in, u8 *__restrict__ par, u8 *__restrict__ out)
+{
+    constexpr u32 per = BB_ / 4096;
+    const u32 chunk = blockIdx.x / per, t0 = (blockIdx.x % per) * 4096 + threadIdx.x * 16;
+    const u8 *s = in + (size_t)chunk * 8 * BB_ + t0;
+    u8 *p = par + (size_t)chunk * 3 * BB_ + t0;
+    if constexpr (ENC) {
+        u32x4 x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            x[j] = ld(s + j * BB_);
+        u32x4 a = x[0], b = x[0], c = x[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            a ^= x[j];
+            b ^= x[j] << 1;
+            c ^= x[j] << 2;
+        }
+        st(p, a);
+        st(p + BB_, b);
+        st(p + 2 * BB_, c);
+    } else {
+        constexpr int keep[5] = {0, 2, 4, 6, 7};
+        u8 *o = out + (size_t)chunk * 8 * BB_ + t0;
+        u32x4 x[8];
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+            x[j] = ld(s + keep[j] * BB_);
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            x[5 + r] = ld(p + r * BB_);
+        u32x4 a = x[5], b = x[6], c = x[7];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            a ^= x[j];
+            b ^= x[j] << 1;
+            c ^= x[j] << 2;
+        }
+        st(o + 1 * BB_, a);
+        st(o + 3 * BB_, b);
+        st(o + 5 * BB_, c);
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+            st(o + keep[j] * BB_, x[j]);
+    }
+}
+
 template <class F>
 double time_ms(F launch)
 {
@@ -268,6 +322,16 @@ int main()
         return rate((double)NC4 * (10.0 * 6554 + 65536),
                     time_ms([&] { hipLaunchKernelGGL(kern, dim3(NC4 * per), dim3(L), 0, 0, a, b, c, 65536u); }));
     };
+    // C5-shaped: algorithmic bytes per chunk: decode 8 B read + 8 B written, encode 8 B + 3 B
+    auto c5 = [&](auto kern, u32 BBv, double per_chunk) {
+        const u32 nch = (u32)(G / (8ull * BBv));
+        return rate((double)nch * per_chunk * BBv,
+                    time_ms([&] { hipLaunchKernelGGL(kern, dim3(nch * (BBv / 4096)), dim3(256), 0, 0, a, b, c); }));
+    };
+    printf("{\"c5_decode_B256K\": %.1f, \"c5_decode_B32K\": %.1f, \"c5_decode_B8K\": %.1f, \"c5_encode_B256K\": %.1f, "
+           "\"c5_encode_B32K\": %.1f}\n",
+           c5(k_c5<262144, false>, 262144, 16.0), c5(k_c5<32768, false>, 32768, 16.0), c5(k_c5<8192, false>, 8192, 16.0),
+           c5(k_c5<262144, true>, 262144, 11.0), c5(k_c5<32768, true>, 32768, 11.0));
     const double c4d_256 = c4d(k_c4dec<256>, 256);
     const double c4d_448 = c4d(k_c4dec<448>, 448);
     printf("{\"c4_decode_lanes256\": %.1f, \"c4_decode_lanes448\": %.1f}\n", c4d_256, c4d_448);

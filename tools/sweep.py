@@ -30,6 +30,10 @@ VARIANTS = {
     "dst2": {"SEC_DEC_ST": 2},
     "dst0": {"SEC_DEC_ST": 0},
     "est2": {"SEC_ENC_ST": 2},
+    "est3": {"SEC_ENC_ST": 3},
+    "est0": {"SEC_ENC_ST": 0},
+    "est2dst2": {"SEC_ENC_ST": 2, "SEC_DEC_ST": 2},
+    "dst3": {"SEC_DEC_ST": 3},
     "xcd": {"SEC_XCD_ORDER": 1},  # api.cpp: XCD order for every group (default: decode full tiles)
     "noxcd": {"SEC_XCD_ORDER": 0},
     "eb4": {"SEC_ENC_BATCH": 4},
