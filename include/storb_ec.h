@@ -139,6 +139,8 @@ int sec_timing_collect(sec_ctx *ctx, int kind, double *total_ms, int64_t *launch
  * with it.  Names (e.g. "SEC_SYN": -1 cost rule, 0 direct decode, 1 syndrome path;
  * "SEC_BS"; "SEC_REGISTER_MIN": bytes, 0 = never page-lock) are listed by
  * sec_option_name(0, 1, ...) up to NULL; their meaning is documented in api.cpp (enum Opt).
+ * Only options that force a shipped path or size the host pipeline exist (round 5 archived
+ * the A/B-only ones with their kernels).
  * No zfec counterpart: the reference has no tuning surface on this path.
  * SEC_EINVAL for an unknown name or a value out of the option's range. */
 int sec_ctx_set_option(sec_ctx *ctx, const char *name, int64_t value);
@@ -297,9 +299,10 @@ int sec_ctx_host_paths(sec_ctx *ctx, int64_t *zero_copy, int64_t *registered, in
  * choice (cost estimate; context option SEC_SYN = 0 / 1 turns the syndrome path off / forces
  * it where it applies); the bytes are the same. */
 int sec_ctx_decode_paths(sec_ctx *ctx, int64_t *syndrome, int64_t *direct);
-/* The same chunks by kernel: the one-wave fused syndrome kernel, the two-wave kernel (parity
- * rows of both groups of zfec(64,96)), the two syndrome kernels (syndromes through device
- * scratch), the direct decode (syndrome = fused + pair + two_kernel). */
+/* The same chunks by kernel: the one-wave fused syndrome kernel, `pair` (always 0 since round 5:
+ * the one-kernel wave pair for parity rows of both groups of zfec(64,96) lost its A/B and is no
+ * longer built; the slot stays for ABI stability), the two syndrome kernels (syndromes through
+ * device scratch), the direct decode (syndrome = fused + two_kernel). */
 int sec_ctx_decode_methods(sec_ctx *ctx, int64_t *fused, int64_t *pair, int64_t *two_kernel, int64_t *direct);
 /* kind: 0 host->device, 1 device->host, 2 device->device; synchronous on the ctx stream */
 int sec_memcpy(sec_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);

@@ -18,7 +18,9 @@ LIB = os.path.join(LIBDIR, "libstorbec.so")
 INCLUDE = os.path.join(ROOT, "include")
 SOURCES = ["kernels.hip", "kernels_bs.hip", "bignum.hip", "api.cpp"]
 HEADERS = ["kernels.hpp", "bignum.hpp", "gf_host.hpp", "gf_const.hpp", "copy_pool.hpp"]
-ARCH = os.environ.get("STORB_EC_ARCH", "gfx950")
+# gfx950 (MI355X) only: the kernels use gfx950 instructions (16-byte global_load_lds, v_bitop3)
+# and up to 160 KiB of LDS per workgroup; kernels_bs.hip stops any other target with #error
+ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 

@@ -122,33 +122,19 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // sec_ctx_set_option; the library reads no environment variable.  Setting an option drops the
 // context's cached plans, so the next call is planned with it.  Names keep the SEC_ prefix the
 // knobs had as environment variables in rounds 1-3 (tools/sweep.py variant strings use them).
+// Round 5 pruned the options whose only use was an A/B against a plan that won (their kernels
+// and results are in tools/archive/); what is left forces a SHIPPED path (tests) or sizes the
+// host pipeline.
 enum Opt {
     O_SYN,               // syndrome decodes: -1 cost rule, 0 off, 1 wherever they apply
     O_SYN_FUSED,         // 0: never the one-wave fused kernel
-    O_SYN_PAIR,          // 1: the two-wave kernel where it applies (default 0: ties the direct decode)
     O_SYN_RATIO,         // syndrome path taken under this many per mille of the direct estimate
-    O_SOLVE_LDS,         // 0: phase 2 of k >= 32 shapes in (span, row group) tiles, not LDS-staged spans
-    O_SYN_WG2,           // 0: phase 1 of parity rows in both groups as one workgroup per (span, group)
     O_BS,                // bit-sliced encode: -1 rule (bs_shape), 0 off, 1 every shape it has
     O_BS_LANES,          // lanes of a bit-sliced / syndrome tile (64, 128, 256)
-    O_BS_SPLIT,          // 1: one launch per 16-row group (64,96)
-    O_BS_R8,             // 1: (32,48) as two interleaved groups of 8 rows
-    O_BS_LDS,            // 1: small bit-sliced chunks LDS-staged whole (default 0: measured slower)
-    O_BS_PAIR,           // 1: (64,96) encode in shared-transpose wave pairs (default 0: measured slower)
-    O_DEC_LDS,           // 1: small chunks' reassembly through an LDS image (default 0: measured slower)
-    O_TILE_U,            // 0 rule (1), or 1 / 2 / 4 u-steps per lane
-    O_ENC_LANES,         // 0 rule, or lanes of U = 1 encode tiles
-    O_FULL_LANES,        // 0 rule, or lanes of U = 1 tiles (both kernels)
-    O_WIDE_K8,           // 8-row groups go to the W kernels from k > this
-    O_DEC_REC_KB,        // -1 rule, 0 off, 8: the 8-slot small-batch decode for 4 < k <= 8 too
-    O_DEC_COPY_KB,       // 0, 4 or 8: reassembling decodes of k <= that through the small-batch variant
-    O_RAGGED_KERNEL,     // 1: ragged ends in a separate tail launch (round-1 form)
-    O_EXACT_LANES,       // 1: chunk-sized tiles, one launch per width (round-1 form)
     O_SHA1_SPLIT,        // -1 rule, 0 one-lane kernel, 1 two-wave kernel
     O_SLAB_BYTES,        // host staging slab
     O_SLAB_BYTES_DIGEST, // host staging slab of SHA-1 / bignum calls
     O_COPY_THREADS,      // 0 rule, or host copy-pool threads
-    O_STAGE_DMA,         // 1: staged EC calls DMA into device memory instead of running on the slabs
     O_REGISTER_MIN,      // page-lock pageable host buffers for calls moving >= this many bytes (0: never)
     O_HOST_JOIN,         // 0: the GPU writes every byte of a host reassembly
     O_COUNT
@@ -162,30 +148,13 @@ struct OptSpec {
 constexpr OptSpec kOpts[O_COUNT] = {
     {"SEC_SYN", -1, -1, 1},
     {"SEC_SYN_FUSED", 1, 0, 1},
-    {"SEC_SYN_PAIR", 0, 0, 1},
     {"SEC_SYN_RATIO", 900, 1, 1000000},
-    {"SEC_SOLVE_LDS", 1, 0, 1},
-    {"SEC_SYN_WG2", 1, 0, 1},
     {"SEC_BS", -1, -1, 1},
     {"SEC_BS_LANES", 256, 64, 256},
-    {"SEC_BS_SPLIT", 0, 0, 1},
-    {"SEC_BS_R8", 0, 0, 1},
-    {"SEC_BS_LDS", 0, 0, 1},
-    {"SEC_BS_PAIR", 0, 0, 1},
-    {"SEC_DEC_LDS", 0, 0, 1},
-    {"SEC_TILE_U", 0, 0, 4},
-    {"SEC_ENC_LANES", 0, 0, 1024},
-    {"SEC_FULL_LANES", 0, 0, 1024},
-    {"SEC_WIDE_K8", 16, 0, 256},
-    {"SEC_DEC_REC_KB", -1, -1, 8},
-    {"SEC_DEC_COPY_KB", 0, 0, 8},
-    {"SEC_RAGGED_KERNEL", 0, 0, 1},
-    {"SEC_EXACT_LANES", 0, 0, 1},
     {"SEC_SHA1_SPLIT", -1, -1, 1},
     {"SEC_SLAB_BYTES", (int64_t)64 << 20, (int64_t)1 << 16, (int64_t)1 << 40},
     {"SEC_SLAB_BYTES_DIGEST", (int64_t)512 << 20, (int64_t)1 << 16, (int64_t)1 << 40},
     {"SEC_COPY_THREADS", 0, 0, 256},
-    {"SEC_STAGE_DMA", 0, 0, 1},
     {"SEC_REGISTER_MIN", (int64_t)4 << 20, 0, (int64_t)1 << 62},
     {"SEC_HOST_JOIN", 1, 0, 1},
 };
@@ -216,7 +185,6 @@ struct Group {
     int rows, U, lanes, wide;  // wide: k > kBatchVecs / U, blocks loaded in several batches
     uint32_t first, count;
     int mfma = 0;              // bin kind.  Encode: 3 = sec_encode_bs_kernel of shape `rows`, row group U;
-                               // 4 = sec_encode_bs_lds_kernel of shape `rows` (one tile per chunk);
                                // decode: the small-batch variant's batch (dec_small_kb), or 0
 };
 
@@ -237,9 +205,9 @@ struct SubPlan {
     // syndrome decodes (decode): phase 1 launches (bit-sliced syndromes) and phase 2 launches
     // (the Cauchy solve), one each per shape
     // (shape, (first, count)) in tiles; synf: the fused kernel (both phases in one wave)
-    std::vector<std::pair<int, std::pair<uint32_t, uint32_t>>> syn1, syn2, synf, synp;  // synp: the wave pairs
+    std::vector<std::pair<int, std::pair<uint32_t, uint32_t>>> syn1, syn2, synf;
     size_t off_sdesc = 0, off_stiles = 0, off_ssoff = 0, off_ssavail = 0, off_vdesc = 0, off_vtiles = 0,
-           off_masks = 0, off_ftiles = 0, off_ptiles = 0;
+           off_masks = 0, off_ftiles = 0;
     uint64_t syn_bytes = 0;  // syndrome scratch of this unit
     int syn_lanes = 256;     // lanes of the syndrome kernels' tiles (their span per tile)
 };
@@ -250,7 +218,7 @@ struct Plan {
     std::vector<SubPlan> subs;
     DevBuf meta;  // device copy of the metadata image of every sub-plan
     bool valid = false;
-    int64_t nsyn = 0, ndirect = 0, nfused = 0, npair = 0;  // decode: chunks with a lost primary, by method
+    int64_t nsyn = 0, ndirect = 0, nfused = 0;  // decode: chunks with a lost primary, by method
 };
 
 // Device-resident GF coefficient tables (5 dwords per coefficient), keyed by
@@ -286,46 +254,17 @@ struct Image {
 // zfec(16,24) even, while C4's 6554 B blocks lose 4.7 %; a mixed batch (C5) keeps one tile
 // width, since its large chunks alone at 64 lanes (a second launch) cost it 9 %.  The 1:1
 // copy behind a decode measured no gain from narrower tiles (-1 %).
-// Options SEC_ENC_LANES / SEC_FULL_LANES override, for A/B.
-int full_lanes(const Options &o, bool decode, bool narrow = false)
-{
-    int64_t l = !decode && narrow ? 64 : sec::kLanes;
-    if (o[O_FULL_LANES])
-        l = o[O_FULL_LANES];
-    if (!decode && o[O_ENC_LANES])
-        l = o[O_ENC_LANES];
-    return (int)std::max<int64_t>(64, std::min<int64_t>(1024, l)) / 64 * 64;
-}
+int full_lanes(bool decode, bool narrow = false) { return !decode && narrow ? 64 : sec::kLanes; }
 
-// u-steps (4 KiB each) a lane covers per tile.  Larger U = more bytes in flight
-// per lane but more registers; option SEC_TILE_U overrides.
-// The kernels keep all k * U loads of a lane in one batch, so U > 1 only when
-// k * U <= kBatchVecs (wider k goes in U = 1 tiles, batched kBatchVecs blocks at a time).
-// (Full tiles are 256 lanes x 4 KiB x U; see add_work.)
-int pick_u(const Options &o, int k)
-{
-    const int forced = (int)o[O_TILE_U];
-    // U = 1 by default: one 16 B vector per block per lane, 4 KiB per workgroup and block.
-    // Measured on C2 against U = 2 / 4: encode 6.48 vs 6.09 / 5.95 TB/s, decode 6.31 vs
-    // 5.79 / 5.62 (profiles/r01_sweep_u.jsonl); U > 1 only on request (SEC_TILE_U).
-    int u = 1;
-    if (forced == 1 || forced == 2 || forced == 4)
-        u = forced;
-    while (u > 1 && k * u > sec::kBatchVecs)
-        u /= 2;
-    return u;
-}
+// One u-step (4 KiB of each block) per 256-lane tile: one 16 B vector per block and lane.
+// Measured on C2 against U = 2 / 4: encode 6.48 vs 6.09 / 5.95 TB/s, decode 6.31 vs 5.79 / 5.62
+// (profiles/r01_sweep_u.jsonl); round 5 stopped building the U > 1 kernels.
+constexpr int kU = 1;
 
-// Whether a group of `rows` output rows over k blocks runs in the wide (W) kernels, which
-// load the blocks in several batches.  Needed when k * U > kBatchVecs; groups of more than 4
-// rows also go there from k > SEC_WIDE_K8 on (A/B option), since the W kernels pair blocks for
-// 8-row groups with smaller batches (kernels.hip SEC_WIDE_BATCH).
-bool is_wide(const Options &o, int k, int U, int rows)
-{
-    if (k * U > sec::kBatchVecs)
-        return true;
-    return U == 1 && rows > 4 && k > o[O_WIDE_K8];
-}
+// Whether a group over k blocks runs in the wide (W) kernels, which load the blocks in several
+// batches (kernels.hip SEC_WIDE_BATCH): k > kBatchVecs.  (Round 4's SEC_WIDE_K8 moved 8-row groups
+// there from a lower k for A/B; its default, 16, is this same rule.)
+bool is_wide(int k) { return k > sec::kBatchVecs; }
 
 using Bins = std::map<std::tuple<int, int, int, int, int>, std::vector<sec::Tile>>;  // (kind, rows, U, lanes, wide)
 
@@ -336,24 +275,8 @@ uint64_t round64(uint64_t v) { return (v + 63) / 64 * 64; }
 // VGPRs, 8 waves per SIMD instead of 4.  Measured on C3 recover-only (tools/sweep.py
 // --recover, env held during the timed calls): 6.42 against 5.91 TB/s; the same batches cost
 // the reassembling decode 4 %, and 8-slot batches for k <= 8 measured 1.4 % slower on RS(8,3)
-// recover-only (profiles/r02_dec_small_kb_ab.jsonl).  Option SEC_DEC_REC_KB = 0 turns it off,
-// = 8 adds the 8-slot variant for 4 < k <= 8 (A/B).
-int dec_small_kb(const Options &o, int k)
-{
-    if (o[O_DEC_REC_KB] == 0)
-        return 0;
-    if (k <= 4)
-        return 4;
-    return o[O_DEC_REC_KB] == 8 && k <= 8 ? 8 : 0;
-}
-
-// A/B only: option SEC_DEC_COPY_KB = 4 or 8 runs the reassembling (copying) decodes of chunks
-// with k <= that through the small-batch variant too (default off: 4-slot batches measured -4 %)
-int dec_copy_kb(const Options &o, int k)
-{
-    const int64_t v = o[O_DEC_COPY_KB];
-    return (v == 4 || v == 8) && k <= v ? (int)v : 0;
-}
+// recover-only (profiles/r02_dec_small_kb_ab.jsonl).
+int dec_small_kb(int k) { return k <= 4 ? 4 : 0; }
 
 // Syndrome decode (kernels_bs.hip) for a chunk that lost e data blocks, when its shape has the
 // bit-sliced kernels: the one-wave kernel sec_decode_bs_kernel ("fused": e <= 16 and every
@@ -370,7 +293,7 @@ int dec_copy_kb(const Options &o, int k)
 //           R 17, BW 5.0; the direct decode's bytes;
 //   two:    phase 1 P (k - e) 8.75 + (k - e) e + 15 e over P touched parity groups, the data
 //           read once per group (BW 5.0, or 4.0 when P = 2), or once when both groups share a
-//           workgroup (SEC_SYN_WG2: BW 5.0); phase 2 2.75 e per touched 16-row group + e^2 + 14 e,
+//           workgroup (sec_syndrome_bs_pair_kernel: BW 5.0); phase 2 2.75 e per touched 16-row group + e^2 + 14 e,
 //           2 e rows of syndrome traffic; R 14.5.
 // A syndrome path is taken when its estimate is under SEC_SYN_RATIO (default 900 per mille) of
 // the direct one (970 for both-group chunks of one workgroup, below).  Options SEC_SYN = 0 / 1 turn the syndrome paths off / force them wherever they
@@ -383,13 +306,12 @@ double vperm_ops(int rows, int slots)
     return v * slots;
 }
 
-// Syndrome methods of a chunk (syn_choice)
-enum SynMethod { kSynTwo = 0, kSynFused = 1, kSynPair = 2 };
+// Syndrome methods of a chunk (syn_choice).  (Round 4's one-kernel wave pair for both-group
+// chunks, SEC_SYN_PAIR, tied the direct decode and is archived: tools/archive/.)
+enum SynMethod { kSynTwo = 0, kSynFused = 1 };
 
-// shape of the syndrome kernels for this chunk, or -1 (direct); `method`: two kernels, the one-wave
-// fused kernel, or (option SEC_SYN_PAIR = 1) the two-wave kernel (sec_decode_bs_pair_kernel: e <= 16
-// present parity rows in both groups of zfec(64,96); its estimate is the fused kernel's with the
-// transposes halved)
+// shape of the syndrome kernels for this chunk, or -1 (direct); `method`: two kernels or the
+// one-wave fused kernel
 int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, bool copies, int &method)
 {
     method = kSynTwo;
@@ -413,36 +335,35 @@ int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, 
         }
     const int P = __builtin_popcountll(touched);
     const bool can_fuse = P == 1 && e <= 16 && o[O_SYN_FUSED] != 0;
-    const bool can_pair = P == 2 && e <= 16 && sec_syn_pair(sh) && o[O_SYN_PAIR] != 0;
     if (o[O_SYN] == 1) {
-        method = can_fuse ? kSynFused : can_pair ? kSynPair : kSynTwo;
+        method = can_fuse ? kSynFused : kSynTwo;
         return sh;
     }
     auto t = [](double ops, double R, double bytes, double bw) { return std::max(ops / R, bytes / bw); };
     const double E = e, KE = k - e, out = copies ? k : e;
     const double direct = t(vperm_ops(e, k), 28, 4.0 * (k + out), 5.6);
     const double p2 = 2.75 * E * __builtin_popcountll(g16) + E * E + 14 * E;
-    // both groups in one two-wave workgroup (SEC_SYN_WG2): the data read once (1.07x at P = 2
-    // instead of 1.45x), which fits the r04 A/B as P = 1's bytes and rate (r04_syn_ab_final.jsonl)
-    const bool wg2 = P == 2 && sec_syn_pair(sh) && o[O_SYN_WG2] != 0;
+    // both groups in one two-wave workgroup (sec_syndrome_bs_pair_kernel): the data read once
+    // (1.07x at P = 2 instead of 1.45x), which fits the r04 A/B as P = 1's bytes and rate
+    // (r04_syn_ab_final.jsonl)
+    const bool wg2 = P == 2 && sec_syn_pair(sh);
     const double two = t(P * KE * 8.75 + KE * E + 15 * E, 14.5,
                          4.0 * (k + (wg2 ? 0 : (P - 1) * KE) + (copies ? KE : 0) + E), P > 1 && !wg2 ? 4.0 : 5.0) +
                        t(p2, 14.5, 4.0 * 2 * E, 5.0);
     const double fuse = can_fuse ? t(KE * (8.75 + E) + 15 * E + 2.75 * E * __builtin_popcountll(g8) + E * E + 14 * E,
                                      17, 4.0 * (k + out), 5.0)
                                  : 1e30;
-    const double pair = can_pair ? t(KE * (6.25 + E) + 15 * E + 2.75 * E * __builtin_popcountll(g8) + E * E + 14 * E,
-                                     17, 4.0 * (k + out), 5.0)
-                                 : 1e30;
-    // margin: SEC_SYN_RATIO, except 3 % for both-group chunks in one workgroup, whose two and
-    // direct estimates fit the r04 A/B within 4 % (r04_syn_ab_final.jsonl: at e = 14 / 16 the two
-    // kernels beat the direct decode by 6-7 % at estimate ratios 0.96 / 0.92)
-    const int64_t ratio = wg2 ? std::max<int64_t>(o[O_SYN_RATIO], 970) : o[O_SYN_RATIO];
+    // margin: SEC_SYN_RATIO; at its default, 3 % for both-group chunks in one workgroup, whose
+    // two and direct estimates fit the r04 A/B within 4 % (r04_syn_ab_final.jsonl: at e = 14 / 16
+    // the two kernels beat the direct decode by 6-7 % at estimate ratios 0.96 / 0.92).  A caller
+    // that sets SEC_SYN_RATIO gets exactly that margin for every chunk.
+    const bool dflt_ratio = o[O_SYN_RATIO] == kOpts[O_SYN_RATIO].dflt;
+    const int64_t ratio = wg2 && dflt_ratio ? 970 : o[O_SYN_RATIO];
     const double lim = (double)ratio / 1000.0 * direct;
-    const double best = std::min(two, std::min(fuse, pair));
+    const double best = std::min(two, fuse);
     if (best >= lim)
         return -1;
-    method = best == fuse ? kSynFused : best == pair ? kSynPair : kSynTwo;
+    method = best == fuse ? kSynFused : kSynTwo;
     return sh;
 }
 
@@ -455,9 +376,8 @@ int syn_choice(const Options &o, const sec_dec_chunk &c, const int *idx, int e, 
 // by byte by the last tile of each row group (Tile::ntail): a separate one-thread-per-
 // byte launch cost C4 13-17 % on top of its main kernels (profiles/r01_c4_kernel_stats).
 // Chunks with valid < 16 get no tile: all of [0, B) becomes one-thread tail items.
-void add_work(const Options &o, Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B,
-              int64_t valid, int rows_total, int k, bool decode, uint64_t start = 0, bool narrow = false,
-              int small_kb = 0)
+void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint64_t B, int64_t valid, int rows_total,
+              int k, bool decode, bool narrow = false, int small_kb = 0)
 {
     if (B == 0)
         return;
@@ -469,62 +389,21 @@ void add_work(const Options &o, Bins &bins, std::vector<sec::TailItem> &tail, ui
             tail.push_back(sec::TailItem{chunk, (uint32_t)t});
         return;
     }
-    const bool ragged_kernel = o[O_RAGGED_KERNEL] != 0;  // A/B: the old tail launch
-    const bool exact = o[O_EXACT_LANES] != 0;            // A/B: chunk-sized tiles
-    if (ragged_kernel)
-        for (uint64_t t = v; t < B; ++t)
-            tail.push_back(sec::TailItem{chunk, (uint32_t)t});
+    const int wide = is_wide(k);
     for (int g = 0; g < ngroups; ++g) {
         const int r0 = g * sec::kMaxRows;
         const int rows = std::min(sec::kMaxRows, rows_total - r0);
-        const int U = pick_u(o, k);
-        const int wide = is_wide(o, k, U, rows);  // U == 1 then (pick_u)
-        const int flanes = U == 1 ? std::min(full_lanes(o, decode, narrow), sec::max_lanes(rows, 1)) : sec::kLanes;
-        const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * U;
+        const int flanes = std::min(full_lanes(decode, narrow), sec::max_lanes(rows, kU));
+        const uint64_t step = (uint64_t)sec::kLaneBytes * flanes * kU;
         // kind: 0, or the small-batch decode variant's batch (the group's kernel, see dec_small_kb)
-        const int kind = small_kb && U == 1 && !wide && k <= small_kb ? small_kb : 0;
-        auto &full = bins[{kind, rows, U, flanes, wide}];
-        sec::Tile *last = nullptr;
-        if (!exact) {
-            // every U = 1 tile is flanes wide, the chunk's last one with idle lanes past
-            // `valid`: one launch per (rows, wide) class however mixed the chunk sizes are
-            // tiles from `start` (the end of a chunk's MFMA range, a multiple of 16), or one
-            // tile at `valid` that only carries the ragged end when that range reaches it
-            const uint64_t from = std::min<uint64_t>(start, v);
-            const uint64_t nfull = U == 1 ? (v - from + step - 1) / step : (v - from) / step;
-            for (uint64_t i = 0; i < nfull; ++i) {
-                full.push_back(sec::Tile{chunk, (uint32_t)(from + i * step), (uint32_t)r0, 0});
-                last = &full.back();
-            }
-            const int ul = std::min(full_lanes(o, decode, narrow), sec::max_lanes(rows, 1));
-            auto &ones = bins[{kind, rows, 1, ul, is_wide(o, k, 1, rows)}];
-            for (uint64_t t0 = from + nfull * step; t0 < v; t0 += (uint64_t)sec::kLaneBytes * ul) {  // U > 1 remainder
-                ones.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
-                last = &ones.back();
-            }
-            if (!last && B > v) {
-                full.push_back(sec::Tile{chunk, (uint32_t)v, (uint32_t)r0, 0});
-                last = &full.back();
-            }
-        } else {
-            // A/B (SEC_EXACT_LANES): partial tiles sized to what is left of the chunk, up to
-            // 1024 lanes — a separate launch per distinct width
-            const uint64_t nfull = v > (uint64_t)sec::kLaneBytes * 1024 ? v / step : 0;
-            for (uint64_t i = 0; i < nfull; ++i) {
-                full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
-                last = &full.back();
-            }
-            for (uint64_t t0 = nfull * step; t0 < v;) {
-                const uint64_t lanes =
-                    std::min<uint64_t>(sec::max_lanes(rows, 1), round64((v - t0 + sec::kLaneBytes - 1) / sec::kLaneBytes));
-                auto &bin = bins[{0, rows, 1, (int)lanes, is_wide(o, k, 1, rows)}];
-                bin.push_back(sec::Tile{chunk, (uint32_t)t0, (uint32_t)r0, 0});
-                last = &bin.back();
-                t0 += lanes * sec::kLaneBytes;
-            }
-        }
-        if (last)  // the ragged end [v, B) rides on the last tile
-            last->ntail = ragged_kernel ? 0 : (uint32_t)(B - v);
+        const int kind = small_kb && !wide && k <= small_kb ? small_kb : 0;
+        auto &full = bins[{kind, rows, kU, flanes, wide}];
+        // every tile is flanes wide, the chunk's last one with idle lanes past `valid`: one
+        // launch per (rows, wide) class however mixed the chunk sizes are
+        const uint64_t nfull = (v + step - 1) / step;
+        for (uint64_t i = 0; i < nfull; ++i)
+            full.push_back(sec::Tile{chunk, (uint32_t)(i * step), (uint32_t)r0, 0});
+        full.back().ntail = (uint32_t)(B - v);  // the ragged end [v, B) rides on the last tile
     }
 }
 
@@ -533,15 +412,13 @@ void add_work(const Options &o, Bins &bins, std::vector<sec::TailItem> &tail, ui
 // position [0, B) of a chunk with B >= 16, ragged end included, so such a chunk gets no
 // sec_encode_kernel tile.  Tiles of SEC_BS_LANES lanes (default 256 = 8 KiB of each block).
 // A shape of several row groups ((64,96): 2 x 16 rows) runs them in one launch, a run of 8
-// tiles of each group in turn, so the tiles that read the same blocks share an XCD's L2
-// (option SEC_BS_SPLIT = 1: one launch per group instead).  SEC_BS = 0 turns the kernel off
-// (then the v_perm rows), SEC_BS = 1 uses it for every shape it has; SEC_BS_R8 = 1 takes
-// (32,48) in two groups of 8 rows.
+// tiles of each group in turn, so the tiles that read the same blocks share an XCD's L2.
+// SEC_BS = 0 turns the kernel off (then the v_perm rows), SEC_BS = 1 uses it for every shape it
+// has.  (Round 4's A/B forms -- one launch per group, (32,48) in 8-row groups, shared-transpose
+// wave pairs, LDS-staged small chunks -- are archived: tools/archive/.)
 constexpr int kBsAllGroups = 99;  // Group::U of an interleaved launch of every row group
-constexpr int kBsPair = 98;       // Group::U of a launch of two-wave workgroups (one per span, both groups)
 constexpr int kSolveLds = 1 << 16;  // phase-2 tile map keys of sec_solve_bs_lds_kernel launches
 constexpr int kSynWg2 = 1 << 16;    // phase-1 tile map keys of sec_syndrome_bs_pair_kernel launches
-constexpr int kDecLds = 16;       // decode bin kind of sec_decode_lds_kernel (one tile per chunk)
 
 int bs_shape(const Options &o, int k, int m, uint64_t B)
 {
@@ -555,42 +432,17 @@ int bs_shape(const Options &o, int k, int m, uint64_t B)
     const int p = m - k;
     if (o[O_BS] != 1 && p < 8 && !(k == 10 && m == 14))
         return -1;
-    if (k == 32 && m == 48 && o[O_BS_R8])
-        return sec_bs_shape(k, m, 8);
     return sec_bs_shape(k, m);
-}
-
-// Chunks of at most sec_bs_lds_max() (64 KiB) bytes with 16 <= B <= 8192 and at most 8 parity rows
-// (C4's 64 KiB zfec(10,14) chunks) take sec_encode_bs_lds_kernel: one workgroup per chunk that
-// reads the chunk as one contiguous run into LDS instead of k unaligned block streams.  Opt-in
-// (SEC_BS_LDS = 1): on C4 it measured 5193 GB/s against the tiles' 5680 (profiles/r04_c4_lds_ab.jsonl).
-bool bs_lds(const Options &o, const sec_enc_chunk &c, uint64_t B)
-{
-    return o[O_BS_LDS] && c.n <= sec_bs_lds_max() && B >= 16 && B <= 8192 && c.m - c.k <= 8;
 }
 
 void add_bs_work(const Options &o, Bins &bins, uint32_t chunk, uint64_t B, int shape)
 {
     const int lanes = o.lanes(O_BS_LANES);
     const uint64_t step = (uint64_t)sec_bs_span() * (lanes / 64);
-    const int ng = sec_bs_groups(shape);
-    if (ng == 2 && o[O_BS_PAIR] && !o[O_BS_SPLIT]) {  // one two-wave workgroup per span
-        auto &bin = bins[{3, shape, kBsPair, 128, 0}];
-        for (uint64_t t0 = 0; t0 < B; t0 += sec_bs_span())
-            bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
-        return;
-    }
-    if (ng > 1 && !o[O_BS_SPLIT]) {  // flatten() interleaves the groups
-        auto &bin = bins[{3, shape, kBsAllGroups, lanes, 0}];
-        for (uint64_t t0 = 0; t0 < B; t0 += step)
-            bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
-        return;
-    }
-    for (int g = 0; g < ng; ++g) {
-        auto &bin = bins[{3, shape, g, lanes, 0}];
-        for (uint64_t t0 = 0; t0 < B; t0 += step)
-            bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
-    }
+    // two row groups ((64,96)): one launch, flatten() interleaves the groups; else group 0
+    auto &bin = bins[{3, shape, sec_bs_groups(shape) > 1 ? kBsAllGroups : 0, lanes, 0}];
+    for (uint64_t t0 = 0; t0 < B; t0 += step)
+        bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
 }
 
 // Tiles of an interleaved bit-sliced launch: runs of 8 positions, each run once per row group
@@ -612,20 +464,13 @@ void bs_interleave(int shape, const std::vector<sec::Tile> &pos, std::vector<sec
 // any count).  Measured (profiles/r01_sweep2_*.jsonl): decode with full 256-lane multi-step
 // tiles (C2/C3, U = 4) +2.6 %; encode within noise; one-tile-per-chunk groups (C4) -4 to
 // -6 %; decode with the default U = 1 full tiles -3 % (profiles/r01_sweep_u1_knobs.jsonl).
-// So it applies to decode groups of full U > 1 tiles only (off by default).  SEC_XCD_ORDER (build knob, for A/B):
-// -1 = that rule, 0 = never, 1 = every group of both kernels.
+// It paid only for decode groups of U > 1 tiles, which are no longer built, so it is off;
+// SEC_XCD_ORDER = 1 (build knob, for A/B) applies it to every tile group of both kernels.
 #ifndef SEC_XCD_ORDER
-#define SEC_XCD_ORDER -1
+#define SEC_XCD_ORDER 0
 #endif
 
-bool use_xcd_order(bool decode, const Group &g)
-{
-    if (g.mfma >= 3)
-        return false;
-    if (SEC_XCD_ORDER >= 0)
-        return SEC_XCD_ORDER == 1;
-    return decode && g.U > 1 && g.lanes == sec::kLanes;
-}
+bool use_xcd_order(bool, const Group &g) { return g.mfma < 3 && SEC_XCD_ORDER == 1; }
 
 void xcd_order(std::vector<sec::Tile> &t)
 {
@@ -716,7 +561,7 @@ struct sec_ctx {
     std::unique_ptr<sec::CopyPool> pool;
     // SEC_F_HOST encode / decode calls by path (sec_ctx_host_paths)
     int64_t zero_copy_calls = 0, registered_calls = 0, staged_calls = 0;
-    int64_t syn_chunks = 0, direct_chunks = 0, fused_chunks = 0, pair_chunks = 0;  // decodes by method (sec_ctx_decode_paths)
+    int64_t syn_chunks = 0, direct_chunks = 0, fused_chunks = 0;  // decodes by method (sec_ctx_decode_paths)
 
     hipStream_t stream() const { return ext ? ext : own; }
     hipEvent_t ev()
@@ -1015,12 +860,10 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
             const int bs = p > 0 ? bs_shape(ctx->opt, c.k, c.m, B) : -1;
-            if (bs >= 0 && bs_lds(ctx->opt, c, B))
-                bins[{4, bs, 0, 256, 0}].push_back(sec::Tile{(uint32_t)(i - c0), 0, 0, 0});
-            else if (bs >= 0)
+            if (bs >= 0)
                 add_bs_work(ctx->opt, bins, (uint32_t)(i - c0), B, bs);
             else if (p > 0)
-                add_work(ctx->opt, bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, 0, narrow);
+                add_work(bins, tail, (uint32_t)(i - c0), B, valid, p, c.k, false, narrow);
         }
         std::vector<sec::Tile> tiles;
         flatten(bins, sp.groups, tiles, false);
@@ -1048,14 +891,11 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
     for (const Group &g : sp.groups) {
-        int e = g.mfma == 4   ? sec_launch_encode_bs_lds(g.rows, in, par, dd, dt + g.first, g.count, s)
-                : g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsAllGroups ? -1 : g.U == kBsPair ? -2 : g.U,
-                                                     g.lanes, in, par, dd, dt + g.first, g.count, s)
-                              : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
+        int e = g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsAllGroups ? -1 : g.U, g.lanes, in, par, dd,
+                                                   dt + g.first, g.count, s)
+                            : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
         if (e)
-            return hip_fail((hipError_t)e, g.mfma == 4   ? "sec_encode_bs_lds_kernel"
-                                           : g.mfma == 3 ? "sec_encode_bs_kernel"
-                                                         : "sec_encode_kernel");
+            return hip_fail((hipError_t)e, g.mfma == 3 ? "sec_encode_bs_kernel" : "sec_encode_kernel");
     }
     if (sp.ntail) {
         int e = sec_launch_encode_tail(in, par, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs, s);
@@ -1185,13 +1025,11 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         RC(table_reset(ctx, tc, need * 2 + ((size_t)1 << 18)));
     }
 
-    plan.nsyn = plan.ndirect = plan.nfused = plan.npair = 0;
+    plan.nsyn = plan.ndirect = plan.nfused = 0;
     for (int64_t i = 0; i < nchunks; ++i)
-        if (e_of[i])
-        {
+        if (e_of[i]) {
             ++(syn_of[i] >= 0 ? plan.nsyn : plan.ndirect);
             plan.nfused += syn_of[i] >= 0 && fuse_of[i] == kSynFused;
-            plan.npair += syn_of[i] >= 0 && fuse_of[i] == kSynPair;
         }
     std::vector<std::pair<int64_t, int64_t>> ranges;
     if (host) {
@@ -1220,7 +1058,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
         std::vector<sec::SynDesc> sdescs;
         std::vector<uint64_t> ssoff;
         std::vector<uint32_t> ssavail;
-        std::map<int, std::vector<sec::Tile>> stiles, vtiles, ftiles, ptiles;
+        std::map<int, std::vector<sec::Tile>> stiles, vtiles, ftiles;
         std::vector<sec::SolveDesc> vdescs;
         std::vector<uint64_t> masks;                                    // w / z scalings (scale_mask)
         std::map<std::string, std::pair<uint32_t, uint32_t>> mask_of;  // pattern -> (wq0, zq0)
@@ -1324,22 +1162,17 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                         ft.push_back(sec::Tile{si, (uint32_t)t, (uint32_t)(gs[0] * NR), copies ? 1u : 0u});
                     continue;
                 }
-                if (method == kSynPair) {  // one two-wave workgroup per span; launches by LDS size
-                    auto &pt = ptiles[sh * 64 + 16];
-                    for (uint64_t t = 0; t < c.B; t += sec_bs_span())
-                        pt.push_back(sec::Tile{si, (uint32_t)t, 0u, copies ? 1u : 0u});
-                    continue;
-                }
-                if (gs.size() == 2 && sec_syn_pair(sh) && ctx->opt[O_SYN_WG2]) {  // both groups, one workgroup
+                if (gs.size() == 2 && sec_syn_pair(sh)) {  // both groups, one two-wave workgroup per span
                     auto &st2 = stiles[kSynWg2 + sh];
                     for (uint64_t t = 0; t < c.B; t += sec_bs_span())
                         st2.push_back(sec::Tile{si, (uint32_t)t, 0u, copies ? 1u : 0u});
                 } else {
-                auto &st = stiles[sh];
-                for (uint64_t t0 = 0; t0 < c.B; t0 += 8 * step)  // runs of 8 positions per group: one XCD
-                    for (int g : gs)
-                        for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
-                            st.push_back(sec::Tile{si, (uint32_t)t, (uint32_t)(g * NR), copies && g == gs[0] ? 1u : 0u});
+                    auto &st = stiles[sh];
+                    for (uint64_t t0 = 0; t0 < c.B; t0 += 8 * step)  // runs of 8 positions per group: one XCD
+                        for (int g : gs)
+                            for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
+                                st.push_back(
+                                    sec::Tile{si, (uint32_t)t, (uint32_t)(g * NR), copies && g == gs[0] ? 1u : 0u});
                 }
                 // phase 2: the groups of lost rows, their tiles interleaved as phase 1's
                 sec::SolveDesc vd{};
@@ -1353,7 +1186,7 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 vd.recover = recover ? 1u : 0u;
                 const uint32_t vi = (uint32_t)vdescs.size();
                 vdescs.push_back(vd);
-                if (ctx->opt[O_SOLVE_LDS] && sec_solve_lds(sh)) {  // one workgroup per span, syndromes in LDS
+                if (sec_solve_lds(sh)) {  // one workgroup per span, syndromes in LDS
                     auto &vt = vtiles[kSolveLds + sh * 64 + ((e + 7) / 8) * 8];
                     for (uint64_t t = 0; t < c.B; t += sec_bs_span())
                         vt.push_back(sec::Tile{vi, (uint32_t)t, 0u, 0u});
@@ -1369,13 +1202,9 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                     for (int g : gl)
                         for (uint64_t t = t0; t < std::min<uint64_t>(c.B, t0 + 8 * step); t += step)
                             vt.push_back(sec::Tile{vi, (uint32_t)t, (uint32_t)(g * NR2), 0u});
-            } else if (nout > 0 && !recover && !nocopy && ctx->opt[O_DEC_LDS] && c.B >= 16 && c.B <= 8192 &&
-                       nout <= sec_dec_lds_max() && e_of[i] <= (uint32_t)sec::kMaxRows) {
-                // small chunk: reassembled in LDS, written out as one run (sec_decode_lds_kernel)
-                bins[{kDecLds, (int)e_of[i], 0, 256, 0}].push_back(sec::Tile{(uint32_t)(i - c0), 0, 0, 0});
             } else if (nout > 0 && !(nocopy && e_of[i] == 0)) {
-                add_work(ctx->opt, bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true, 0, false,
-                         recover || nocopy ? dec_small_kb(ctx->opt, c.k) : dec_copy_kb(ctx->opt, c.k));
+                add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true, false,
+                         recover || nocopy ? dec_small_kb(c.k) : 0);
             }
         }
         std::vector<sec::Tile> tiles, stl, vtl;
@@ -1394,12 +1223,6 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
             ftl.insert(ftl.end(), kv.second.begin(), kv.second.end());
         }
         sp.off_ftiles = img.put(ftl.data(), ftl.size() * sizeof(sec::Tile));
-        std::vector<sec::Tile> ptl;
-        for (auto &kv : ptiles) {
-            sp.synp.push_back({kv.first, {(uint32_t)ptl.size(), (uint32_t)kv.second.size()}});
-            ptl.insert(ptl.end(), kv.second.begin(), kv.second.end());
-        }
-        sp.off_ptiles = img.put(ptl.data(), ptl.size() * sizeof(sec::Tile));
         sp.off_sdesc = img.put(sdescs.data(), sdescs.size() * sizeof(sec::SynDesc));
         sp.off_stiles = img.put(stl.data(), stl.size() * sizeof(sec::Tile));
         sp.off_ssoff = img.put(ssoff.data(), ssoff.size() * 8);
@@ -1432,12 +1255,11 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::DecSlots sl{plan.meta.as<uint64_t>(sp.off_soff), plan.meta.as<uint32_t>(sp.off_srow),
                            plan.meta.as<uint32_t>(sp.off_mrow), plan.meta.as<uint32_t>(sp.off_savail)};
     for (const Group &g : sp.groups) {
-        // decode groups: the bin kind is the small-batch variant (or 0), or kDecLds
-        int e = g.mfma == kDecLds ? sec_launch_decode_lds(g.rows, blocks, out, dd, dt + g.first, g.count, tabs, sl, s)
-                                  : sec_launch_decode(g.rows, g.U, g.wide, g.lanes, blocks, out, dd, dt + g.first,
-                                                      g.count, tabs, sl, s, g.mfma);
+        // decode groups: the bin kind is the small-batch variant's batch (or 0)
+        int e = sec_launch_decode(g.rows, g.U, g.wide, g.lanes, blocks, out, dd, dt + g.first, g.count, tabs, sl, s,
+                                  g.mfma);
         if (e)
-            return hip_fail((hipError_t)e, g.mfma == kDecLds ? "sec_decode_lds_kernel" : "sec_decode_kernel");
+            return hip_fail((hipError_t)e, "sec_decode_kernel");
     }
     if (sp.ntail) {
         int e = sec_launch_decode_tail(blocks, out, dd, plan.meta.as<sec::TailItem>(sp.off_tail), sp.ntail, tabs,
@@ -1445,7 +1267,7 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_tail");
     }
-    if (sp.syn1.empty() && sp.synf.empty() && sp.synp.empty())
+    if (sp.syn1.empty() && sp.synf.empty())
         return SEC_OK;
     if (!syn && !sp.syn1.empty())
         return SEC_EINVAL;
@@ -1461,13 +1283,6 @@ int launch_decode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
         int e = sec_launch_decode_bs(g.first, lanes, blocks, out, sd, ft + g.second.first, g.second.second, ss, s);
         if (e)
             return hip_fail((hipError_t)e, "sec_decode_bs_kernel");
-    }
-    const sec::Tile *pt = plan.meta.as<sec::Tile>(sp.off_ptiles);
-    for (const auto &g : sp.synp) {
-        int e = sec_launch_decode_bs_pair(g.first / 64, g.first % 64, blocks, out, sd, pt + g.second.first,
-                                          g.second.second, ss, s);
-        if (e)
-            return hip_fail((hipError_t)e, "sec_decode_bs_pair_kernel");
     }
     for (const auto &g : sp.syn1) {
         const bool wg2 = g.first >= kSynWg2;  // key kSynWg2 + shape: two-wave workgroups, both groups
@@ -1549,7 +1364,6 @@ bool pinned(uintptr_t a, uint64_t len, PinnedRange *cache)
 // copies.  A small call then costs its two host copies and one kernel, not two DMA
 // round trips as well.  SHA-1 and the bignum kernels (one latency-bound lane or wave per
 // message) keep the DMA into device scratch: every PCIe read would stall their chains.
-// SEC_STAGE_DMA=1 forces the DMA form for the EC kernels too (A/B).
 bool pinned_mapped(const PinBuf &b)
 {
     PinnedRange cache;
@@ -1561,7 +1375,6 @@ int run_pipeline(sec_ctx *ctx, Plan &plan, Gather gather, Scatter scatter, Launc
 {
     RC(slots_init(ctx));
     CK(hipEventRecord(ctx->meta_ev, ctx->stream()));  // behind the plan upload / table expansion
-    direct = direct && ctx->opt[O_STAGE_DMA] == 0;
     size_t i = 0;
     for (const SubPlan &sp : plan.subs) {
         Slot &sl = ctx->slots[i++ % kSlots];
@@ -2791,7 +2604,6 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
     ctx->syn_chunks += plan.nsyn;
     ctx->direct_chunks += plan.ndirect;
     ctx->fused_chunks += plan.nfused;
-    ctx->pair_chunks += plan.npair;
 
     if (!host) {
         hipEvent_t t0 = nullptr;
@@ -2929,10 +2741,10 @@ int sec_ctx_decode_methods(sec_ctx *ctx, int64_t *fused, int64_t *pair, int64_t 
         return SEC_EINVAL;
     if (fused)
         *fused = ctx->fused_chunks;
-    if (pair)
-        *pair = ctx->pair_chunks;
+    if (pair)  // the one-kernel wave pair is archived (round 5): always 0
+        *pair = 0;
     if (two_kernel)
-        *two_kernel = ctx->syn_chunks - ctx->fused_chunks - ctx->pair_chunks;
+        *two_kernel = ctx->syn_chunks - ctx->fused_chunks;
     if (direct)
         *direct = ctx->direct_chunks;
     return SEC_OK;

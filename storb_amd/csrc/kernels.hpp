@@ -1,8 +1,8 @@
 // kernels.hpp — device-side descriptors shared by kernels.hip and api.cpp.
 //
 // Work decomposition.  A "tile" is one workgroup of L lanes over a run of
-// L*16*U consecutive byte positions t of ONE chunk's blocks (U = 1, 2 or 4;
-// L = 256, or for U = 1 tiles any multiple of 64 up to 1024, sized to the chunk),
+// L*16*U consecutive byte positions t of ONE chunk's blocks (U = 1: the kernels keep U as a
+// template parameter, but only U = 1 is built; L any multiple of 64 up to 1024),
 // and a group of up to 8 output rows (parity rows for encode, missing data rows
 // for decode).  Each lane owns 16 consecutive positions per u-step, so every
 // wave reads one coalesced 1 KiB run from each of the k input blocks and
@@ -150,20 +150,13 @@ int sec_launch_encode(int rows, int U, int wide, int lanes, const uint8_t *in, u
 // (else -1; rows = 0: the first kernel of that (k, m), else the one of `rows` rows per group):
 // all of [0, B) of chunks with B >= 16, row group `group` of sec_bs_groups(shape) (-1: every
 // group in one launch, each tile's r0 = group * sec_bs_rows(shape)), tiles of `lanes` (64..256)
-// lanes over lanes / 64 wave spans of sec_bs_span() positions; group -2 (two-group shapes): one
-// 128-lane workgroup per span (tile t0), its two waves the two row groups sharing the transposes
+// lanes over lanes / 64 wave spans of sec_bs_span() positions
 int sec_bs_shape(int k, int m, int rows = 0);
 int sec_bs_groups(int shape);
 int sec_bs_rows(int shape);
 uint32_t sec_bs_span();
 int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs,
                          const sec::Tile *t, uint32_t ntiles, void *stream);
-// The same rows for chunks of at most sec_bs_lds_max() bytes with 16 <= B <= 8192, one 256-lane
-// workgroup per chunk (tile t0 = 0) that reads the chunk contiguously into LDS first; for the
-// shapes of at most 8 parity rows (else hipErrorInvalidValue)
-uint32_t sec_bs_lds_max();
-int sec_launch_encode_bs_lds(int shape, const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::Tile *t,
-                             uint32_t ntiles, void *stream);
 // Syndrome decode, phase 1, for the shapes sec_syn_shape knows (else -1): tiles as the bit-sliced
 // encode's (r0 = the row group's first parity row; ntail bit 0 = this tile also copies the
 // present primaries to `out`)
@@ -179,12 +172,8 @@ int sec_launch_syndrome_bs_pair(int shape, const uint8_t *blocks, uint8_t *out, 
 // the syndromes stay in registers
 int sec_launch_decode_bs(int shape, int lanes, const uint8_t *blocks, uint8_t *out, const sec::SynDesc *descs,
                          const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream);
-// Both phases in a two-wave workgroup per span (tile t0; ntail bit 0 as above) for chunks whose
-// e <= 16 present parity rows lie in both 16-row groups, on the shapes sec_syn_pair accepts
-// (e_max: the largest e among the tiles' chunks, at most 16)
+// The shapes with the two-wave phase-1 kernel (zfec(64,96): both 16-row parity groups)
 int sec_syn_pair(int shape);
-int sec_launch_decode_bs_pair(int shape, int e_max, const uint8_t *blocks, uint8_t *out, const sec::SynDesc *descs,
-                              const sec::Tile *t, uint32_t ntiles, sec::SynSlots sl, void *stream);
 // Phase 2: the lost data rows of row group r0 / sec_solve_rows(shape) of each tile's chunk
 int sec_solve_rows(int shape);
 // Phase 2, one workgroup per span (tile t0): the span's e <= slots syndrome rows staged in LDS once,
@@ -196,7 +185,7 @@ int sec_launch_solve_bs(int shape, int lanes, const uint8_t *syn, uint8_t *out, 
                         const sec::Tile *t, uint32_t ntiles, const uint64_t *masks, void *stream);
 int sec_launch_encode_tail(const uint8_t *in, uint8_t *par, const sec::EncDesc *descs, const sec::TailItem *items,
                            uint32_t nitems, const uint32_t *tabs, void *stream);
-// kb (4 or 8): the kernel variant whose load batch is kb slots (every chunk of the group has
+// kb (4): the kernel variant whose load batch is kb slots (every chunk of the group has
 // k <= kb; U = 1, not wide); 0: the default batch
 int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *blocks, uint8_t *out,
                       const sec::DecDesc *descs, const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs,
@@ -205,12 +194,6 @@ int sec_launch_decode(int rows, int U, int wide, int lanes, const uint8_t *block
 // one lane per message
 int sec_launch_sha1(const uint8_t *base0, const uint8_t *base1, const sec::MsgDesc *msgs, uint32_t nmsgs,
                     uint8_t *digests, void *stream, int split = 0);
-// Reassembly of chunks of at most sec_dec_lds_max() bytes with 16 <= B <= 8192 and rows = e <= 8
-// lost primaries (every one recovered here), one 256-lane workgroup per chunk (tile t0 = 0): the
-// chunk is put together in LDS and written out as one contiguous run
-uint32_t sec_dec_lds_max();
-int sec_launch_decode_lds(int rows, const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
-                          const sec::Tile *tiles, uint32_t ntiles, const uint32_t *tabs, sec::DecSlots sl, void *stream);
 int sec_launch_decode_tail(const uint8_t *blocks, uint8_t *out, const sec::DecDesc *descs,
                            const sec::TailItem *items, uint32_t nitems, const uint32_t *tabs, sec::DecSlots slots,
                            void *stream);

@@ -103,10 +103,12 @@ def test_options_listed_with_defaults_and_no_environment_reads():
     assert {"SEC_SYN", "SEC_BS", "SEC_BS_LANES", "SEC_REGISTER_MIN", "SEC_HOST_JOIN"} <= set(names)
     assert engine.option_default("SEC_SYN") == -1 and engine.option_default("SEC_BS_LANES") == 256
     assert engine.option_default("SEC_REGISTER_MIN") == 4 << 20
-    # the round-4 A/B outcomes: the kernels that lost are opt-in, the winners on
-    for name, want in (("SEC_BS_LDS", 0), ("SEC_DEC_LDS", 0), ("SEC_BS_PAIR", 0), ("SEC_SYN_PAIR", 0),
-                       ("SEC_SOLVE_LDS", 1), ("SEC_SYN_WG2", 1)):
-        assert engine.option_default(name) == want, name
+    # round 5 archived the A/B-only options with their kernels: at most 12
+    # remain, each forcing a shipped path or sizing the host pipeline
+    assert len(names) <= 12, names
+    for gone in ("SEC_BS_LDS", "SEC_DEC_LDS", "SEC_BS_PAIR", "SEC_SYN_PAIR", "SEC_SOLVE_LDS", "SEC_SYN_WG2",
+                 "SEC_TILE_U", "SEC_STAGE_DMA", "SEC_EXACT_LANES", "SEC_RAGGED_KERNEL"):
+        assert gone not in names, gone
     lib = _lib.load()
     v = ctypes.c_int64(0)
     assert lib.sec_ctx_get_option(None, b"SEC_NOPE", ctypes.byref(v)) == _lib.SEC_EINVAL

@@ -43,11 +43,7 @@ MODES = {
     "all256": {"SEC_BS": 1},
     "all128": {"SEC_BS": 1, "SEC_BS_LANES": 128},
     "all64": {"SEC_BS": 1, "SEC_BS_LANES": 64},
-    "split": {"SEC_BS": 1, "SEC_BS_SPLIT": 1},  # (64,96): one launch per row group
-    "r8": {"SEC_BS": 1, "SEC_BS_R8": 1},  # (32,48) in two interleaved groups of 8 rows
     "off": {"SEC_BS": 0},
-    "lds": {"SEC_BS": 1, "SEC_BS_LDS": 1},  # small chunks LDS-staged whole (opt-in; default is the block-stream tiles)
-    "pair": {"SEC_BS": 1, "SEC_BS_PAIR": 1},  # (64,96): shared-transpose wave pairs (opt-in)
 }
 
 

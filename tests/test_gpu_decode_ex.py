@@ -124,14 +124,13 @@ def _oracle_recovered(data, k, m, keep):
     return b"".join(blocks[s] for s in range(k) if s not in keep)
 
 
-@pytest.mark.parametrize("kb", ["default", "0", "8"])
 @pytest.mark.parametrize("k,m", [(1, 2), (2, 3), (3, 5), (4, 6), (5, 7), (8, 11), (10, 14), (16, 24), (16, 40), (32, 48)])
-def test_recover_only_vs_oracle_device(k, m, kb):
-    """kb: the copy-free decodes' small-batch kernel variants (api.cpp dec_small_kb): default
-    (4-slot batches for k <= 4), "0" (off: 16-slot batches), "8" (also 8-slot for k <= 8)."""
+def test_recover_only_vs_oracle_device(k, m):
+    """The copy-free decodes: k <= 4 through the small-batch kernel variant (api.cpp dec_small_kb,
+    4-slot batches), wider k through the 16-slot batches."""
     from storb_amd.engine import Engine
 
-    engine = Engine(0, options={} if kb == "default" else {"SEC_DEC_REC_KB": int(kb)})
+    engine = Engine(0)
     rng = random.Random(1000 + k * m)
     sizes = [n for n in (k * k, 4096 * k - 3, 65536, 65536 + 9, 6554 * k - 1, 300007)
              if -(-n // k) * (k - 1) <= n]
@@ -402,15 +401,13 @@ def test_fuzz_host_reassembly_join(mode):
         eng.close()
 
 
-@pytest.mark.parametrize("opts", [{}, {"SEC_DEC_LDS": 1}, {"SEC_HOST_JOIN": 0}])
-def test_small_chunks_reassembled_in_lds(opts):
-    """With SEC_DEC_LDS = 1 (opt-in: measured slower than the tiles on C4, profiles/r04_c4_lds_ab.jsonl)
-    chunks of at most 64 KiB with B <= 8192 and e <= 8 reassemble through LDS
-    (sec_decode_lds_kernel: the chunk put together in LDS, written out as one run); against the
-    source bytes and the oracle's decode, B of every residue mod 16 (odd B: byte writes into the
-    image), e = 0 .. 8, block k-1 in place with its short avail, device buffers; with
-    SEC_HOST_JOIN = 0 the same blocks from host buffers (staged, the kernels write every byte);
-    the default is the row-stream tile path."""
+@pytest.mark.parametrize("opts", [{}, {"SEC_HOST_JOIN": 0}])
+def test_small_chunks_reassembled(opts):
+    """Chunks of at most 64 KiB with B <= 8192 and e <= 8 (the shapes round 4's LDS reassembly
+    kernel took; it lost its A/B and is archived) through the row-stream tiles: against the source
+    bytes and the oracle's decode, B of every residue mod 16, e = 0 .. 8, block k-1 in place with
+    its short avail, device buffers; with SEC_HOST_JOIN = 0 the same blocks from host buffers
+    (staged, the kernels write every byte)."""
     from storb_amd.engine import Engine
 
     eng = Engine(0, options=opts)

@@ -16,8 +16,9 @@ with the oracle's own decode of exactly the blocks the kernels were given, for:
 * syndrome chunks mixed with direct-path chunks and other shapes in one call;
 * the path actually taken (sec_ctx_decode_paths / _methods) under SEC_SYN=1 (forced) and the
   default cost rule, with SEC_SYN=0 (the direct decode) giving the same bytes;
-* zfec(64,96) with e <= 16 present parity rows in BOTH groups: the two-wave kernel
-  (sec_decode_bs_pair_kernel), against the two kernels (SEC_SYN_PAIR = 0).
+* zfec(64,96) with e <= 16 present parity rows in BOTH groups: the two kernels, phase 1 in
+  two-wave workgroups (sec_syndrome_bs_pair_kernel).  (Round 4's one-kernel wave pair and the
+  (span, row group) tile forms of both phases lost their A/Bs and are archived.)
 """
 
 import random
@@ -38,20 +39,16 @@ SHAPES = [(16, 24), (32, 48), (64, 96), (10, 14), (8, 12), (8, 11)]
 
 def _engine(syn=None, fused=None):
     """A fresh context with the syndrome options forced (None: the library default).  fused = 0:
-    neither one-kernel method (the one-wave kernel, the wave pair), i.e. the two kernels, phase 2
-    of k >= 32 with each span's syndromes staged in LDS (sec_solve_bs_lds_kernel) and, for parity
-    rows in both groups of (64,96), phase 1 in two-wave workgroups (sec_syndrome_bs_pair_kernel);
-    "tiles": the two kernels with both phases in (span, row group) tiles (SEC_SOLVE_LDS = 0,
-    SEC_SYN_WG2 = 0)."""
+    not the one-wave kernel, i.e. the two kernels, phase 2 of k >= 32 with each span's syndromes
+    staged in LDS (sec_solve_bs_lds_kernel) and, for parity rows in both groups of (64,96),
+    phase 1 in two-wave workgroups (sec_syndrome_bs_pair_kernel)."""
     from storb_amd.engine import Engine
 
     opts = {}
-    if fused == "tiles":
-        fused, opts["SEC_SOLVE_LDS"], opts["SEC_SYN_WG2"] = 0, 0, 0
     if syn is not None:
         opts["SEC_SYN"] = int(syn)
     if fused is not None:
-        opts["SEC_SYN_FUSED"] = opts["SEC_SYN_PAIR"] = int(fused)
+        opts["SEC_SYN_FUSED"] = int(fused)
     return Engine(0, options=opts)
 
 
@@ -157,7 +154,7 @@ def _run(eng, k, m, cases, recover=False, host=None):
 
 @pytest.mark.parametrize("k,m", SHAPES)
 @pytest.mark.parametrize("recover", [False, True])
-@pytest.mark.parametrize("fused", [None, 0, "tiles"])
+@pytest.mark.parametrize("fused", [None, 0])
 def test_syndrome_decode_forced_device(k, m, recover, fused):
     """SEC_SYN=1: every chunk on the syndrome path (the one-wave kernel where it applies, or with
     SEC_SYN_FUSED=0 always the two kernels with the syndromes in HBM; both phase-2 layouts)."""
@@ -258,8 +255,7 @@ def test_syndrome_mixed_batch_with_direct_chunks():
         eng.close()
 
 
-@pytest.mark.parametrize("k,m,e,fused", [(64, 96, 32, 0), (64, 96, 32, "tiles"), (64, 96, 24, None),
-                                         (64, 96, 24, "tiles"), (64, 96, 16, None), (64, 96, 9, None),
+@pytest.mark.parametrize("k,m,e,fused", [(64, 96, 32, 0), (64, 96, 24, None), (64, 96, 16, None), (64, 96, 9, None),
                                          (64, 96, 16, 0), (32, 48, 12, None), (32, 48, 16, 0), (16, 24, 6, None)])
 def test_syndrome_random_patterns(k, m, e, fused):
     """Random lost data blocks and random present parity rows (both parity groups of (64,96): the
@@ -303,11 +299,11 @@ def test_syndrome_lanes_option_and_replan(lanes):
 
 
 @pytest.mark.parametrize("recover", [False, True])
-def test_syndrome_wave_pair_both_groups(recover):
-    """SEC_SYN_PAIR = 1: zfec(64,96), e = 1 .. 16 lost data blocks with present parity rows drawn
-    from both 16-row groups (rows r and r + 16 both present included): the two-wave kernel decodes every chunk
-    (decode_methods' pair count; e = 1 with one row takes the one-wave kernel), equal to the
-    oracle's decode; then the same chunks with the wave pair off (the two kernels), same bytes."""
+def test_syndrome_both_groups(recover):
+    """SEC_SYN = 1: zfec(64,96), e = 1 .. 16 lost data blocks with present parity rows drawn from
+    both 16-row groups (rows r and r + 16 both present included): the two kernels decode every
+    both-group chunk (phase 1 in two-wave workgroups), the one-wave kernel the one-group chunks
+    (decode_methods; the archived wave pair's count stays 0), equal to the oracle's decode."""
     k, m = 64, 96
     rng = random.Random(96 + recover)
     cases = []
@@ -323,15 +319,6 @@ def test_syndrome_wave_pair_both_groups(recover):
             cases.append((n, keep))
     both = sum(1 for _, keep in cases if {(s - k) // 16 for s in keep if s >= k} == {0, 1})
     eng = _engine(1)
-    eng.set_option("SEC_SYN_PAIR", 1)
-    try:
-        _run(eng, k, m, cases, recover=recover)
-        one, pair, two, direct = eng.decode_methods()
-        assert pair == both and one == len(cases) - both and two == 0 and direct == 0, (one, pair, two, direct)
-    finally:
-        eng.close()
-    eng = _engine(1)
-    eng.set_option("SEC_SYN_PAIR", 0)
     try:
         _run(eng, k, m, cases, recover=recover)
         one, pair, two, direct = eng.decode_methods()

@@ -31,13 +31,16 @@ CLASSES = (("4K-64K", 0, 64 << 10), ("64K-1M", 64 << 10, 1 << 20), ("1M-4M", 1 <
 K, M, ERASED = 8, 11, (1, 3, 5)
 
 
-def run(reps: int):
+def run(reps: int, libs: str = "base"):
     import torch
 
     import bench
+    from storb_amd import _build
     from storb_amd.engine import Engine
 
-    eng = Engine(0)
+    tags = libs.split(",")
+    engs = {t: Engine(0, lib_path=_build.LIB if t == "base" else os.path.join(_build.LIBDIR, f"libstorbec_{t}.so"))
+            for t in tags}
     sizes_all = np.array(bench.c5_sizes(), dtype=np.int64)
     res = {"config": f"C5 sizes (bench.c5_sizes) by class, RS(8,3), decode {ERASED} erased reassemble, "
                      f"{reps} launches each, per-launch HIP events", "lib_digest": bench.lib_digest(), "plan": []}
@@ -49,31 +52,35 @@ def run(reps: int):
         par = torch.empty(int(np.sum(B)) * (M - K), dtype=torch.uint8, device="cuda:0")
         out = torch.empty_like(src)
         dd, sn, offs, av = bench.dec_descs_var(sizes, K, M, B, src.data_ptr(), par.data_ptr(), ERASED)
-        eng.encode_batch(ed, src, par)
-        eng.decode_batch(dd, sn, offs, 0, out, block_avail=av)
-        torch.cuda.synchronize()
-        assert torch.equal(out, src), name
-        eng.set_timing(True)
-        for _ in range(reps):
-            eng.encode_batch(ed, src, par, asynchronous=True)
-        for _ in range(reps):
-            eng.decode_batch(dd, sn, offs, 0, out, block_avail=av, asynchronous=True)
-        eng.sync()
-        eng.set_timing(False)
-        ems, en = eng.collect_timing("encode")
-        dms, dn = eng.collect_timing("decode")
-        te, td = ems / en, dms / dn
         ea = total + int(np.sum(B)) * (M - K)
         da = int(np.sum(B)) * K + total
-        res[name] = {"chunks": len(sizes), "bytes": total, "encode_ms": round(te, 4),
-                     "encode_TBs": round(ea / te / 1e9, 3), "decode_ms": round(td, 4),
-                     "decode_TBs": round(da / td / 1e9, 3), "encode_alg_bytes": ea, "decode_alg_bytes": da,
-                     "mean_chunk": round(total / max(len(sizes), 1))}
-        res["plan"].append({"class": name, "launches": 1 + reps, "encode_alg": ea, "decode_alg": da})
+        for tag, eng in engs.items():
+            eng.encode_batch(ed, src, par)
+            eng.decode_batch(dd, sn, offs, 0, out, block_avail=av)
+            torch.cuda.synchronize()
+            if tag == "base":  # (a calibration variant's "parity" is not Reed-Solomon parity)
+                assert torch.equal(out, src), name
+            eng.set_timing(True)
+            for _ in range(reps):
+                eng.encode_batch(ed, src, par, asynchronous=True)
+            for _ in range(reps):
+                eng.decode_batch(dd, sn, offs, 0, out, block_avail=av, asynchronous=True)
+            eng.sync()
+            eng.set_timing(False)
+            ems, en = eng.collect_timing("encode")
+            dms, dn = eng.collect_timing("decode")
+            te, td = ems / en, dms / dn
+            key = name if tag == "base" else f"{name}@{tag}"
+            res[key] = {"chunks": len(sizes), "bytes": total, "encode_ms": round(te, 4),
+                        "encode_TBs": round(ea / te / 1e9, 3), "decode_ms": round(td, 4),
+                        "decode_TBs": round(da / td / 1e9, 3), "encode_alg_bytes": ea, "decode_alg_bytes": da,
+                        "mean_chunk": round(total / max(len(sizes), 1))}
+        res["plan"].append({"class": name, "launches": (1 + reps) * len(engs), "encode_alg": ea, "decode_alg": da})
         del src, par, out
         torch.cuda.empty_cache()
     print(json.dumps(res, indent=1), flush=True)
-    eng.close()
+    for eng in engs.values():
+        eng.close()
 
 
 def _rows(d):
@@ -130,9 +137,10 @@ def main():
     ap.add_argument("mode", choices=("run", "summarize"))
     ap.add_argument("dirs", nargs="*")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--libs", default="base", help="comma list: base and/or tools/sweep.py variant tags (built)")
     a = ap.parse_args()
     if a.mode == "run":
-        run(a.reps)
+        run(a.reps, a.libs)
     else:
         summarize(a.dirs[0], a.dirs[1])
 

@@ -1,10 +1,10 @@
 #!/bin/bash
-# GPU test run: the given pytest targets (default: the whole -m gpu suite), one process,
-# per-test timeout, output under gpurun_out/.
+# The GPU test suite (or the given pytest targets) and smoke(), as the driver runs them: one
+# pytest process, per-test timeouts, output under gpurun_out/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
 T=${*:-tests}
-timeout -k 10 900 python3 -u -m pytest $T -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
-rc=$?
-tail -40 $O/pytest_gpu.log
-exit $rc
+timeout -k 10 600 python -u -m pytest $T -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+tail -3 $O/pytest_gpu.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
