@@ -223,6 +223,22 @@ int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *di
 int sec_encode_digest_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks,
                             const uint8_t *in, uint8_t *parity, uint8_t *digests, unsigned flags);
 
+/* ---- pieces: easyfec's Encoder.encode output in the caller's piece buffers -------------------
+ * Replaces zfec.easyfec.Encoder(k, m).encode(chunk) at /root/reference/storb/util/piece.py:
+ * 129-130 (k slices copied out of the chunk, the last zero-padded, then the m - k parity
+ * blocks), writing every one of chunk c's m pieces to its own host buffer pieces[M_c + j]
+ * (B = ceil(n / k) bytes each; M_c = sum of m over chunks before c), and, when digests is not
+ * NULL, each piece's SHA-1 (20 bytes at digests + 20 (M_c + j): storb's piece id,
+ * hashlib.sha1(piece), piece.py:54-68 / validator.py:1081).  Host memory only (SEC_F_HOST
+ * required; SEC_F_STAGED as for sec_encode_batch); chunks[c].parity_off / parity_stride are
+ * ignored (the parity goes through a context-owned pinned scratch).  The data pieces are copied
+ * and hashed on the context's host threads while the calling thread runs the GPU encode, the
+ * parity pieces right after it; the call returns when every piece and digest is written.
+ * Preconditions and errors as sec_encode_batch; SEC_EINVAL for a NULL piece buffer of a
+ * non-empty chunk. */
+int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
+                      uint8_t *const *pieces, uint8_t *digests, unsigned flags);
+
 /* ---- APDP proofs of data possession: 2048-bit modular arithmetic ----------
  * Replaces the gmpy2 calls of storb's ChallengeSystem
  * (/root/reference/storb/challenge/__init__.py:304-350 generate_tag,

@@ -17,7 +17,7 @@ LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libstorbec.so")
 INCLUDE = os.path.join(ROOT, "include")
 SOURCES = ["kernels.hip", "kernels_bs.hip", "bignum.hip", "api.cpp"]
-HEADERS = ["kernels.hpp", "bignum.hpp", "gf_host.hpp", "gf_const.hpp", "copy_pool.hpp"]
+HEADERS = ["kernels.hpp", "bignum.hpp", "gf_host.hpp", "gf_const.hpp", "copy_pool.hpp", "task_pool.hpp"]
 # gfx950 (MI355X) only: the kernels use gfx950 instructions (16-byte global_load_lds, v_bitop3)
 # and up to 160 KiB of LDS per workgroup; kernels_bs.hip stops any other target with #error
 ARCH = "gfx950"
@@ -32,6 +32,39 @@ def _digest() -> str:
     with open(os.path.join(INCLUDE, "storb_ec.h"), "rb") as f:
         h.update(f.read())
     h.update(ARCH.encode())
+    return h.hexdigest()
+
+
+def _read(path: str) -> str | None:
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _includes(path: str, seen: set) -> None:
+    """The local headers `path` includes, transitively (csrc/ and include/)."""
+    with open(path, encoding="utf-8", errors="replace") as f:
+        for line in f:
+            line = line.strip()
+            if line.startswith("#include \""):
+                name = line.split("\"")[1]
+                for d in (CSRC, INCLUDE):
+                    h = os.path.join(d, name)
+                    if os.path.exists(h) and h not in seen:
+                        seen.add(h)
+                        _includes(h, seen)
+
+
+def _obj_key(src: str, flags: list) -> str:
+    path = os.path.join(CSRC, src)
+    deps: set = set()
+    _includes(path, deps)
+    h = hashlib.sha256(" ".join(flags).encode())
+    for p in [path, *sorted(deps)]:
+        with open(p, "rb") as f:
+            h.update(p.encode() + f.read())
     return h.hexdigest()
 
 
@@ -58,14 +91,23 @@ def build(force: bool = False, verbose: bool = False, defines: dict | None = Non
     for src in SOURCES:
         obj = os.path.join(objdir, src + ".o")
         objs.append(obj)
+        # an object is rebuilt only when its source, a header it includes or the flags changed
+        # (kernels_bs.hip alone takes minutes; an api.cpp edit should not recompile it)
+        key = _obj_key(src, flags)
+        if not force and os.path.exists(obj) and _read(obj + ".key") == key:
+            continue
         cmd = [HIPCC, *flags, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
-        procs.append((src, subprocess.Popen(cmd)))
-    failed = [src for src, p in procs if p.wait() != 0]
+        procs.append((src, obj, key, subprocess.Popen(cmd)))
+    failed = [src for src, _, _, p in procs if p.wait() != 0]
     if failed:
         raise RuntimeError(f"hipcc failed on {', '.join(failed)}")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", tmp, *objs]
+    for _, obj, key, _ in procs:
+        with open(obj + ".key", "w") as f:
+            f.write(key)
+    # libcrypto: OpenSSL's SHA-1 for the host piece ids of sec_encode_pieces (task_pool.hpp)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", "-o", tmp, *objs, "-lcrypto"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

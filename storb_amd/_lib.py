@@ -92,6 +92,7 @@ _SIGS = {
     "sec_decode_batch_ex": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint]),
     "sec_sha1_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, ctypes.c_uint]),
     "sec_encode_digest_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_uint]),
+    "sec_encode_pieces": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_uint]),
     "sec_bn_key_create": (ctypes.c_int, [_vp, _vp, ctypes.POINTER(_vp)]),
     "sec_bn_key_destroy": (None, [_vp]),
     "sec_bn_key_set_crt": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),

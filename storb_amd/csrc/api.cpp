@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "copy_pool.hpp"
+#include "task_pool.hpp"
 #include "bignum.hpp"
 #include "gf_host.hpp"
 #include "kernels.hpp"
@@ -559,6 +560,8 @@ struct sec_ctx {
     size_t bn_part_stride = 0;
     Slot slots[kSlots];
     std::unique_ptr<sec::CopyPool> pool;
+    std::unique_ptr<sec::TaskPool> tasks;  // sec_encode_pieces: piece copies and host SHA-1
+    PinBuf piece_par;                      // sec_encode_pieces: the parity, before the piece copies
     // SEC_F_HOST encode / decode calls by path (sec_ctx_host_paths)
     int64_t zero_copy_calls = 0, registered_calls = 0, staged_calls = 0;
     int64_t syn_chunks = 0, direct_chunks = 0, fused_chunks = 0;  // decodes by method (sec_ctx_decode_paths)
@@ -585,14 +588,24 @@ int set_dev(const sec_ctx *ctx)
     return SEC_OK;
 }
 
+int host_threads(const sec_ctx *ctx)
+{
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    return ctx->opt[O_COPY_THREADS] ? (int)ctx->opt[O_COPY_THREADS] : (int)std::min(7u, std::max(1u, hw / 2));
+}
+
 sec::CopyPool &pool(sec_ctx *ctx)
 {
-    if (!ctx->pool) {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        const int n = ctx->opt[O_COPY_THREADS] ? (int)ctx->opt[O_COPY_THREADS] : (int)std::min(7u, std::max(1u, hw / 2));
-        ctx->pool.reset(new sec::CopyPool(n));
-    }
+    if (!ctx->pool)
+        ctx->pool.reset(new sec::CopyPool(host_threads(ctx)));
     return *ctx->pool;
+}
+
+sec::TaskPool &tasks(sec_ctx *ctx)
+{
+    if (!ctx->tasks)
+        ctx->tasks.reset(new sec::TaskPool(host_threads(ctx)));
+    return *ctx->tasks;
 }
 
 int slots_init(sec_ctx *ctx)
@@ -1672,7 +1685,9 @@ void sec_ctx_destroy(sec_ctx *ctx)
         if (s.s)
             (void)hipStreamDestroy(s.s);
     }
+    ctx->tasks.reset();
     ctx->pool.reset();
+    ctx->piece_par.release();
     ctx->pin.release();
     ctx->enc_tabs.buf.release();
     ctx->dec_tabs.buf.release();
@@ -1731,8 +1746,10 @@ int sec_ctx_set_option(sec_ctx *ctx, const char *name, int64_t value)
     ctx->opt.v[i] = value;
     for (Plan *p : {&ctx->enc_plan, &ctx->dec_plan, &ctx->sha_plan, &ctx->bn_plan})
         p->valid = false;
-    if (i == O_COPY_THREADS)
+    if (i == O_COPY_THREADS) {
         ctx->pool.reset();
+        ctx->tasks.reset();
+    }
     return SEC_OK;
 }
 
@@ -2175,6 +2192,96 @@ int sec_encode_digest_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t n
                             uint8_t *parity, uint8_t *digests, unsigned flags)
 {
     return encode_impl(ctx, chunks, nchunks, in, parity, digests, flags, true);
+}
+
+// easyfec's Encoder.encode output for every chunk, as pieces in caller buffers: the k data
+// slices (copies, the last zero-padded to B) and the m - k parity blocks, each in its own buffer,
+// plus (digests) each piece's SHA-1.  The data pieces are copied and hashed on the context's
+// task threads while this thread runs the encode (the parity into a pinned scratch); the parity
+// pieces are copied and hashed as soon as it returns.  Everything but the GPU call is host work
+// that the Python layer would otherwise do on its own threads, under the GIL's hand-offs
+// (VERDICT r04 next #7).
+int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
+                      uint8_t *const *pieces, uint8_t *digests, unsigned flags)
+{
+    if (!ctx || nchunks < 0 || (nchunks > 0 && (!chunks || !pieces)) || !(flags & SEC_F_HOST) ||
+        (flags & ~(SEC_F_HOST | SEC_F_STAGED)))
+        return SEC_EINVAL;
+    if (nchunks == 0)
+        return SEC_OK;
+    if (nchunks >= (int64_t)UINT32_MAX)
+        return SEC_EINVAL;
+    uint64_t total_par = 0;
+    for (int64_t i = 0; i < nchunks; ++i) {  // easyfec / _fec preconditions (as encode_impl)
+        const sec_enc_chunk &c = chunks[i];
+        if (c.k < 1 || c.m < c.k || c.m > 256)
+            return SEC_EKM;
+        const uint64_t B = enc_B(c);
+        if (c.k > 1 && (uint64_t)(c.k - 1) * B > c.n)
+            return SEC_EBLOCKLEN;
+        if (B >= (1ull << 31))
+            return SEC_ESIZE;
+        total_par += (uint64_t)(c.m - c.k) * B;
+    }
+    for (int64_t i = 0, pb = 0; i < nchunks; pb += chunks[i++].m)  // a buffer for every non-empty piece
+        for (int j = 0; j < chunks[i].m; ++j)
+            if (!pieces[pb + j] && enc_B(chunks[i]) > 0)
+                return SEC_EINVAL;
+    RC(set_dev(ctx));
+    RC(ctx->piece_par.ensure(std::max<uint64_t>(total_par, 1)));
+    sec::TaskPool &tp = tasks(ctx);
+    sec::TaskPool::Group data, par;
+    std::vector<sec_enc_chunk> tmp(chunks, chunks + nchunks);
+    uint64_t pb = 0, po = 0;
+    for (int64_t i = 0; i < nchunks; ++i) {
+        const sec_enc_chunk &c = chunks[i];
+        const uint64_t B = enc_B(c);
+        for (int j = 0; j < c.k && B > 0; ++j) {
+            const uint64_t start = (uint64_t)j * B;
+            const uint64_t av = c.n > start ? std::min<uint64_t>(B, c.n - start) : 0;
+            uint8_t *dst = pieces[pb + j];
+            // (a NULL `in` with absolute in_off is legal here, as in sec_encode_batch's host mode)
+            const uint8_t *src = (const uint8_t *)((uintptr_t)in + c.in_off + start);
+            uint8_t *dig = digests ? digests + (pb + j) * 20 : nullptr;
+            tp.submit(data, [=] {
+                if (av)
+                    memcpy(dst, src, av);
+                if (av < B)
+                    memset(dst + av, 0, B - av);
+                return !dig || sec::sha1_padded(dst, B, B, dig);
+            });
+        }
+        tmp[i].parity_off = po;
+        tmp[i].parity_stride = B;
+        po += (uint64_t)(c.m - c.k) * B;
+        pb += (uint64_t)c.m;
+    }
+    int rc = SEC_OK;
+    if (total_par)
+        rc = encode_impl(ctx, tmp.data(), nchunks, in, (uint8_t *)ctx->piece_par.p, nullptr,
+                         SEC_F_HOST | (flags & SEC_F_STAGED), false);
+    if (rc == SEC_OK) {
+        pb = 0;
+        for (int64_t i = 0; i < nchunks; ++i) {
+            const sec_enc_chunk &c = chunks[i];
+            const uint64_t B = enc_B(c);
+            for (int r = 0; r < c.m - c.k && B > 0; ++r) {
+                uint8_t *dst = pieces[pb + c.k + r];
+                const uint8_t *src = (const uint8_t *)ctx->piece_par.p + tmp[i].parity_off + (uint64_t)r * B;
+                uint8_t *dig = digests ? digests + (pb + c.k + r) * 20 : nullptr;
+                tp.submit(par, [=] {
+                    memcpy(dst, src, B);
+                    return !dig || sec::sha1_padded(dst, B, B, dig);
+                });
+            }
+            pb += (uint64_t)c.m;
+        }
+    }
+    const bool ok_data = tp.wait(data), ok_par = tp.wait(par);  // both waited: no task outlives the call
+    const bool ok = ok_data && ok_par;
+    if (rc == SEC_OK && !ok)
+        rc = SEC_EINVAL;  // OpenSSL failed (no other cause)
+    return rc;
 }
 
 int sec_sha1_batch(sec_ctx *ctx, const sec_msg *msgs, int64_t nmsgs, uint8_t *digests, unsigned flags)

@@ -306,6 +306,32 @@ class Engine:
             self.encode_batch(descs, 0, out, host=True, staged=staged)
         return out, layout
 
+    def encode_pieces_into(self, chunks, shapes, piece_addrs, digests: np.ndarray | None = None,
+                           staged: bool = False) -> None:
+        """easyfec's Encoder.encode output for every chunk written to caller buffers
+        (sec_encode_pieces): piece_addrs[M_c + j] = the address of a writable B-byte buffer for
+        piece j of chunk c (M_c = sum of m over the chunks before c); digests (optional, a
+        writable uint8 array of 20 bytes per piece) receives each piece's SHA-1, computed on the
+        library's host threads while the GPU encodes.  shapes: [(k, m)] per chunk."""
+        n = len(chunks)
+        descs = np.zeros(n, dtype=ENC_DTYPE)
+        keep = []
+        for i, (c, (k, m)) in enumerate(zip(chunks, shapes)):
+            a, kp = addr(c)
+            keep.append(kp)
+            ln = len(kp) if isinstance(kp, np.ndarray) else len(c)
+            B = -(-ln // k) if ln else 0
+            descs[i] = (a, ln, 0, max(B, 1), k, m)
+        pa = np.ascontiguousarray(piece_addrs, dtype=np.uint64)
+        if pa.size != sum(m for (_, m) in shapes):
+            raise ValueError("encode_pieces_into: one piece address per piece")
+        if digests is not None and digests.size < 20 * pa.size:
+            raise ValueError("encode_pieces_into: digests needs 20 bytes per piece")
+        flags = SEC_F_HOST | (SEC_F_STAGED if staged else 0)
+        if n:
+            self._check(self.lib.sec_encode_pieces(self._ctx, _ptr(descs), n, None, _ptr(pa),
+                                                   None if digests is None else _ptr(digests), flags))
+
     def encode_host(self, chunks, shapes, digests: bool = False):
         """Parity blocks for each chunk.  chunks: bytes-like list; shapes: [(k, m)] per chunk.
 

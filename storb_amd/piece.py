@@ -80,6 +80,11 @@ PREFETCH_MIN_CHUNK = 512 << 10
 # 4 MiB object fell from 1236-1289 to 811 MiB/s per chunk, 1327-1469 to 868 streamed).
 PARALLEL_COPY_MIN = 256 << 10
 HASH_ON_FILL = True  # encode_chunk: each large piece's id hashing starts as soon as that piece is filled
+# The pieces (easyfec's k slices + the parity) and their SHA-1 ids made by the library in one call
+# (sec_encode_pieces: copies and OpenSSL SHA-1 on its own host threads, the data pieces while
+# the GPU encodes), instead of Python slicing / numpy fills and hashlib on the thread pool.
+# False: the round-4 paths (A/B: tools/c1_loopback.py, tools/small_call_profile.py).
+HOST_PIECES = True
 
 # The library never retunes the host process's allocator.  A validator that drops each chunk's
 # pieces after sending them can keep glibc from trimming the freed heap back to the kernel (so the
@@ -500,6 +505,54 @@ def _pieces_parallel(chunks: list, shapes: list, digests: bool = False, hash_ids
     return (out, ids) if digests else out
 
 
+class _Done:
+    """A finished result in the memo's future slot (the library computed the digest already)."""
+
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v
+
+    def result(self):
+        return self.v
+
+    def cancel(self):
+        return False
+
+
+def _encode_pieces(chunks: list, shapes: list, ids: bool):
+    """Every chunk's m pieces as new bytes objects, filled by the library (sec_encode_pieces:
+    the k data slices, zero-padded, then the parity), and with `ids` each piece's SHA-1 hex
+    (the library's host threads, OpenSSL: hashlib's bytes).  Returns (pieces, ids or None)."""
+    objs, addrs = [], []
+    for (k, m, B, _) in shapes:
+        row = []
+        for _ in range(m):
+            b, v = _new_bytes(B)
+            row.append((b, v))
+            addrs.append(v.ctypes.data if B else 0)
+        objs.append(row)
+    dig = np.empty(max(20 * len(addrs), 1), dtype=np.uint8) if ids else None
+    # staged, not page-locked: the library's threads fault in the new pieces meanwhile, and locking
+    # waits on the same memory-map lock (6.4 against 0.55 ms for one 8 MiB chunk on MI355X,
+    # profiles/r03_upload_ab.jsonl)
+    get_engine().encode_pieces_into(chunks, [(k, m) for (k, m, _, _) in shapes], addrs, dig, staged=True)
+    pieces = [[_finalize(b) for b, _ in row] for row in objs]
+    hexes = None
+    if ids:
+        hx, hexes, f = dig.tobytes().hex(), [], 0
+        for (_, m, _, _) in shapes:
+            hexes.append([hx[40 * (f + j):40 * (f + j + 1)] for j in range(m)])
+            f += m
+    return pieces, hexes
+
+
+def _short_middle(shapes, chunks) -> None:
+    for c, (k, m, B, _) in zip(chunks, shapes):
+        if k > 1 and (k - 1) * B > len(c):  # easyfec's short middle slice, as Encoder.encode
+            raise Error("Precondition violation: Input blocks are required to be all the same length.")
+
+
 def _build(chunk_idx: int, k: int, m: int, B: int, padlen: int, n: int, blocks: list[bytes]) -> EncodedChunk:
     pieces = []
     for i, block in enumerate(blocks):
@@ -517,6 +570,14 @@ def encode_chunk(chunk: bytes, chunk_idx: int) -> EncodedChunk:
     logger.debug("[encode_chunk] chunk %d: %d bytes, piece_size = %d", chunk_idx, chunk_size, piece_size)
     k, m, B, padlen = chunk_shape(chunk_size)
     enc_ = Encoder(k, m)
+    if HOST_PIECES:  # pieces and (prefetched) ids from the library in one call
+        call = _memo.begin(m * B) if PREFETCH_PIECE_IDS else None
+        _short_middle([(k, m, B, padlen)], [chunk])
+        pieces, ids = _encode_pieces([chunk], [(k, m, B, padlen)], call is not None)
+        if call is not None:
+            for b, h in zip(pieces[0], ids[0]):
+                _memo.put(b, _Done(h), call)
+        return _build(chunk_idx, k, m, B, padlen, chunk_size, pieces[0])
     call = _memo.begin(m * B) if PREFETCH_PIECE_IDS and chunk_size >= PREFETCH_MIN_CHUNK else None
     if call is None:
         encoded_pieces = enc_.encode(chunk)
@@ -558,6 +619,11 @@ def encode_chunks(chunks: typing.Sequence[bytes], first_chunk_idx: int = 0, *, d
         parts = grp.map_shares(lambda share, lo: encode_chunks(share, first_chunk_idx + lo, devices=_ONE),
                                list(chunks), [len(c) for c in chunks])
         return [ec for p in parts if p for ec in p]
+    if HOST_PIECES:
+        _short_middle(shapes, chunks)
+        pieces, _ = _encode_pieces(list(chunks), shapes, False)
+        return [_build(first_chunk_idx + i, k, m, B, padlen, len(c), ps)
+                for i, (c, (k, m, B, padlen), ps) in enumerate(zip(chunks, shapes, pieces))]
     if min(B for (_, _, B, _) in shapes) >= PARALLEL_COPY_MIN:  # piece copies in parallel
         pieces = _pieces_parallel(list(chunks), shapes)
         return [_build(first_chunk_idx + i, k, m, B, padlen, len(c), ps)
@@ -807,6 +873,11 @@ def _encode_window(window: list, first_idx: int, piece_ids: bool):
         hp = _pool("hash")
         if GPU_PIECE_IDS and min(B for (_, _, B, _) in shapes) >= PARALLEL_COPY_MIN:
             pieces, ids = _pieces_parallel(window, shapes, digests=True)
+            out = [_build(first_idx + i, k, m, B, padlen, len(c), ps)
+                   for i, (c, (k, m, B, padlen), ps) in enumerate(zip(window, shapes, pieces))]
+            return list(zip(out, ids)), err
+        if HOST_PIECES:  # ids by the library's host threads (OpenSSL), pieces in the same call
+            pieces, ids = _encode_pieces(list(window), shapes, True)
             out = [_build(first_idx + i, k, m, B, padlen, len(c), ps)
                    for i, (c, (k, m, B, padlen), ps) in enumerate(zip(window, shapes, pieces))]
             return list(zip(out, ids)), err

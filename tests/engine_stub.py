@@ -61,3 +61,18 @@ class OracleHostEngine(Engine):
                     p + int(c["parity_off"]) + (i - k) * int(c["parity_stride"]), B)
                 d[20 * j:20 * (j + 1)] = np.frombuffer(hashlib.sha1(blk).digest(), np.uint8)
                 j += 1
+
+    def encode_pieces_into(self, chunks, shapes, piece_addrs, digests=None, staged=False):
+        """sec_encode_pieces on the oracle: every piece written to its address, its SHA-1 beside."""
+        from oracle import cfec
+
+        self.threads.add(threading.get_ident())
+        self.chunks_encoded += len(chunks)
+        j = 0
+        for c, (k, m) in zip(chunks, shapes):
+            for b in cfec.easy_encode(bytes(c), k, m):
+                if b:
+                    ctypes.memmove(int(piece_addrs[j]), b, len(b))
+                if digests is not None:
+                    digests[20 * j:20 * (j + 1)] = np.frombuffer(hashlib.sha1(b).digest(), np.uint8)
+                j += 1

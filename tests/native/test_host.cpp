@@ -1,6 +1,6 @@
-// Host-side unit test of libstorbec's C++ helpers (no HIP): GF matrices and the
-// staging copy pool.  Built by tests/test_native_host.py with g++ under
-// AddressSanitizer + UBSan and, separately, ThreadSanitizer (the pool's threads).
+// Host-side unit test of libstorbec's C++ helpers (no HIP): GF matrices, the staging copy
+// pool, and the task pool + SHA-1 of sec_encode_pieces.  Built by tests/test_native_host.py
+// with g++ under AddressSanitizer + UBSan and, separately, ThreadSanitizer (the pools' threads).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -10,6 +10,7 @@
 
 #include "copy_pool.hpp"
 #include "gf_host.hpp"
+#include "task_pool.hpp"
 
 static int fails = 0;
 #define EXPECT(c)                                                        \
@@ -73,10 +74,57 @@ static void test_copy_pool()
     }
 }
 
+static void test_task_pool_sha1()
+{
+    // known answers (FIPS 180-1): "abc", and the empty message
+    uint8_t d[20];
+    const uint8_t abc[20] = {0xa9, 0x99, 0x3e, 0x36, 0x47, 0x06, 0x81, 0x6a, 0xba, 0x3e,
+                             0x25, 0x71, 0x78, 0x50, 0xc2, 0x6c, 0x9c, 0xd0, 0xd8, 0x9d};
+    EXPECT(sec::sha1_padded((const uint8_t *)"abc", 3, 3, d) && memcmp(d, abc, 20) == 0);
+    const uint8_t empty[20] = {0xda, 0x39, 0xa3, 0xee, 0x5e, 0x6b, 0x4b, 0x0d, 0x32, 0x55,
+                               0xbf, 0xef, 0x95, 0x60, 0x18, 0x90, 0xaf, 0xd8, 0x07, 0x09};
+    EXPECT(sec::sha1_padded(nullptr, 0, 0, d) && memcmp(d, empty, 20) == 0);
+    // the padded form equals the hash of the explicitly zero-padded bytes, from many threads
+    std::mt19937_64 rng(11);
+    sec::TaskPool pool(6);
+    for (int round = 0; round < 8; ++round) {
+        const int n = 1 + (int)(rng() % 64);
+        std::vector<std::vector<uint8_t>> msg(n);
+        std::vector<size_t> avail(n);
+        std::vector<uint8_t> got((size_t)n * 20), want((size_t)n * 20);
+        for (int i = 0; i < n; ++i) {
+            const size_t len = rng() % (round % 2 ? 70000 : 300);
+            avail[i] = len ? rng() % (len + 1) : 0;
+            msg[i].assign(len, 0);
+            for (size_t b = 0; b < avail[i]; ++b)
+                msg[i][b] = (uint8_t)rng();
+            EXPECT(sec::sha1_padded(msg[i].data(), len, len, &want[(size_t)i * 20]));
+        }
+        sec::TaskPool::Group g1, g2;
+        for (int i = 0; i < n; ++i) {
+            sec::TaskPool::Group &g = i % 2 ? g1 : g2;
+            const uint8_t *p = msg[i].data();
+            const size_t av = avail[i], len = msg[i].size();
+            uint8_t *o = &got[(size_t)i * 20];
+            pool.submit(g, [=] { return sec::sha1_padded(p, av, len, o); });
+        }
+        EXPECT(pool.wait(g1));
+        EXPECT(pool.wait(g2));
+        EXPECT(got == want);
+    }
+    sec::TaskPool::Group gf;  // a failing task is reported, the rest still run
+    std::atomic<int> ran{0};
+    for (int i = 0; i < 20; ++i)
+        pool.submit(gf, [&ran, i] { ++ran; return i != 7; });
+    EXPECT(!pool.wait(gf));
+    EXPECT(ran.load() == 20);
+}
+
 int main()
 {
     test_matrices();
     test_copy_pool();
+    test_task_pool_sha1();
     if (fails)
         return 1;
     printf("native host tests ok\n");

@@ -1,0 +1,120 @@
+"""GPU: sec_encode_pieces — easyfec's Encoder.encode output written straight into the caller's
+piece buffers, with each piece's SHA-1 from the library's host threads (VERDICT r04 next #7:
+the per-call floor at storb's granularity).  Every piece is compared with the oracle's
+(oracle/fec_oracle.c easy_encode) and every digest with hashlib; the drop-in's encode_chunk /
+encode_chunks / encode_chunks_stream give the same pieces and ids with the library path on and
+off (piece.HOST_PIECES)."""
+
+import ctypes
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from oracle import cfec
+
+pytestmark = pytest.mark.gpu
+
+from storb_amd import piece  # noqa: E402
+from storb_amd.engine import ECRuntimeError, Error, get_engine  # noqa: E402
+
+
+def _shapes_and_chunks(rng):
+    out = []
+    for n in (1, 2, 17, 4096, 16384, 16385, 70_000, 256 << 10, (256 << 10) + 1, 1 << 20, 3 << 20, (8 << 20) + 5):
+        out.append((piece.chunk_shape(n), rng.randbytes(n)))
+    for k, m, n in ((1, 2, 999), (4, 6, 6554 * 4 - 3), (10, 14, 65536), (8, 11, 300_007), (16, 24, 2 << 20),
+                    (64, 96, 1 << 20), (3, 3, 5000)):
+        B = -(-n // k)
+        out.append(((k, m, B, k * B - n), rng.randbytes(n)))
+    return out
+
+
+def _run(cases, digests=True):
+    eng = get_engine()
+    bufs, addrs = [], []
+    for (k, m, B, _), _ in cases:
+        row = [np.empty(B, np.uint8) for _ in range(m)]
+        bufs.append(row)
+        addrs += [a.ctypes.data for a in row]
+    dig = np.zeros(20 * len(addrs), np.uint8) if digests else None
+    eng.encode_pieces_into([c for _, c in cases], [(k, m) for (k, m, _, _), _ in cases], addrs, dig)
+    return bufs, dig
+
+
+def test_pieces_and_ids_vs_oracle():
+    rng = random.Random(1)
+    cases = _shapes_and_chunks(rng)
+    rng.shuffle(cases)  # shapes interleaved in one call
+    bufs, dig = _run(cases)
+    j = 0
+    for ((k, m, B, padlen), c), row in zip(cases, bufs):
+        want = cfec.easy_encode(c, k, m)
+        assert [r.tobytes() for r in row] == want, (k, m, len(c))
+        for w in want:
+            assert dig[20 * j:20 * (j + 1)].tobytes() == hashlib.sha1(w).digest(), (k, m, len(c), j)
+            j += 1
+
+
+def test_pieces_without_ids_and_repeat_calls():
+    rng = random.Random(2)
+    cases = _shapes_and_chunks(rng)[:8]
+    for _ in range(3):  # the pinned parity scratch and the task pool reused across calls
+        bufs, dig = _run(cases, digests=False)
+        assert dig is None
+        for ((k, m, _, _), c), row in zip(cases, bufs):
+            assert [r.tobytes() for r in row] == cfec.easy_encode(c, k, m)
+
+
+def test_pieces_errors():
+    eng = get_engine()
+    with pytest.raises(Error):  # easyfec's short middle slice (k = 4, n = 5: B = 2, 3 * 2 > 5)
+        eng.encode_pieces_into([b"12345"], [(4, 6)], [np.empty(2, np.uint8).ctypes.data] * 6)
+    with pytest.raises(ECRuntimeError, match="invalid argument"):  # a NULL piece buffer (SEC_EINVAL)
+        eng.encode_pieces_into([b"x" * 100], [(2, 3)], [0, 0, 0])
+    with pytest.raises(ValueError):  # one address per piece
+        eng.encode_pieces_into([b"x" * 100], [(2, 3)], [1, 2])
+    lib = eng.lib
+    assert lib.sec_encode_pieces(eng._ctx, None, 1, None, None, None, 1) != 0  # no descriptors
+    assert lib.sec_encode_pieces(eng._ctx, None, 0, None, None, None, 0) != 0  # device mode refused
+
+
+@pytest.mark.parametrize("n", [1000, 256 << 10, 512 << 10, 8 << 20])
+def test_encode_chunk_host_pieces_same_as_round4_path(n):
+    data = random.Random(n).randbytes(n)
+    old = piece.HOST_PIECES
+    try:
+        piece.HOST_PIECES = False
+        a = piece.encode_chunk(data, 3)
+        piece.HOST_PIECES = True
+        b = piece.encode_chunk(data, 3)
+    finally:
+        piece.HOST_PIECES = old
+    assert a.model_dump() == b.model_dump()
+    k, m = b.k, b.m
+    assert [p.data for p in b.pieces] == cfec.easy_encode(data, k, m)
+    # the validator's piece_hash right after encode_chunk (validator.py:1081): the library's ids
+    assert [piece.piece_hash(p.data) for p in b.pieces] == [hashlib.sha1(p.data).hexdigest() for p in b.pieces]
+
+
+def test_encode_chunks_and_stream_host_pieces():
+    rng = random.Random(5)
+    chunks = [rng.randbytes(rng.choice([3, 4096, 100_000, 300_001, 1 << 20])) for _ in range(12)]
+    ecs = piece.encode_chunks(chunks, 4)
+    for c, ec in zip(chunks, ecs):
+        assert [p.data for p in ec.pieces] == cfec.easy_encode(c, ec.k, ec.m)
+    outs = list(piece.encode_chunks_stream(chunks, 0, piece_ids=True, window_bytes=600_000))
+    for c, (ec, ids) in zip(chunks, outs):
+        want = cfec.easy_encode(c, ec.k, ec.m)
+        assert [p.data for p in ec.pieces] == want
+        assert ids == [hashlib.sha1(w).hexdigest() for w in want]
+
+
+def test_pieces_bytes_are_immutable_objects():
+    """The pieces are ordinary bytes objects (filled in place before anyone sees them)."""
+    ec = piece.encode_chunk(b"abc" * 50_000, 0)
+    for p in ec.pieces:
+        assert type(p.data) is bytes
+    raw = ctypes.string_at(id(ec.pieces[0].data) + bytes.__basicsize__ - 1, 4) if piece._FILL_IN_PLACE else None
+    assert raw is None or raw == ec.pieces[0].data[:4]

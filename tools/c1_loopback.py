@@ -18,6 +18,8 @@ same bytes, median of --reps runs, one thread of caller code:
                   piece_hash per piece, reconstruct_data
   dropin_no_prefetch  the same with PREFETCH_PIECE_IDS = False (piece ids hashed serially by
                   the caller, exactly as the reference)
+  dropin_round4_host_path  the same with HOST_PIECES = False (round 4's host side: Python piece
+                  fills and a hashlib thread pool instead of sec_encode_pieces)
   streamed        the pipelined entry points: encode_chunks_stream(piece_ids=True) and
                   reconstruct_data_stream
 """
@@ -128,10 +130,16 @@ def main():
             r["dropin_no_prefetch"] = timed(lambda d: loopback(d, *drop), data, a.reps)
         finally:
             piece.PREFETCH_PIECE_IDS = True
+        piece.HOST_PIECES = False  # A/B: round 4's Python piece fills and hashlib pool
+        try:
+            r["dropin_round4_host_path"] = timed(lambda d: loopback(d, *drop), data, a.reps)
+        finally:
+            piece.HOST_PIECES = True
         r["streamed"] = timed(streamed, data, a.reps)
         res[label] = {k: round(v, 1) for k, v in r.items()}
         res[label]["dropin_over_reference"] = round(r["dropin"] / r["reference_cpu"], 2)
         res[label]["dropin_no_prefetch_over_reference"] = round(r["dropin_no_prefetch"] / r["reference_cpu"], 2)
+        res[label]["dropin_round4_over_reference"] = round(r["dropin_round4_host_path"] / r["reference_cpu"], 2)
     print(json.dumps(res, indent=1))
 
 

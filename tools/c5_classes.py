@@ -31,7 +31,7 @@ CLASSES = (("4K-64K", 0, 64 << 10), ("64K-1M", 64 << 10, 1 << 20), ("1M-4M", 1 <
 K, M, ERASED = 8, 11, (1, 3, 5)
 
 
-def run(reps: int, libs: str = "base"):
+def run(reps: int, libs: str = "base", extra: bool = False):
     import torch
 
     import bench
@@ -44,16 +44,19 @@ def run(reps: int, libs: str = "base"):
     sizes_all = np.array(bench.c5_sizes(), dtype=np.int64)
     res = {"config": f"C5 sizes (bench.c5_sizes) by class, RS(8,3), decode {ERASED} erased reassemble, "
                      f"{reps} launches each, per-launch HIP events", "lib_digest": bench.lib_digest(), "plan": []}
-    for name, lo, hi in CLASSES:
-        sizes = [int(s) for s in sizes_all if lo <= s < hi]
+    cases = [(name, [int(s) for s in sizes_all if lo <= s < hi], K, M, ERASED) for name, lo, hi in CLASSES]
+    if extra:  # the other BASELINE shapes through the same harness (C3: 1024 x 1 MiB RS(4,2); C4: one GPU's share)
+        cases += [("C3_1024x1MiB_rs42", [1 << 20] * 1024, 4, 6, (1, 3)),
+                  ("C4_8192x64KiB_rs104", [65536] * 8192, 10, 14, (0, 2, 5, 7))]
+    for name, sizes, K_, M_, ER in cases:
         total = int(np.sum(sizes))
-        ed, B = bench.enc_descs_var(sizes, K, M)
+        ed, B = bench.enc_descs_var(sizes, K_, M_)
         src = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda:0")
-        par = torch.empty(int(np.sum(B)) * (M - K), dtype=torch.uint8, device="cuda:0")
+        par = torch.empty(int(np.sum(B)) * (M_ - K_), dtype=torch.uint8, device="cuda:0")
         out = torch.empty_like(src)
-        dd, sn, offs, av = bench.dec_descs_var(sizes, K, M, B, src.data_ptr(), par.data_ptr(), ERASED)
-        ea = total + int(np.sum(B)) * (M - K)
-        da = int(np.sum(B)) * K + total
+        dd, sn, offs, av = bench.dec_descs_var(sizes, K_, M_, B, src.data_ptr(), par.data_ptr(), ER)
+        ea = total + int(np.sum(B)) * (M_ - K_)
+        da = int(np.sum(B)) * K_ + total
         for tag, eng in engs.items():
             eng.encode_batch(ed, src, par)
             eng.decode_batch(dd, sn, offs, 0, out, block_avail=av)
@@ -138,9 +141,10 @@ def main():
     ap.add_argument("dirs", nargs="*")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--libs", default="base", help="comma list: base and/or tools/sweep.py variant tags (built)")
+    ap.add_argument("--extra", action="store_true", help="also C3 (1024 x 1 MiB RS(4,2)) and one GPU's C4 share")
     a = ap.parse_args()
     if a.mode == "run":
-        run(a.reps, a.libs)
+        run(a.reps, a.libs, a.extra)
     else:
         summarize(a.dirs[0], a.dirs[1])
 

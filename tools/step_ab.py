@@ -62,7 +62,8 @@ def main():
         out.zero_()
         e.encode_batch(ed, src, par)
         e.decode_batch(dd, sn, offs, 0, out, block_avail=av)
-        assert torch.equal(out, src), t
+        if t != "nogf":  # (the calibration variant writes no Reed-Solomon bytes)
+            assert torch.equal(out, src), t
     wall = {t: [] for t in tags}
     kern = {t: {"encode": [], "decode": []} for t in tags}
     for _ in range(a.rounds):
