@@ -323,6 +323,16 @@ int sec_ctx_decode_methods(sec_ctx *ctx, int64_t *fused, int64_t *pair, int64_t 
 /* kind: 0 host->device, 1 device->host, 2 device->device; synchronous on the ctx stream */
 int sec_memcpy(sec_ctx *ctx, void *dst, const void *src, size_t bytes, int kind);
 int sec_memset(sec_ctx *ctx, void *dptr, int value, size_t bytes);
+/* Host-to-host copies on the context's copy threads (the caller's thread takes part): dst[i] <-
+ * src[i] for len[i] bytes, src 0 = zero-fill.  The Python layer joins a reassembled chunk's rows
+ * (present pieces and recovered rows) into its output object with this instead of a
+ * single-threaded b"".join (easyfec's join, /root/reference/storb/util/piece.py:196-197). */
+typedef struct sec_copy {
+    uint64_t dst;
+    uint64_t src;
+    uint64_t len;
+} sec_copy;
+int sec_host_copy(sec_ctx *ctx, const sec_copy *jobs, int64_t njobs);
 
 #ifdef __cplusplus
 }

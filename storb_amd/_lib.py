@@ -57,6 +57,7 @@ ENC_DTYPE = np.dtype([("in_off", "<u8"), ("n", "<u8"), ("parity_off", "<u8"), ("
 DEC_DTYPE = np.dtype([("out_off", "<u8"), ("B", "<u8"), ("padlen", "<u8"), ("slot0", "<u8"),
                       ("k", "<i4"), ("m", "<i4")], align=True)
 MSG_DTYPE = np.dtype([("addr", "<u8"), ("len", "<u8"), ("avail", "<u8")], align=True)
+COPY_DTYPE = np.dtype([("dst", "<u8"), ("src", "<u8"), ("len", "<u8")], align=True)  # sec_copy
 
 
 class sec_msg(ctypes.Structure):
@@ -118,6 +119,7 @@ _SIGS = {
                                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "sec_memcpy": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_int]),
     "sec_memset": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_size_t]),
+    "sec_host_copy": (ctypes.c_int, [_vp, _vp, ctypes.c_int64]),
 }
 SYMBOLS = tuple(_SIGS)
 

@@ -2880,6 +2880,29 @@ int sec_memcpy(sec_ctx *ctx, void *dst, const void *src, size_t bytes, int kind)
     return SEC_OK;
 }
 
+// Host-to-host copies on the context's copy threads (the calling thread takes part): the join of
+// a reassembled chunk's rows into one output buffer -- present primaries straight from the
+// caller's piece objects, recovered rows from a result buffer -- without the caller's
+// single-threaded join (easyfec's b"".join, /root/reference/storb/util/piece.py:196-197).
+// src == 0: zero-fill.
+int sec_host_copy(sec_ctx *ctx, const sec_copy *jobs, int64_t njobs)
+{
+    if (!ctx || njobs < 0 || (njobs > 0 && !jobs))
+        return SEC_EINVAL;
+    std::vector<sec::CopyJob> cj;
+    cj.reserve((size_t)njobs);
+    for (int64_t i = 0; i < njobs; ++i) {
+        if (!jobs[i].len)
+            continue;
+        if (!jobs[i].dst)
+            return SEC_EINVAL;
+        cj.push_back(sec::CopyJob{(void *)(uintptr_t)jobs[i].dst, (const void *)(uintptr_t)jobs[i].src,
+                                  (size_t)jobs[i].len});
+    }
+    pool(ctx).run(cj);
+    return SEC_OK;
+}
+
 int sec_memset(sec_ctx *ctx, void *dptr, int value, size_t bytes)
 {
     if (!ctx || (bytes && !dptr))

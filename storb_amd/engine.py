@@ -23,7 +23,7 @@ import weakref
 import numpy as np
 
 from . import _lib
-from ._lib import DEC_DTYPE, ENC_DTYPE, MSG_DTYPE, SEC_F_ASYNC, SEC_F_HOST, SEC_F_RECOVER, SEC_F_STAGED
+from ._lib import COPY_DTYPE, DEC_DTYPE, ENC_DTYPE, MSG_DTYPE, SEC_F_ASYNC, SEC_F_HOST, SEC_F_RECOVER, SEC_F_STAGED
 
 
 class Error(Exception):
@@ -365,39 +365,66 @@ class Engine:
         digs = [[bytes(dv[20 * (f + j):20 * (f + j + 1)]) for j in range(m)] for f, m in zip(first, ms)]
         return par, digs
 
+    # joins of at least this many bytes go to the library's copy threads (sec_host_copy) instead
+    # of a single-threaded b"".join under the GIL
+    NATIVE_JOIN_MIN = 1 << 20
+
+    def _join_into(self, views, base: int) -> int:
+        """Copy `views` back to back to the host address `base` on the copy threads; returns the
+        bytes written."""
+        jobs = np.zeros(len(views), dtype=COPY_DTYPE)
+        off = 0
+        keep = []
+        for i, v in enumerate(views):
+            a = np.frombuffer(v, dtype=np.uint8)
+            keep.append(a)
+            n = a.size
+            jobs[i] = (base + off, a.ctypes.data if n else 0, n)
+            off += n
+        if len(views):
+            self._check(self.lib.sec_host_copy(self._ctx, _ptr(jobs), len(views)))
+        return off
+
+    def _joined(self, views) -> bytes:
+        from ._hostbytes import _finalize, _new_bytes
+
+        total = sum(len(v) for v in views)
+        if total < self.NATIVE_JOIN_MIN:
+            return b"".join(views)
+        b, dst = _new_bytes(total)
+        self._join_into(views, dst.ctypes.data)
+        return _finalize(b)
+
     def decode_host(self, items) -> bytes:
         """Reassemble chunks from host blocks, concatenated in order.
 
         items: [(k, m, blocks, sharenums, padlen)] with exactly k equal-length blocks each.
         Returns the concatenation of every chunk's k*B - padlen bytes.
         """
-        return b"".join(self._decode_parts(items, per_chunk=False))
+        return self._joined(self._decode_parts(items, per_chunk=False))
 
     def decode_host_into(self, items, dst: np.ndarray) -> int:
         """``decode_host`` written into `dst` (a writable uint8 array) instead of a new bytes
         object: the output of a share of a multi-device call lands straight in the caller's
         result.  Returns the bytes written; ValueError when `dst` is too small."""
-        off = 0
-        for v in self._decode_parts(items, per_chunk=False):
-            n = len(v)
-            if off + n > dst.size:
-                raise ValueError("decode_host_into: destination too small")
-            dst[off:off + n] = np.frombuffer(v, dtype=np.uint8)
-            off += n
-        return off
+        views = self._decode_parts(items, per_chunk=False)
+        if sum(len(v) for v in views) > dst.size:
+            raise ValueError("decode_host_into: destination too small")
+        return self._join_into(views, dst.ctypes.data) if dst.size else 0
 
     def decode_host_chunks(self, items) -> list[bytes]:
         """``decode_host``, one bytes object per chunk."""
-        return self._decode_parts(items, per_chunk=True)
+        return [self._joined(p) for p in self._decode_parts(items, per_chunk=True, views=True)]
 
-    def _decode_parts(self, items, per_chunk: bool) -> list:
+    def _decode_parts(self, items, per_chunk: bool, views: bool = False) -> list:
         """Chunks with a missing primary go to the GPU in ONE sec_decode_batch_ex call (recover-only);
         a chunk whose k blocks are its k primaries needs no field arithmetic at all (zfec's fec_decode writes
         nothing for present primaries and easyfec joins them, /root/reference/storb/util/
         piece.py:196-197), so it is the join of its blocks, taken as views with no staging or
-        PCIe round trip.  Returns per chunk either that chunk's bytes (per_chunk) or a list of
-        buffers whose concatenation is the output."""
+        PCIe round trip.  Returns per chunk either that chunk's bytes (per_chunk; with `views`
+        the list of its buffers instead) or a list of buffers whose concatenation is the output."""
         n = len(items)
+        as_views = views
         gpu = []  # indices of chunks with a missing primary
         for i, item in enumerate(items):
             check_decode_item(*item)
@@ -451,7 +478,7 @@ class Engine:
                 views.append(v[:left] if left < B else v)
                 left -= B
             if per_chunk:
-                parts.append(b"".join(views))
+                parts.append(views if as_views else b"".join(views))
             else:
                 parts.extend(views)
         return parts

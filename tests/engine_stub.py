@@ -76,3 +76,12 @@ class OracleHostEngine(Engine):
                 if digests is not None:
                     digests[20 * j:20 * (j + 1)] = np.frombuffer(hashlib.sha1(b).digest(), np.uint8)
                 j += 1
+
+    def _join_into(self, views, base):
+        """sec_host_copy on the host: the views back to back at `base`."""
+        off = 0
+        for v in views:
+            b = bytes(v)
+            ctypes.memmove(base + off, b, len(b))
+            off += len(b)
+        return off

@@ -118,3 +118,34 @@ def test_pieces_bytes_are_immutable_objects():
         assert type(p.data) is bytes
     raw = ctypes.string_at(id(ec.pieces[0].data) + bytes.__basicsize__ - 1, 4) if piece._FILL_IN_PLACE else None
     assert raw is None or raw == ec.pieces[0].data[:4]
+
+
+def test_native_join_decode_host():
+    """Reassembled chunks of >= Engine.NATIVE_JOIN_MIN bytes are joined on the library's copy
+    threads (sec_host_copy): every data piece present (no GPU work) and with pieces lost, per
+    chunk and concatenated, against the source bytes."""
+    from storb_amd._lib import COPY_DTYPE
+
+    eng = get_engine()
+    rng = random.Random(9)
+    items, want = [], []
+    for n in (3 << 20, (1 << 20) + 7, 5000, 8 << 20):
+        data = rng.randbytes(n)
+        k, m, B, padlen = piece.chunk_shape(n)
+        blocks = cfec.easy_encode(data, k, m)
+        for lost in ((), (0,), tuple(range(min(m - k, k)))):
+            keep = [j for j in range(m) if j not in lost][:k]
+            items.append((k, m, [blocks[j] for j in keep], keep, padlen))
+            want.append(data)
+    assert eng.decode_host_chunks(items) == want
+    assert eng.decode_host(items) == b"".join(want)
+    dst = np.zeros(sum(map(len, want)), np.uint8)
+    assert eng.decode_host_into(items, dst) == dst.size and dst.tobytes() == b"".join(want)
+    # zero-fill and a NULL destination
+    buf = np.full(64, 7, np.uint8)
+    jobs = np.zeros(1, dtype=COPY_DTYPE)
+    jobs[0] = (buf.ctypes.data + 8, 0, 16)
+    assert eng.lib.sec_host_copy(eng._ctx, jobs.ctypes.data, 1) == 0
+    assert buf[8:24].sum() == 0 and buf[:8].tolist() == [7] * 8 and buf[24:].tolist() == [7] * 40
+    jobs[0] = (0, buf.ctypes.data, 16)
+    assert eng.lib.sec_host_copy(eng._ctx, jobs.ctypes.data, 1) != 0

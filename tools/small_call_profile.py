@@ -65,6 +65,9 @@ def main():
             piece.HOST_PIECES = hp
             sfx = "" if hp else "_round4"
             r["encode_chunk" + sfx] = med_us(lambda: piece.encode_chunk(chunk, 0), a.reps)
+            # a fresh piece-id memo: the loop above took no ids, so the memo would have paused
+            # prefetching (its idle rule) and most of the next loop would hash serially
+            piece._memo = piece._PieceIdMemo()
             r["encode_chunk_plus_ids" + sfx] = med_us(
                 lambda: [piece.piece_hash(p.data) for p in piece.encode_chunk(chunk, 0).pieces], a.reps)
         piece.HOST_PIECES = True

@@ -31,7 +31,8 @@ VARIANTS = {
     "dst0": {"SEC_DEC_ST": 0},
     "est2": {"SEC_ENC_ST": 2},
     "est3": {"SEC_ENC_ST": 3},
-    "nogf": {"SEC_PROBE_NOGF": 1},  # calibration: the product kernels' traffic with no GF arithmetic
+    "nogf": {"SEC_PROBE_NOGF": 1},
+    "pipe": {"SEC_SOLVE_PIPE": 1},  # (archived: tools/archive/kernels_bs_r05_solve_pipe.diff)  # calibration: the product kernels' traffic with no GF arithmetic
     "est0": {"SEC_ENC_ST": 0},
     "est2dst2": {"SEC_ENC_ST": 2, "SEC_DEC_ST": 2},
     "dst3": {"SEC_DEC_ST": 3},
