@@ -2593,9 +2593,26 @@ int sec_decode_batch(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks,
     return sec_decode_batch_ex(ctx, chunks, nchunks, sharenums, block_offs, nullptr, blocks, out, flags);
 }
 
+namespace {
+constexpr uint64_t kJoinPiece = (uint64_t)1 << 20;  // host-join copies per task
+int decode_core(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const int32_t *sharenums,
+                const uint64_t *block_offs, const uint64_t *block_avail, const uint8_t *blocks, uint8_t *out,
+                unsigned flags, bool rows_only);
+}  // namespace
+
 int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const int32_t *sharenums,
                         const uint64_t *block_offs, const uint64_t *block_avail, const uint8_t *blocks, uint8_t *out,
                         unsigned flags)
+{
+    return decode_core(ctx, chunks, nchunks, sharenums, block_offs, block_avail, blocks, out, flags, false);
+}
+
+namespace {
+// rows_only (a host reassembly whose present primaries the caller copies itself, see below):
+// run the kernels for the recovered rows only, written to their output rows.
+int decode_core(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const int32_t *sharenums,
+                const uint64_t *block_offs, const uint64_t *block_avail, const uint8_t *blocks, uint8_t *out,
+                unsigned flags, bool rows_only)
 {
     if (!ctx || nchunks < 0 || (nchunks > 0 && (!chunks || !sharenums || !block_offs)) ||
         (flags & ~(SEC_F_HOST | SEC_F_ASYNC | SEC_F_RECOVER | SEC_F_STAGED)) ||
@@ -2625,13 +2642,77 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
     }
     if (total_out == 0)
         return SEC_OK;
-    if (!out)  // blocks may be NULL: block_offs are then absolute addresses
-        return SEC_EINVAL;
-    // A reassembly of host buffers leaves the present primaries to the host (the copy pool, from
-    // the caller's blocks into `out`) and moves only what the GPU computes over PCIe: the
-    // recovered rows, e * B per chunk instead of the whole chunk (option SEC_HOST_JOIN = 0: the
-    // GPU writes every output byte, the A/B).
+    // (blocks and out may be NULL: block_offs / out_off are then absolute addresses)
+    // A reassembly of host buffers leaves the present primaries to the host (the context's task
+    // threads copy them from the caller's blocks into `out`) and moves only what the GPU computes
+    // over PCIe: the recovered rows, e * B per chunk instead of the whole chunk (option
+    // SEC_HOST_JOIN = 0: the GPU writes every output byte).  Chunks with every primary present
+    // never reach the GPU.
     const bool join = host && !recover && ctx->opt[O_HOST_JOIN] != 0;
+    if (join && !rows_only) {
+        sec::TaskPool &tp = tasks(ctx);
+        sec::TaskPool::Group g;
+        std::vector<sec_dec_chunk> sub;  // the chunks with a lost primary
+        for (int64_t i = 0; i < nchunks; ++i) {
+            const sec_dec_chunk &c = chunks[i];
+            const uint64_t n = (uint64_t)c.k * c.B - c.padlen;
+            bool lost = false;
+            for (int j = 0; j < c.k; ++j)
+                lost |= sharenums[c.slot0 + j] >= c.k;
+            if (lost)
+                sub.push_back(c);
+            for (int q = 0; q < c.k; ++q) {
+                const int j = sharenums[c.slot0 + q];
+                if (j >= c.k || (uint64_t)j * c.B >= n)
+                    continue;
+                const uint64_t row = std::min<uint64_t>(c.B, n - (uint64_t)j * c.B);
+                const uint64_t av = std::min<uint64_t>(row, slot_avail(c, block_avail, q));
+                uint8_t *dst = (uint8_t *)((uintptr_t)out + c.out_off + (uint64_t)j * c.B);
+                const uint8_t *src = (const uint8_t *)((uintptr_t)blocks + block_offs[c.slot0 + q]);
+                for (uint64_t o = 0; o < row; o += kJoinPiece) {  // 1 MiB pieces over the threads
+                    const uint64_t len = std::min<uint64_t>(kJoinPiece, row - o);
+                    const uint64_t cp = o < av ? std::min<uint64_t>(len, av - o) : 0;
+                    tp.submit(g, [=] {
+                        if (cp)
+                            memcpy(dst + o, src + o, cp);
+                        if (cp < len)
+                            memset(dst + o + cp, 0, len - cp);
+                        return true;
+                    });
+                }
+            }
+        }
+        tp.wait(g);  // the present primaries are in `out` now
+        if (sub.empty())
+            return SEC_OK;
+        // The chunks with a lost primary then read their present primaries back from `out` (one
+        // contiguous range per chunk, which a large call page-locks and the kernels read over
+        // PCIe in place) instead of from the scattered piece objects (each staged), and write the
+        // recovered rows into `out` beside them (tools/stream_rate.py: 8 MiB chunks, one data
+        // piece lost, r05_stream_rate.json).  Slots keep their indices; offsets become absolute.
+        uint64_t nsl = 0;
+        for (const sec_dec_chunk &c : sub)
+            nsl = std::max<uint64_t>(nsl, c.slot0 + (uint64_t)c.k);
+        std::vector<uint64_t> offs2(nsl, 0), avail2(nsl, 0);
+        for (const sec_dec_chunk &c : sub) {
+            const uint64_t n = (uint64_t)c.k * c.B - c.padlen;  // (padlen <= k*B: checked above)
+            for (int q = 0; q < c.k; ++q) {
+                const uint64_t s = c.slot0 + (uint64_t)q;
+                const int j = sharenums[s];
+                // only a row `out` holds whole: a row cut by padlen keeps its own block, whose
+                // bytes past the cut are not necessarily zero (any padlen <= k*B is legal)
+                if (j < c.k && (uint64_t)(j + 1) * c.B <= n) {
+                    offs2[s] = (uintptr_t)out + c.out_off + (uint64_t)j * c.B;
+                    avail2[s] = c.B;
+                } else {
+                    offs2[s] = (uintptr_t)blocks + block_offs[s];
+                    avail2[s] = slot_avail(c, block_avail, q);
+                }
+            }
+        }
+        return decode_core(ctx, sub.data(), (int64_t)sub.size(), sharenums, offs2.data(), avail2.data(), nullptr,
+                           out, flags, true);
+    }
     // pinned (or lockable) caller buffers: the device path on them directly (see encode_impl)
     HostLock lock(ctx->stream());
     bool direct = false;
@@ -2645,7 +2726,7 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
     // the primaries a joining call copies on the host: row j of chunk i from the slot holding
     // primary j, up to that slot's avail (zero past it), rows clipped to the chunk's n bytes
     std::vector<sec::CopyJob> joins;
-    if (join) {
+    if (join && !rows_only) {
         for (int64_t i = 0; i < nchunks; ++i) {
             const sec_dec_chunk &c = chunks[i];
             const uint64_t n = (uint64_t)c.k * c.B - c.padlen;
@@ -2775,6 +2856,7 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
         pool(ctx).run(joins);
     return SEC_OK;
 }
+}  // namespace
 
 // ---------------------------------------------------------------------------
 int sec_malloc(sec_ctx *ctx, size_t bytes, void **dptr)

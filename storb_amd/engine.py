@@ -395,26 +395,83 @@ class Engine:
         self._join_into(views, dst.ctypes.data)
         return _finalize(b)
 
+    # A host reassembly in ONE library call (sec_decode_batch_ex's host join: the present pieces
+    # copied into the output by the library's task threads, then the GPU recovers the missing
+    # rows reading them back from there; chunks with every data piece present never reach the GPU).  False: round 4's form
+    # (recover-only call into a pinned scratch, then the join, A/B: tools/stream_rate.py --ab-join).
+    LIBRARY_JOIN = True
+
+    def _reassemble(self, items, outs) -> None:
+        """Every chunk's k*B - padlen bytes written to the host address outs[i], one call."""
+        for it in items:
+            check_decode_item(*it)
+        n = len(items)
+        descs = np.zeros(n, dtype=DEC_DTYPE)
+        nslots = sum(it[0] for it in items)
+        sn = np.zeros(max(nslots, 1), dtype=np.int32)
+        bo = np.zeros(max(nslots, 1), dtype=np.uint64)
+        keep = []
+        slot = 0
+        for j, (k, m, blocks, sharenums, padlen) in enumerate(items):
+            B = len(blocks[0])
+            for q, b in enumerate(blocks):
+                a, kp = addr(b)
+                keep.append(kp)
+                bo[slot + q] = a
+                sn[slot + q] = int(sharenums[q])
+            descs[j] = (int(outs[j]), B, padlen, slot, k, m)
+            slot += k
+        if n:
+            # (not staged: the library copies the present pieces first, then a large call's
+            # kernels read them back from the output in place, page-locked for the call)
+            self.decode_batch(descs, sn, bo, 0, 0, host=True)
+
     def decode_host(self, items) -> bytes:
         """Reassemble chunks from host blocks, concatenated in order.
 
         items: [(k, m, blocks, sharenums, padlen)] with exactly k equal-length blocks each.
         Returns the concatenation of every chunk's k*B - padlen bytes.
         """
-        return self._joined(self._decode_parts(items, per_chunk=False))
+        if not self.LIBRARY_JOIN:
+            return self._joined(self._decode_parts(items, per_chunk=False))
+        from ._hostbytes import _finalize, _new_bytes
+
+        lens = [it[0] * len(it[2][0]) - it[4] for it in items]
+        b, dst = _new_bytes(sum(lens))
+        if dst.size:
+            starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64) if lens else []
+            self._reassemble(items, [dst.ctypes.data + int(o) for o in starts])
+        return _finalize(b)
 
     def decode_host_into(self, items, dst: np.ndarray) -> int:
         """``decode_host`` written into `dst` (a writable uint8 array) instead of a new bytes
         object: the output of a share of a multi-device call lands straight in the caller's
         result.  Returns the bytes written; ValueError when `dst` is too small."""
-        views = self._decode_parts(items, per_chunk=False)
-        if sum(len(v) for v in views) > dst.size:
+        if not self.LIBRARY_JOIN:
+            views = self._decode_parts(items, per_chunk=False)
+            if sum(len(v) for v in views) > dst.size:
+                raise ValueError("decode_host_into: destination too small")
+            return self._join_into(views, dst.ctypes.data) if dst.size else 0
+        lens = [it[0] * len(it[2][0]) - it[4] for it in items]
+        total = sum(lens)
+        if total > dst.size:
             raise ValueError("decode_host_into: destination too small")
-        return self._join_into(views, dst.ctypes.data) if dst.size else 0
+        if total:
+            starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+            self._reassemble(items, [dst.ctypes.data + int(o) for o in starts])
+        return total
 
     def decode_host_chunks(self, items) -> list[bytes]:
         """``decode_host``, one bytes object per chunk."""
-        return [self._joined(p) for p in self._decode_parts(items, per_chunk=True, views=True)]
+        if not self.LIBRARY_JOIN:
+            return [self._joined(p) for p in self._decode_parts(items, per_chunk=True, views=True)]
+        from ._hostbytes import _finalize, _new_bytes
+
+        objs = [_new_bytes(it[0] * len(it[2][0]) - it[4]) for it in items]
+        live = [(it, v.ctypes.data) for it, (_, v) in zip(items, objs) if v.size]
+        if live:
+            self._reassemble([it for it, _ in live], [a for _, a in live])
+        return [_finalize(b) for b, _ in objs]
 
     def _decode_parts(self, items, per_chunk: bool, views: bool = False) -> list:
         """Chunks with a missing primary go to the GPU in ONE sec_decode_batch_ex call (recover-only);

@@ -98,7 +98,11 @@ STREAM_WINDOW_BYTES = 64 << 20  # chunk bytes per GPU call in the *_stream pipel
 # The kernel is one lane per piece, so a window's hashing takes about one piece's chain
 # whatever the window size: 1 GiB object, 8 MiB chunks, zfec(16,24): 7.1 / 9.1 GiB/s with
 # 256 / 512 MiB windows against 3.2-5.3 hashing on the host (profiles/r02_stream_rate.json).
-GPU_PIECE_IDS = True
+# Round 5: the host ids from sec_encode_pieces (OpenSSL on the library's threads, HOST_PIECES)
+# beat them at every window: 8.1-8.3 GiB/s at 64-256 MiB against 4.6-7.1 for GPU ids
+# (profiles/r05_stream_rate.json), at the 64 MiB window (lower latency to the first chunk), so
+# the GPU ids are off by default.
+GPU_PIECE_IDS = False
 STREAM_WINDOW_IDS_BYTES = 256 << 20
 STREAM_WORKERS = 4  # single-thread workers (one engine each) the *_stream pipelines are spread over
 

@@ -149,3 +149,31 @@ def test_native_join_decode_host():
     assert buf[8:24].sum() == 0 and buf[:8].tolist() == [7] * 8 and buf[24:].tolist() == [7] * 40
     jobs[0] = (0, buf.ctypes.data, 16)
     assert eng.lib.sec_host_copy(eng._ctx, jobs.ctypes.data, 1) != 0
+
+
+@pytest.mark.parametrize("library_join", [True, False])
+def test_reassembly_paths_agree(library_join, monkeypatch):
+    """decode_host / _chunks / _into with the library's one-call reassembly (sec_decode_batch_ex's
+    host join: present pieces copied by the task threads, the GPU on the chunks with a lost data
+    piece only) and with round 4's recover-then-join form: same bytes, small and large chunks,
+    padded last blocks, nothing / one / every possible primary lost, mixed shapes in one call."""
+    from storb_amd.engine import Engine
+
+    monkeypatch.setattr(Engine, "LIBRARY_JOIN", library_join)
+    eng = get_engine()
+    rng = random.Random(31)
+    items, want = [], []
+    for n in (1, 100, 70_000, (1 << 20) + 3, 3 << 20, (8 << 20) - 1):
+        data = rng.randbytes(n)
+        k, m, B, padlen = piece.chunk_shape(n)
+        blocks = cfec.easy_encode(data, k, m)
+        for lost in ((), (k - 1,), tuple(range(min(m - k, k)))):
+            keep = [j for j in range(m) if j not in lost][:k]
+            rng.shuffle(keep)
+            items.append((k, m, [blocks[j] for j in keep], keep, padlen))
+            want.append(data)
+    assert eng.decode_host_chunks(items) == want
+    assert eng.decode_host(items) == b"".join(want)
+    dst = np.zeros(sum(map(len, want)) + 5, np.uint8)
+    assert eng.decode_host_into(items, dst) == dst.size - 5
+    assert dst[:-5].tobytes() == b"".join(want)

@@ -118,9 +118,15 @@ def main():
                 n += len(b)
             assert n == len(data)
 
-        assert b"".join(piece.reconstruct_data_stream(pieces, chunks)) == data
-        res[f"download_per_chunk_{label}"] = round(len(data) / best(down_per_chunk, a.reps) / GIB, 3)
-        res[f"download_stream_{label}"] = round(len(data) / best(down_stream, a.reps) / GIB, 3)
+        from storb_amd.engine import Engine
+
+        for lj in (True, False):  # A/B: the library's one-call reassembly vs round 4's recover + join
+            Engine.LIBRARY_JOIN = lj
+            sfx = "" if lj else "_round4_join"
+            assert b"".join(piece.reconstruct_data_stream(pieces, chunks)) == data
+            res[f"download_per_chunk_{label}{sfx}"] = round(len(data) / best(down_per_chunk, a.reps) / GIB, 3)
+            res[f"download_stream_{label}{sfx}"] = round(len(data) / best(down_stream, a.reps) / GIB, 3)
+        Engine.LIBRARY_JOIN = True
     print(json.dumps(res, indent=1))
 
 
