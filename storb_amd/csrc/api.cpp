@@ -2647,9 +2647,17 @@ int decode_core(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
     // threads copy them from the caller's blocks into `out`) and moves only what the GPU computes
     // over PCIe: the recovered rows, e * B per chunk instead of the whole chunk (option
     // SEC_HOST_JOIN = 0: the GPU writes every output byte).  Chunks with every primary present
-    // never reach the GPU.
+    // never reach the GPU.  Buffers all in persistently pinned memory take the direct path below
+    // instead (kernels on them in place, the present rows copied while the kernels run).
     const bool join = host && !recover && ctx->opt[O_HOST_JOIN] != 0;
+    bool all_pinned = false;
     if (join && !rows_only) {
+        HostLock probe(ctx->stream());  // (may_lock false: locks nothing)
+        all_pinned =
+            probe.acquire(decode_ranges(chunks, nchunks, sharenums, block_offs, block_avail, blocks, out, recover), 0,
+                          false) == 1;
+    }
+    if (join && !rows_only && !all_pinned) {
         sec::TaskPool &tp = tasks(ctx);
         sec::TaskPool::Group g;
         std::vector<sec_dec_chunk> sub;  // the chunks with a lost primary

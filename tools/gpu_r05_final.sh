@@ -1,15 +1,7 @@
 #!/bin/bash
-# Round 5 evidence: tools/gpu_round.sh (GPU tests, smoke, PMC c2/c4/c5 on this build, bench lines,
-# kernel stats, --gpus 2 rehearsal with the nested in-process form, every BASELINE config), then
-# the in-process form on two contexts of the one GPU, the wide-decode A/B of the final build, the
-# per-call profile and the C1 loopback.
+# Round 5 evidence, part 1: tools/gpu_round.sh without the configs sweep (GPU tests, smoke, PMC
+# c2/c4/c5 on this build, bench lines, kernel stats, --gpus 2 rehearsal with the nested
+# in-process form).  Part 2: tools/gpu_r05_final2.sh.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
-bash tools/gpu_round.sh || exit 1
-echo "== in-process 0,0" && timeout -k 10 300 python3 -u bench.py --gpus 2 --in-process --inproc-devices 0,0 --steps 20 --warmup 3 --c5-steps 5 > $O/inproc00.log 2>&1 || { tail -30 $O/inproc00.log; exit 1; }
-grep '^{' $O/inproc00.log
-echo "== syn A/B" && timeout -k 10 600 python3 -u tools/syn_ab.py --rounds 3 --variants "auto,direct@SEC_SYN=0" --cases "32 lost;24 lost (random;30 %;16 lost (random;20 %;rows 64..73" > $O/syn_ab_final.jsonl 2> $O/syn_ab_final.err || { tail -20 $O/syn_ab_final.err; exit 1; }
-cat $O/syn_ab_final.jsonl
-echo "== small calls" && timeout -k 10 300 python3 -u tools/small_call_profile.py --reps 100 > $O/small_calls.json 2> $O/small_calls.err || { tail -20 $O/small_calls.err; exit 1; }
-echo "== c1" && timeout -k 10 300 python3 -u tools/c1_loopback.py --reps 20 > $O/c1.json 2> $O/c1.err || { tail -20 $O/c1.err; exit 1; }
-cat $O/c1.json
+SKIP_CONFIGS=1 bash tools/gpu_round.sh || exit 1
