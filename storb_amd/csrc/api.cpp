@@ -1973,8 +1973,9 @@ public:
     HostLock &operator=(const HostLock &) = delete;
 
     // 0: staged; 1: every range in persistently pinned memory (zero-copy, nothing locked);
-    // 2: zero-copy on pages this call locked (plus persistently pinned ones)
-    int acquire(const std::vector<HostRange> &rs, int64_t register_min, bool may_lock = true)
+    // 2: zero-copy on pages this call locked (plus persistently pinned ones).  dry: lock
+    // nothing, 2 = the ranges pass the size rules (a lock would be tried)
+    int acquire(const std::vector<HostRange> &rs, int64_t register_min, bool may_lock = true, bool dry = false)
     {
         TransientLocks &tl = transient_locks();
         std::lock_guard<std::mutex> g(tl.mu);
@@ -2006,6 +2007,8 @@ public:
                     merged.push_back(q);
             if (merged.size() * ((uint64_t)1 << 20) > total)
                 return 0;
+            if (dry)
+                return 2;
             bool ok = true;
             for (auto &q : merged) {
                 if (tl.touches(q.first, q.second - q.first) ||
@@ -2608,6 +2611,98 @@ int sec_decode_batch_ex(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchun
 }
 
 namespace {
+bool primary_lost(const sec_dec_chunk &c, const int32_t *sharenums)
+{
+    for (int j = 0; j < c.k; ++j)
+        if (sharenums[c.slot0 + j] >= c.k)
+            return true;
+    return false;
+}
+
+// The present primaries of chunk c, from the caller's blocks to their rows in `out` (rows
+// clipped to the chunk's n bytes, zero past a slot's avail), as 1 MiB tasks on the pool.
+void submit_row_copies(sec::TaskPool &tp, sec::TaskPool::Group &g, const sec_dec_chunk &c, const int32_t *sharenums,
+                       const uint64_t *block_offs, const uint64_t *block_avail, const uint8_t *blocks, uint8_t *out)
+{
+    const uint64_t n = (uint64_t)c.k * c.B - c.padlen;
+    for (int q = 0; q < c.k; ++q) {
+        const int j = sharenums[c.slot0 + q];
+        if (j >= c.k || (uint64_t)j * c.B >= n)
+            continue;
+        const uint64_t row = std::min<uint64_t>(c.B, n - (uint64_t)j * c.B);
+        const uint64_t av = std::min<uint64_t>(row, slot_avail(c, block_avail, q));
+        uint8_t *dst = (uint8_t *)((uintptr_t)out + c.out_off + (uint64_t)j * c.B);
+        const uint8_t *src = (const uint8_t *)((uintptr_t)blocks + block_offs[c.slot0 + q]);
+        for (uint64_t o = 0; o < row; o += kJoinPiece) {
+            const uint64_t len = std::min<uint64_t>(kJoinPiece, row - o);
+            const uint64_t cp = o < av ? std::min<uint64_t>(len, av - o) : 0;
+            tp.submit(g, [=] {
+                if (cp)
+                    memcpy(dst + o, src + o, cp);
+                if (cp < len)
+                    memset(dst + o + cp, 0, len - cp);
+                return true;
+            });
+        }
+    }
+}
+
+// A staged reassembly of host buffers (decode_core found them neither pinned nor lockable: e.g.
+// one piece object per block), every chunk with a lost primary.  The present primaries go from
+// the caller's blocks into `out` on the context's task threads, and a rows-only call computes
+// the lost ones, reading the present primaries either
+//  - back from `out`, once the copies are done, when those ranges would be page-locked (one
+//    contiguous range per chunk in place of scattered pieces, read over PCIe in place), or
+//  - from the caller's blocks, staged, while the copies run.
+// Slots keep their indices; re-pointed offsets are absolute.
+int join_staged(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const int32_t *sharenums,
+                const uint64_t *block_offs, const uint64_t *block_avail, const uint8_t *blocks, uint8_t *out,
+                unsigned flags)
+{
+    sec::TaskPool &tp = tasks(ctx);
+    sec::TaskPool::Group g;
+    std::vector<sec_dec_chunk> sub(chunks, chunks + nchunks);
+    for (const sec_dec_chunk &c : sub)
+        submit_row_copies(tp, g, c, sharenums, block_offs, block_avail, blocks, out);
+    --ctx->staged_calls;  // the rows-only call counts this call's host path
+    uint64_t nsl = 0;
+    for (const sec_dec_chunk &c : sub)
+        nsl = std::max<uint64_t>(nsl, c.slot0 + (uint64_t)c.k);
+    std::vector<uint64_t> offs2(nsl, 0), avail2(nsl, 0);
+    for (const sec_dec_chunk &c : sub) {
+        const uint64_t n = (uint64_t)c.k * c.B - c.padlen;  // (padlen <= k*B: checked)
+        for (int q = 0; q < c.k; ++q) {
+            const uint64_t s = c.slot0 + (uint64_t)q;
+            const int j = sharenums[s];
+            // only a row `out` holds whole: a row cut by padlen keeps its own block, whose bytes
+            // past the cut are not necessarily zero (any padlen <= k*B is legal)
+            if (j < c.k && (uint64_t)(j + 1) * c.B <= n) {
+                offs2[s] = (uintptr_t)out + c.out_off + (uint64_t)j * c.B;
+                avail2[s] = c.B;
+            } else {
+                offs2[s] = (uintptr_t)blocks + block_offs[s];
+                avail2[s] = slot_avail(c, block_avail, q);
+            }
+        }
+    }
+    HostLock probe(ctx->stream());
+    const bool from_out =
+        probe.acquire(decode_ranges(sub.data(), (int64_t)sub.size(), sharenums, offs2.data(), avail2.data(), nullptr,
+                                    out, false),
+                      ctx->opt[O_REGISTER_MIN], !(flags & SEC_F_STAGED), true) != 0;
+    int rc;
+    if (from_out) {
+        tp.wait(g);  // the present primaries are in `out` now
+        rc = decode_core(ctx, sub.data(), (int64_t)sub.size(), sharenums, offs2.data(), avail2.data(), nullptr, out,
+                         flags, true);
+    } else {
+        rc = decode_core(ctx, sub.data(), (int64_t)sub.size(), sharenums, block_offs, block_avail, blocks, out, flags,
+                         true);
+        tp.wait(g);
+    }
+    return rc;
+}
+
 // rows_only (a host reassembly whose present primaries the caller copies itself, see below):
 // run the kernels for the recovered rows only, written to their output rows.
 int decode_core(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, const int32_t *sharenums,
@@ -2647,79 +2742,29 @@ int decode_core(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
     // threads copy them from the caller's blocks into `out`) and moves only what the GPU computes
     // over PCIe: the recovered rows, e * B per chunk instead of the whole chunk (option
     // SEC_HOST_JOIN = 0: the GPU writes every output byte).  Chunks with every primary present
-    // never reach the GPU.  Buffers all in persistently pinned memory take the direct path below
-    // instead (kernels on them in place, the present rows copied while the kernels run).
+    // never reach the GPU.  Buffers the device can use in place (pinned, or pageable and
+    // locked for the call) keep the concurrent form below instead: the kernels write the
+    // recovered rows in place while the copy threads join the present rows.
     const bool join = host && !recover && ctx->opt[O_HOST_JOIN] != 0;
-    bool all_pinned = false;
     if (join && !rows_only) {
-        HostLock probe(ctx->stream());  // (may_lock false: locks nothing)
-        all_pinned =
-            probe.acquire(decode_ranges(chunks, nchunks, sharenums, block_offs, block_avail, blocks, out, recover), 0,
-                          false) == 1;
-    }
-    if (join && !rows_only && !all_pinned) {
-        sec::TaskPool &tp = tasks(ctx);
-        sec::TaskPool::Group g;
-        std::vector<sec_dec_chunk> sub;  // the chunks with a lost primary
-        for (int64_t i = 0; i < nchunks; ++i) {
-            const sec_dec_chunk &c = chunks[i];
-            const uint64_t n = (uint64_t)c.k * c.B - c.padlen;
-            bool lost = false;
-            for (int j = 0; j < c.k; ++j)
-                lost |= sharenums[c.slot0 + j] >= c.k;
-            if (lost)
-                sub.push_back(c);
-            for (int q = 0; q < c.k; ++q) {
-                const int j = sharenums[c.slot0 + q];
-                if (j >= c.k || (uint64_t)j * c.B >= n)
-                    continue;
-                const uint64_t row = std::min<uint64_t>(c.B, n - (uint64_t)j * c.B);
-                const uint64_t av = std::min<uint64_t>(row, slot_avail(c, block_avail, q));
-                uint8_t *dst = (uint8_t *)((uintptr_t)out + c.out_off + (uint64_t)j * c.B);
-                const uint8_t *src = (const uint8_t *)((uintptr_t)blocks + block_offs[c.slot0 + q]);
-                for (uint64_t o = 0; o < row; o += kJoinPiece) {  // 1 MiB pieces over the threads
-                    const uint64_t len = std::min<uint64_t>(kJoinPiece, row - o);
-                    const uint64_t cp = o < av ? std::min<uint64_t>(len, av - o) : 0;
-                    tp.submit(g, [=] {
-                        if (cp)
-                            memcpy(dst + o, src + o, cp);
-                        if (cp < len)
-                            memset(dst + o + cp, 0, len - cp);
-                        return true;
-                    });
-                }
-            }
+        // chunks with every primary present: copies on the task threads only (no GPU, and their
+        // buffers are not page-locked), the rest of the call running meanwhile
+        std::vector<sec_dec_chunk> sub;
+        for (int64_t i = 0; i < nchunks; ++i)
+            if (primary_lost(chunks[i], sharenums))
+                sub.push_back(chunks[i]);
+        if ((int64_t)sub.size() < nchunks) {
+            sec::TaskPool &tp = tasks(ctx);
+            sec::TaskPool::Group g;
+            for (int64_t i = 0; i < nchunks; ++i)
+                if (!primary_lost(chunks[i], sharenums))
+                    submit_row_copies(tp, g, chunks[i], sharenums, block_offs, block_avail, blocks, out);
+            const int rc = sub.empty() ? SEC_OK
+                                       : decode_core(ctx, sub.data(), (int64_t)sub.size(), sharenums, block_offs,
+                                                     block_avail, blocks, out, flags, false);
+            tp.wait(g);
+            return rc;
         }
-        tp.wait(g);  // the present primaries are in `out` now
-        if (sub.empty())
-            return SEC_OK;
-        // The chunks with a lost primary then read their present primaries back from `out` (one
-        // contiguous range per chunk, which a large call page-locks and the kernels read over
-        // PCIe in place) instead of from the scattered piece objects (each staged), and write the
-        // recovered rows into `out` beside them (tools/stream_rate.py: 8 MiB chunks, one data
-        // piece lost, r05_stream_rate.json).  Slots keep their indices; offsets become absolute.
-        uint64_t nsl = 0;
-        for (const sec_dec_chunk &c : sub)
-            nsl = std::max<uint64_t>(nsl, c.slot0 + (uint64_t)c.k);
-        std::vector<uint64_t> offs2(nsl, 0), avail2(nsl, 0);
-        for (const sec_dec_chunk &c : sub) {
-            const uint64_t n = (uint64_t)c.k * c.B - c.padlen;  // (padlen <= k*B: checked above)
-            for (int q = 0; q < c.k; ++q) {
-                const uint64_t s = c.slot0 + (uint64_t)q;
-                const int j = sharenums[s];
-                // only a row `out` holds whole: a row cut by padlen keeps its own block, whose
-                // bytes past the cut are not necessarily zero (any padlen <= k*B is legal)
-                if (j < c.k && (uint64_t)(j + 1) * c.B <= n) {
-                    offs2[s] = (uintptr_t)out + c.out_off + (uint64_t)j * c.B;
-                    avail2[s] = c.B;
-                } else {
-                    offs2[s] = (uintptr_t)blocks + block_offs[s];
-                    avail2[s] = slot_avail(c, block_avail, q);
-                }
-            }
-        }
-        return decode_core(ctx, sub.data(), (int64_t)sub.size(), sharenums, offs2.data(), avail2.data(), nullptr,
-                           out, flags, true);
     }
     // pinned (or lockable) caller buffers: the device path on them directly (see encode_impl)
     HostLock lock(ctx->stream());
@@ -2731,6 +2776,8 @@ int decode_core(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
         direct = true;
         flags &= ~(SEC_F_HOST | SEC_F_ASYNC);
     }
+    if (join && !rows_only && !direct)
+        return join_staged(ctx, chunks, nchunks, sharenums, block_offs, block_avail, blocks, out, flags);
     // the primaries a joining call copies on the host: row j of chunk i from the slot holding
     // primary j, up to that slot's avail (zero past it), rows clipped to the chunk's n bytes
     std::vector<sec::CopyJob> joins;
