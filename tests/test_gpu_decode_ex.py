@@ -401,6 +401,52 @@ def test_fuzz_host_reassembly_join(mode):
         eng.close()
 
 
+@pytest.mark.parametrize("staged_flag", [False, True])
+def test_scattered_blocks_read_back_from_out(staged_flag):
+    """A host reassembly whose blocks are too scattered to page-lock (256 KiB blocks 5 MiB apart:
+    the library stages them) but whose output is one large range (api.cpp join_staged): the
+    present primaries are copied into `out` first and the rows-only call reads them from there
+    with `out` locked (host path counts: one locked call, nothing staged).  With staged=True
+    nothing may be locked: the rows-only call stages the caller's blocks while the copies run.
+    Chunks with every primary present, one lost, and block k-1 lost or short in place."""
+    from storb_amd.engine import Engine
+
+    eng = Engine(0)
+    try:
+        rng = random.Random(5)
+        k, m, B, gap = 8, 12, 256 << 10, 5 << 20
+        nch = 6
+        sizes = [k * B - rng.randrange(0, 3) for _ in range(nch)]
+        arena = np.empty(nch * k * gap + B, np.uint8)  # untouched pages cost nothing
+        src = [rng.randbytes(n) for n in sizes]
+        place = iter(range(0, arena.size - B + 1, gap))
+        dd = np.zeros(nch, dtype=DEC_DTYPE)
+        sn = np.zeros(nch * k, np.int32)
+        offs = np.zeros(nch * k, np.uint64)
+        avail = np.zeros(nch * k, np.uint64)
+        lost_sets = [(), (3,), (k - 1,), (0, 5), (), (2, k - 1)]
+        for i, (n, data) in enumerate(zip(sizes, src)):
+            blocks = cfec.easy_encode(data, k, m)
+            dd["out_off"][i], dd["B"][i], dd["padlen"][i] = i * k * B, B, k * B - n
+            dd["k"][i], dd["m"][i], dd["slot0"][i] = k, m, i * k
+            keep = [j for j in range(m) if j not in lost_sets[i]][:k]
+            rng.shuffle(keep)
+            for q, j in enumerate(keep):
+                o = next(place)
+                av = n - (k - 1) * B if j == k - 1 else B  # block k-1 short in place
+                arena[o:o + av] = np.frombuffer(blocks[j][:av], np.uint8)
+                sn[i * k + q], offs[i * k + q], avail[i * k + q] = j, arena.ctypes.data + o, av
+        out = np.full(nch * k * B, 0xA5, np.uint8)
+        z0, r0, s0 = eng.host_paths()
+        eng.decode_batch(dd, sn, offs, 0, out, block_avail=avail, host=True, staged=staged_flag)
+        z1, r1, s1 = eng.host_paths()
+        for i, (n, data) in enumerate(zip(sizes, src)):
+            assert out[i * k * B:i * k * B + n].tobytes() == data, i
+        assert (z1 - z0, r1 - r0, s1 - s0) == ((0, 0, 1) if staged_flag else (0, 1, 0))
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("opts", [{}, {"SEC_HOST_JOIN": 0}])
 def test_small_chunks_reassembled(opts):
     """Chunks of at most 64 KiB with B <= 8192 and e <= 8 (the shapes round 4's LDS reassembly
