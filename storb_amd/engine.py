@@ -395,10 +395,11 @@ class Engine:
         self._join_into(views, dst.ctypes.data)
         return _finalize(b)
 
-    # A host reassembly in ONE library call (sec_decode_batch_ex's host join: the present pieces
-    # copied into the output by the library's task threads, then the GPU recovers the missing
-    # rows reading them back from there; chunks with every data piece present never reach the GPU).  False: round 4's form
-    # (recover-only call into a pinned scratch, then the join, A/B: tools/stream_rate.py --ab-join).
+    # A host reassembly in ONE library call (sec_decode_batch_ex's host join, api.cpp decode_core
+    # / join_staged): chunks with every data piece present are copied by the library's task
+    # threads and never reach the GPU; the others are recovered on the GPU beside those copies,
+    # only the recovered rows crossing PCIe.  False: round 4's form (a recover-only call into a
+    # pinned scratch, then the join; A/B in tools/stream_rate.py).
     LIBRARY_JOIN = True
 
     def _reassemble(self, items, outs) -> None:
@@ -422,8 +423,9 @@ class Engine:
             descs[j] = (int(outs[j]), B, padlen, slot, k, m)
             slot += k
         if n:
-            # (not staged: the library copies the present pieces first, then a large call's
-            # kernels read them back from the output in place, page-locked for the call)
+            # (not staged=True: when the pieces are too scattered to page-lock, the library
+            # copies the present ones into the output first and a large call's kernels read
+            # them back from there, the output page-locked for the call)
             self.decode_batch(descs, sn, bo, 0, 0, host=True)
 
     def decode_host(self, items) -> bytes:
