@@ -5,9 +5,9 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
 export TMPDIR=/tmp
-echo "== syn occ" && timeout -k 10 500 python3 -u tools/syn_ab.py --rounds 3 --reps 5 --modes reassemble --variants "auto,w3/w3,w3r6/w3r6" --cases "32 lost;24 lost (random;16 lost (random, parity;30 % of blocks lost, first" > $O/syn_occ.jsonl 2> $O/syn_occ.err || { tail -20 $O/syn_occ.err; exit 1; }
+echo "== syn occ" && timeout -k 10 500 python3 -u tools/syn_ab.py --rounds 3 --reps 5 --modes reassemble --variants "${SYN_VARIANTS:-auto,w3/w3,w3r6/w3r6}" --cases "32 lost;24 lost (random;16 lost (random, parity;30 % of blocks lost, first" > $O/syn_occ${SYN_TAG}.jsonl 2> $O/syn_occ${SYN_TAG}.err || { tail -20 $O/syn_occ${SYN_TAG}.err; exit 1; }
 python3 -c "
 import json
-for l in open('$O/syn_occ.jsonl'):
+for l in open('$O/syn_occ${SYN_TAG}.jsonl'):
     d=json.loads(l); print(d['case'][:60], {k: v['reassemble'] for k, v in d.items() if isinstance(v, dict) and 'reassemble' in v})
 "
