@@ -177,3 +177,48 @@ def test_reassembly_paths_agree(library_join, monkeypatch):
     dst = np.zeros(sum(map(len, want)) + 5, np.uint8)
     assert eng.decode_host_into(items, dst) == dst.size - 5
     assert dst[:-5].tobytes() == b"".join(want)
+
+
+def test_reassembly_threads_concurrent():
+    """Host reassembly from several threads at once, each on its own engine (the stream workers'
+    form): piece objects (staged or read back from a locked output), all-present chunks copied
+    without the GPU, per-call page locks of neighbouring outputs that touch one another's
+    registrations.  Every result is exact however the calls interleave."""
+    import threading
+
+    from storb_amd.engine import Engine
+
+    rng = random.Random(41)
+    cases = []
+    for n in (3 << 20, (1 << 20) + 11, 8 << 20, 70_000):
+        data = rng.randbytes(n)
+        k, m, B, padlen = piece.chunk_shape(n)
+        blocks = cfec.easy_encode(data, k, m)
+        for lost in ((), (0,), tuple(range(min(m - k, k)))):
+            keep = [j for j in range(m) if j not in lost][:k]
+            cases.append(((k, m, [blocks[j] for j in keep], keep, padlen), data))
+    errors = []
+
+    def run(seed):
+        try:
+            eng = Engine(0)
+            try:
+                r = random.Random(seed)
+                for _ in range(6):
+                    pick = r.sample(cases, 6)
+                    items = [c for c, _ in pick]
+                    if r.random() < 0.5:
+                        assert eng.decode_host_chunks(items) == [d for _, d in pick]
+                    else:
+                        assert eng.decode_host(items) == b"".join(d for _, d in pick)
+            finally:
+                eng.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=run, args=(s,)) for s in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
