@@ -248,6 +248,42 @@ __global__ __launch_bounds__(256) void k_c5(const u8 *__restrict__ in, u8 *__res
     }
 }
 
+// C5's decode traffic with zfec's own block boundaries (B not a multiple of 16, as in the bench's
+// log-uniform chunk sizes): every row read and written at an unaligned address
+typedef u32x4 u32x4_u1 __attribute__((aligned(1)));
+__device__ __forceinline__ u32x4 ldu(const u8 *p) { return __builtin_nontemporal_load((const u32x4_u1 *)p); }
+__device__ __forceinline__ void stu(u8 *p, u32x4 v) { __builtin_nontemporal_store(v, (u32x4_u1 *)p); }
+template <u32 BB_>
+__global__ __launch_bounds__(256) void k_c5u(const u8 *__restrict__ in, u8 *__restrict__ par, u8 *__restrict__ out)
+{
+    constexpr u32 per = (BB_ + 4095) / 4096;
+    const u32 chunk = blockIdx.x / per, t0 = min((blockIdx.x % per) * 4096 + threadIdx.x * 16, BB_ - 16);
+    const u8 *s = in + (size_t)chunk * 8 * BB_ + t0;
+    const u8 *p = par + (size_t)chunk * 3 * BB_ + t0;
+    constexpr int keep[5] = {0, 2, 4, 6, 7};
+    u8 *o = out + (size_t)chunk * 8 * BB_ + t0;
+    u32x4 x[8];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        x[j] = ldu(s + keep[j] * BB_);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        x[5 + r] = ldu(p + r * BB_);
+    u32x4 a = x[5], b = x[6], c = x[7];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        a ^= x[j];
+        b ^= x[j] << 1;
+        c ^= x[j] << 2;
+    }
+    stu(o + 1 * BB_, a);
+    stu(o + 3 * BB_, b);
+    stu(o + 5 * BB_, c);
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        stu(o + keep[j] * BB_, x[j]);
+}
+
 template <class F>
 double time_ms(F launch)
 {
@@ -332,6 +368,13 @@ int main()
            "\"c5_encode_B32K\": %.1f}\n",
            c5(k_c5<262144, false>, 262144, 16.0), c5(k_c5<32768, false>, 32768, 16.0), c5(k_c5<8192, false>, 8192, 16.0),
            c5(k_c5<262144, true>, 262144, 11.0), c5(k_c5<32768, true>, 32768, 11.0));
+    auto c5u = [&](auto kern, u32 BBv) {
+        const u32 nch = (u32)(G / (8ull * BBv + 4096));
+        return rate((double)nch * 16.0 * BBv,
+                    time_ms([&] { hipLaunchKernelGGL(kern, dim3(nch * ((BBv + 4095) / 4096)), dim3(256), 0, 0, a, b, c); }));
+    };
+    printf("{\"c5_decode_unaligned_B256K+6\": %.1f, \"c5_decode_unaligned_B32K+6\": %.1f, \"c5_decode_B256K_again\": %.1f}\n",
+           c5u(k_c5u<262150>, 262150), c5u(k_c5u<32774>, 32774), c5(k_c5<262144, false>, 262144, 16.0));
     const double c4d_256 = c4d(k_c4dec<256>, 256);
     const double c4d_448 = c4d(k_c4dec<448>, 448);
     printf("{\"c4_decode_lanes256\": %.1f, \"c4_decode_lanes448\": %.1f}\n", c4d_256, c4d_448);
