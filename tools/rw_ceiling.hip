@@ -284,6 +284,46 @@ __global__ __launch_bounds__(256) void k_c5u(const u8 *__restrict__ in, u8 *__re
         stu(o + keep[j] * BB_, x[j]);
 }
 
+// the same with separate row strides for the blocks read and the rows written (which side's
+// misalignment costs what)
+// XR: workgroup b runs logical tile (b / 64) * 64 + (b % 8) * 8 + (b / 8) % 8, so each XCD (b % 8)
+// takes runs of 8 consecutive tiles of a row at about the same time: a 128-byte line that two
+// neighbouring tiles' unaligned rows share is written within one XCD's L2
+template <u32 BI, u32 BO, bool XR = false>
+__global__ __launch_bounds__(256) void k_c5m(const u8 *__restrict__ in, u8 *__restrict__ par, u8 *__restrict__ out)
+{
+    constexpr u32 BB_ = BI < BO ? BI : BO, per = (BB_ + 4095) / 4096;
+    u32 bx = blockIdx.x;
+    if constexpr (XR)
+        if ((bx | 63u) < gridDim.x)  // (a partial last run of 64 keeps the plain order)
+            bx = (bx & ~63u) + (bx % 8) * 8 + (bx / 8) % 8;
+    const u32 chunk = bx / per, t0 = min((bx % per) * 4096 + threadIdx.x * 16, BB_ - 16);
+    const u8 *s = in + (size_t)chunk * 8 * BI + t0;
+    const u8 *p = par + (size_t)chunk * 3 * BI + t0;
+    constexpr int keep[5] = {0, 2, 4, 6, 7};
+    u8 *o = out + (size_t)chunk * 8 * BO + t0;
+    u32x4 x[8];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        x[j] = ldu(s + keep[j] * BI);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        x[5 + r] = ldu(p + r * BI);
+    u32x4 a = x[5], b = x[6], c = x[7];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        a ^= x[j];
+        b ^= x[j] << 1;
+        c ^= x[j] << 2;
+    }
+    stu(o + 1 * BO, a);
+    stu(o + 3 * BO, b);
+    stu(o + 5 * BO, c);
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        stu(o + keep[j] * BO, x[j]);
+}
+
 template <class F>
 double time_ms(F launch)
 {
@@ -375,6 +415,20 @@ int main()
     };
     printf("{\"c5_decode_unaligned_B256K+6\": %.1f, \"c5_decode_unaligned_B32K+6\": %.1f, \"c5_decode_B256K_again\": %.1f}\n",
            c5u(k_c5u<262150>, 262150), c5u(k_c5u<32774>, 32774), c5(k_c5<262144, false>, 262144, 16.0));
+    auto c5m = [&](auto kern, u32 BI, u32 BO) {
+        const u32 BBv = BI < BO ? BI : BO, BMAX = BI < BO ? BO : BI;
+        const u32 nch = (u32)(G / (8ull * BMAX + 4096));
+        return rate((double)nch * 16.0 * BBv,
+                    time_ms([&] { hipLaunchKernelGGL(kern, dim3(nch * ((BBv + 4095) / 4096)), dim3(256), 0, 0, a, b, c); }));
+    };
+    printf("{\"c5_decode_unaligned_reads_only_B256K\": %.1f, \"c5_decode_unaligned_writes_only_B256K\": %.1f, "
+           "\"c5_decode_unaligned_reads_only_B32K\": %.1f, \"c5_decode_unaligned_writes_only_B32K\": %.1f}\n",
+           c5m(k_c5m<262150, 262144>, 262150, 262144), c5m(k_c5m<262144, 262150>, 262144, 262150),
+           c5m(k_c5m<32774, 32768>, 32774, 32768), c5m(k_c5m<32768, 32774>, 32768, 32774));
+    printf("{\"c5_decode_unaligned_xcd_runs_B256K\": %.1f, \"c5_decode_unaligned_writes_only_xcd_runs_B256K\": %.1f, "
+           "\"c5_decode_aligned_xcd_runs_B256K\": %.1f, \"c5_decode_unaligned_xcd_runs_B32K\": %.1f}\n",
+           c5m(k_c5m<262150, 262150, true>, 262150, 262150), c5m(k_c5m<262144, 262150, true>, 262144, 262150),
+           c5m(k_c5m<262144, 262144, true>, 262144, 262144), c5m(k_c5m<32774, 32774, true>, 32774, 32774));
     const double c4d_256 = c4d(k_c4dec<256>, 256);
     const double c4d_448 = c4d(k_c4dec<448>, 448);
     printf("{\"c4_decode_lanes256\": %.1f, \"c4_decode_lanes448\": %.1f}\n", c4d_256, c4d_448);
