@@ -324,6 +324,74 @@ __global__ __launch_bounds__(256) void k_c5m(const u8 *__restrict__ in, u8 *__re
         stu(o + keep[j] * BO, x[j]);
 }
 
+// Unaligned rows written as aligned 16-byte segments: lane l stores the segment that starts in
+// its own 16 bytes and ends in lane l + 1's (wave_shl:1 DPP, v_alignbyte by the row's uniform
+// misalignment d); lanes 0 and 63 also store their own unaligned 16 bytes, which cover the
+// wave's partial first and last segments (the overlaps rewrite identical bytes).  Waves not
+// wholly inside the row keep plain unaligned stores.
+__device__ __forceinline__ u32 shl1(u32 x) { return (u32)__builtin_amdgcn_mov_dpp((int)x, 0x130, 0xf, 0xf, false); }
+template <int Q>
+__device__ __forceinline__ u32x4 window(const u32 (&c)[8], u32 r)
+{
+    return u32x4{__builtin_amdgcn_alignbyte(c[Q + 1], c[Q], r), __builtin_amdgcn_alignbyte(c[Q + 2], c[Q + 1], r),
+                 __builtin_amdgcn_alignbyte(c[Q + 3], c[Q + 2], r), __builtin_amdgcn_alignbyte(c[Q + 4], c[Q + 3], r)};
+}
+template <bool EDGES = true>
+__device__ __forceinline__ void st_realigned(u8 *o, u32x4 v, bool whole_wave)
+{
+    const u32 d = __builtin_amdgcn_readfirstlane((u32)(uintptr_t)o) & 15u;  // (lane offsets are multiples of 16)
+    if (!whole_wave || d == 0) {
+        stu(o, v);
+        return;
+    }
+    const u32 c[8] = {v.x, v.y, v.z, v.w, shl1(v.x), shl1(v.y), shl1(v.z), shl1(v.w)};
+    const u32 sft = 16 - d, r = sft & 3;
+    u32x4 w;
+    switch (sft >> 2) {
+    case 0: w = window<0>(c, r); break;
+    case 1: w = window<1>(c, r); break;
+    case 2: w = window<2>(c, r); break;
+    default: w = window<3>(c, r); break;
+    }
+    const u32 lane = threadIdx.x & 63;
+    if (lane < 63)
+        st(o - d + 16, w);
+    if (EDGES && (lane == 0 || lane == 63))
+        stu(o, v);
+}
+template <u32 BB_, bool EDGES = true>
+__global__ __launch_bounds__(256) void k_c5r(const u8 *__restrict__ in, u8 *__restrict__ par, u8 *__restrict__ out)
+{
+    constexpr u32 per = (BB_ + 4095) / 4096;
+    const u32 chunk = blockIdx.x / per, traw = (blockIdx.x % per) * 4096 + threadIdx.x * 16;
+    const u32 t0 = min(traw, BB_ - 16);
+    const bool whole = ((blockIdx.x % per) * 4096 + (threadIdx.x & ~63u) * 16 + 1024) <= BB_;  // wave-uniform
+    const u8 *s = in + (size_t)chunk * 8 * BB_ + t0;
+    const u8 *p = par + (size_t)chunk * 3 * BB_ + t0;
+    constexpr int keep[5] = {0, 2, 4, 6, 7};
+    u8 *o = out + (size_t)chunk * 8 * BB_ + t0;
+    u32x4 x[8];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        x[j] = ldu(s + keep[j] * BB_);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        x[5 + r] = ldu(p + r * BB_);
+    u32x4 a = x[5], b = x[6], c = x[7];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        a ^= x[j];
+        b ^= x[j] << 1;
+        c ^= x[j] << 2;
+    }
+    st_realigned<EDGES>(o + 1 * BB_, a, whole);
+    st_realigned<EDGES>(o + 3 * BB_, b, whole);
+    st_realigned<EDGES>(o + 5 * BB_, c, whole);
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        st_realigned<EDGES>(o + keep[j] * BB_, x[j], whole);
+}
+
 template <class F>
 double time_ms(F launch)
 {
@@ -429,6 +497,21 @@ int main()
            "\"c5_decode_aligned_xcd_runs_B256K\": %.1f, \"c5_decode_unaligned_xcd_runs_B32K\": %.1f}\n",
            c5m(k_c5m<262150, 262150, true>, 262150, 262150), c5m(k_c5m<262144, 262150, true>, 262144, 262150),
            c5m(k_c5m<262144, 262144, true>, 262144, 262144), c5m(k_c5m<32774, 32774, true>, 32774, 32774));
+    {
+        // realigned stores: correctness against the plain unaligned kernel on the same inputs
+        const u32 BBv = 262150, nch = (u32)(G / (8ull * BBv + 4096));
+        hipLaunchKernelGGL(k_c5u<262150>, dim3(nch * ((BBv + 4095) / 4096)), dim3(256), 0, 0, a, b, c);
+        std::vector<u8> ref(4 << 20), got(4 << 20);
+        CK(hipMemcpy(ref.data(), c, ref.size(), hipMemcpyDeviceToHost));
+        CK(hipMemset(c, 0x5a, (size_t)nch * 8 * BBv));
+        hipLaunchKernelGGL(k_c5r<262150>, dim3(nch * ((BBv + 4095) / 4096)), dim3(256), 0, 0, a, b, c);
+        CK(hipMemcpy(got.data(), c, got.size(), hipMemcpyDeviceToHost));
+        printf("{\"c5_realigned_matches_unaligned\": %s, \"c5_decode_realigned_B256K+6\": %.1f, "
+               "\"c5_decode_realigned_B32K+6\": %.1f, \"c5_decode_unaligned_B256K+6_again\": %.1f, "
+               "\"c5_decode_realigned_no_edges_B256K+6\": %.1f, \"c5_decode_realigned_no_edges_B32K+6\": %.1f}\n",
+               ref == got ? "true" : "false", c5u(k_c5r<262150>, 262150), c5u(k_c5r<32774>, 32774),
+               c5u(k_c5u<262150>, 262150), c5u(k_c5r<262150, false>, 262150), c5u(k_c5r<32774, false>, 32774));
+    }
     const double c4d_256 = c4d(k_c4dec<256>, 256);
     const double c4d_448 = c4d(k_c4dec<448>, 448);
     printf("{\"c4_decode_lanes256\": %.1f, \"c4_decode_lanes448\": %.1f}\n", c4d_256, c4d_448);
