@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void k_c5u(const u8 *__restrict__ in, u8 *__re
 // XR: workgroup b runs logical tile (b / 64) * 64 + (b % 8) * 8 + (b / 8) % 8, so each XCD (b % 8)
 // takes runs of 8 consecutive tiles of a row at about the same time: a 128-byte line that two
 // neighbouring tiles' unaligned rows share is written within one XCD's L2
-template <u32 BI, u32 BO, bool XR = false>
+template <u32 BI, u32 BO, bool XR = false, u32 OFF = 0>
 __global__ __launch_bounds__(256) void k_c5m(const u8 *__restrict__ in, u8 *__restrict__ par, u8 *__restrict__ out)
 {
     constexpr u32 BB_ = BI < BO ? BI : BO, per = (BB_ + 4095) / 4096;
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) void k_c5m(const u8 *__restrict__ in, u8 *__re
     const u8 *s = in + (size_t)chunk * 8 * BI + t0;
     const u8 *p = par + (size_t)chunk * 3 * BI + t0;
     constexpr int keep[5] = {0, 2, 4, 6, 7};
-    u8 *o = out + (size_t)chunk * 8 * BO + t0;
+    u8 *o = out + OFF + (size_t)chunk * 8 * BO + t0;
     u32x4 x[8];
 #pragma unroll
     for (int j = 0; j < 5; ++j)
@@ -497,6 +497,12 @@ int main()
            "\"c5_decode_aligned_xcd_runs_B256K\": %.1f, \"c5_decode_unaligned_xcd_runs_B32K\": %.1f}\n",
            c5m(k_c5m<262150, 262150, true>, 262150, 262150), c5m(k_c5m<262144, 262150, true>, 262144, 262150),
            c5m(k_c5m<262144, 262144, true>, 262144, 262144), c5m(k_c5m<32774, 32774, true>, 32774, 32774));
+    // aligned rows whose output base is shifted by 16 / 64 / 128 bytes: 16-byte aligned stores
+    // whose 1 KiB wave runs start inside a 128-byte line (16, 64) or on one (128)
+    printf("{\"c5_decode_out_shift16_B256K\": %.1f, \"c5_decode_out_shift64_B256K\": %.1f, "
+           "\"c5_decode_out_shift128_B256K\": %.1f, \"c5_decode_out_shift0_B256K\": %.1f}\n",
+           c5m(k_c5m<262144, 262144, false, 16>, 262144, 262144), c5m(k_c5m<262144, 262144, false, 64>, 262144, 262144),
+           c5m(k_c5m<262144, 262144, false, 128>, 262144, 262144), c5m(k_c5m<262144, 262144, false, 0>, 262144, 262144));
     {
         // realigned stores: correctness against the plain unaligned kernel on the same inputs
         const u32 BBv = 262150, nch = (u32)(G / (8ull * BBv + 4096));
