@@ -289,7 +289,8 @@ __global__ __launch_bounds__(256) void k_c5u(const u8 *__restrict__ in, u8 *__re
 // XR: workgroup b runs logical tile (b / 64) * 64 + (b % 8) * 8 + (b / 8) % 8, so each XCD (b % 8)
 // takes runs of 8 consecutive tiles of a row at about the same time: a 128-byte line that two
 // neighbouring tiles' unaligned rows share is written within one XCD's L2
-template <u32 BI, u32 BO, bool XR = false, u32 OFF = 0>
+__device__ __forceinline__ void stu_plain(u8 *p, u32x4 v) { *(u32x4_u1 *)p = v; }
+template <u32 BI, u32 BO, bool XR = false, u32 OFF = 0, bool NT = true>
 __global__ __launch_bounds__(256) void k_c5m(const u8 *__restrict__ in, u8 *__restrict__ par, u8 *__restrict__ out)
 {
     constexpr u32 BB_ = BI < BO ? BI : BO, per = (BB_ + 4095) / 4096;
@@ -316,12 +317,12 @@ __global__ __launch_bounds__(256) void k_c5m(const u8 *__restrict__ in, u8 *__re
         b ^= x[j] << 1;
         c ^= x[j] << 2;
     }
-    stu(o + 1 * BO, a);
-    stu(o + 3 * BO, b);
-    stu(o + 5 * BO, c);
+    NT ? stu(o + 1 * BO, a) : stu_plain(o + 1 * BO, a);
+    NT ? stu(o + 3 * BO, b) : stu_plain(o + 3 * BO, b);
+    NT ? stu(o + 5 * BO, c) : stu_plain(o + 5 * BO, c);
 #pragma unroll
     for (int j = 0; j < 5; ++j)
-        stu(o + keep[j] * BO, x[j]);
+        NT ? stu(o + keep[j] * BO, x[j]) : stu_plain(o + keep[j] * BO, x[j]);
 }
 
 // Unaligned rows written as aligned 16-byte segments: lane l stores the segment that starts in
@@ -497,6 +498,14 @@ int main()
            "\"c5_decode_aligned_xcd_runs_B256K\": %.1f, \"c5_decode_unaligned_xcd_runs_B32K\": %.1f}\n",
            c5m(k_c5m<262150, 262150, true>, 262150, 262150), c5m(k_c5m<262144, 262150, true>, 262144, 262150),
            c5m(k_c5m<262144, 262144, true>, 262144, 262144), c5m(k_c5m<32774, 32774, true>, 32774, 32774));
+    // unaligned rows with plain (write-back) stores, plain and XCD-run tile order: whether two
+    // waves' / workgroups' partial sectors merge in L2 before they are written back
+    printf("{\"c5_decode_unaligned_plain_st_B256K\": %.1f, \"c5_decode_unaligned_plain_st_xcd_runs_B256K\": %.1f, "
+           "\"c5_decode_unaligned_nt_B256K\": %.1f, \"c5_decode_aligned_plain_st_B256K\": %.1f}\n",
+           c5m(k_c5m<262150, 262150, false, 0, false>, 262150, 262150),
+           c5m(k_c5m<262150, 262150, true, 0, false>, 262150, 262150),
+           c5m(k_c5m<262150, 262150, false, 0, true>, 262150, 262150),
+           c5m(k_c5m<262144, 262144, false, 0, false>, 262144, 262144));
     // aligned rows whose output base is shifted by 16 / 64 / 128 bytes: 16-byte aligned stores
     // whose 1 KiB wave runs start inside a 128-byte line (16, 64) or on one (128)
     printf("{\"c5_decode_out_shift16_B256K\": %.1f, \"c5_decode_out_shift64_B256K\": %.1f, "
