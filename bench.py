@@ -209,12 +209,9 @@ def rank_context(args) -> SimpleNamespace:
     from storb_amd import dist as D
 
     rank, local, world = D.rank_env()
-    stub = os.environ.get("STORB_BENCH_ENGINE")
+    stub = _stub_factory()
     if stub:  # tests: the oracle behind the Engine interface, CPU tensors, gloo
-        import importlib
-
-        mod, cls = stub.split(":")
-        eng = getattr(importlib.import_module(mod), cls)()
+        eng = stub()
         device, sync, dev_idx = "cpu", (lambda: None), None
         dmod = D.init(os.environ.get("STORB_DIST_BACKEND") or "gloo")
     else:
@@ -621,9 +618,10 @@ def main_c2c3(args, ctx):
     # N > 1 ranks: the same workloads from ONE process over all N devices (engine.EngineGroup),
     # taken by rank 0 after every rank-per-GPU measurement while the other ranks wait on a CPU
     # (gloo) barrier with their buffers freed: reported beside `value`, never as it
-    if ctx.world > 1 and not args.no_in_process and not os.environ.get("STORB_BENCH_ENGINE"):
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
+    if ctx.world > 1 and not args.no_in_process:
+        if ctx.local is not None:  # a GPU rank (the stub's ranks hold CPU tensors)
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
         cpu_grp = ctx.dmod.new_group(backend="gloo")
         ctx.dmod.barrier(group=cpu_grp)
         if ctx.rank == 0:
@@ -998,25 +996,27 @@ def _inproc_timed(grp, prep, body, steps, done=None):
     return t1 - t0, res
 
 
-def inproc_c2c3(grp, steps, warmup, nchunks=N_CHUNKS) -> dict:
+def inproc_c2c3(grp, steps, warmup, nchunks=N_CHUNKS, cpu=False) -> dict:
     """The headline workload on every device of `grp` from ONE process and one host thread per
     device (engine.EngineGroup): each device owns its own 1024 x 1 MiB
     RS(4,2) chunks (weak scaling, as the torchrun form); value = all devices' chunk bytes
-    encoded + decoded / wall time of the slowest."""
+    encoded + decoded / wall time of the slowest.  cpu: the tests' stub engines on CPU tensors."""
     import torch
 
     from storb_amd.engine import get_engine
 
     def prep(i):
         d = grp.devices[i]
-        torch.cuda.set_device(d)
+        dev = "cpu" if cpu else f"cuda:{d}"
+        if not cpu:
+            torch.cuda.set_device(d)
         eng = get_engine()
         n, k, m = CHUNK, K, M
-        g = torch.Generator(device=f"cuda:{d}")
+        g = torch.Generator(device=dev)
         g.manual_seed(1000 + i)
-        src = torch.randint(0, 256, (nchunks * n,), dtype=torch.uint8, device=f"cuda:{d}", generator=g)
+        src = torch.randint(0, 256, (nchunks * n,), dtype=torch.uint8, device=dev, generator=g)
         ed, B = enc_descs(nchunks, n, k, m)
-        par = torch.empty(nchunks * (m - k) * B, dtype=torch.uint8, device=f"cuda:{d}")
+        par = torch.empty(nchunks * (m - k) * B, dtype=torch.uint8, device=dev)
         out = torch.empty_like(src)
         dd, sn, offs, av = dec_descs(nchunks, n, k, m, B, src.data_ptr(), par.data_ptr(), ERASED)
         st = {"eng": eng, "ed": ed, "src": src, "par": par, "out": out, "dd": dd, "sn": sn, "offs": offs, "av": av}
@@ -1034,7 +1034,8 @@ def inproc_c2c3(grp, steps, warmup, nchunks=N_CHUNKS) -> dict:
     def done(st):
         for key in ("src", "par", "out"):
             st.pop(key)
-        torch.cuda.empty_cache()
+        if not cpu:
+            torch.cuda.empty_cache()
 
     el, _ = _inproc_timed(grp, prep, body, steps, done)
     nbytes = len(grp) * nchunks * 2 * CHUNK
@@ -1109,12 +1110,24 @@ def inproc_devices(args, ndev) -> list[int]:
     return list(range(ndev))
 
 
+def _stub_factory():
+    """STORB_BENCH_ENGINE's class (tests: the oracle behind the Engine interface), or None."""
+    stub = os.environ.get("STORB_BENCH_ENGINE")
+    if not stub:
+        return None
+    import importlib
+
+    mod, cls = stub.split(":")
+    return getattr(importlib.import_module(mod), cls)
+
+
 def inproc_results(args, ndev) -> dict:
     from storb_amd.engine import EngineGroup
 
-    grp = EngineGroup(inproc_devices(args, ndev))
+    stub = _stub_factory()
+    grp = EngineGroup(inproc_devices(args, ndev), engine_factory=(lambda d: stub()) if stub else None)
     try:
-        res = {"c2c3": inproc_c2c3(grp, args.steps, args.warmup, args.chunks)}
+        res = {"c2c3": inproc_c2c3(grp, args.steps, args.warmup, args.chunks, cpu=stub is not None)}
         if not args.no_c5:
             res["c5"] = inproc_c5(grp, args.c5_steps, min(args.warmup, 2), args.c5_bytes)
     finally:
@@ -1128,7 +1141,7 @@ def main_in_process(args) -> None:
     import torch
 
     n = args.gpus
-    if max(inproc_devices(args, n)) >= torch.cuda.device_count():
+    if _stub_factory() is None and max(inproc_devices(args, n)) >= torch.cuda.device_count():
         raise SystemExit(f"bench --in-process: devices {inproc_devices(args, n)} asked, "
                          f"{torch.cuda.device_count()} visible")
     r = inproc_results(args, n)

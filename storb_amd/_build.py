@@ -17,7 +17,7 @@ LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libstorbec.so")
 INCLUDE = os.path.join(ROOT, "include")
 SOURCES = ["kernels.hip", "kernels_bs.hip", "bignum.hip", "api.cpp"]
-HEADERS = ["kernels.hpp", "bignum.hpp", "gf_host.hpp", "gf_const.hpp", "copy_pool.hpp", "task_pool.hpp"]
+HEADERS = ["kernels.hpp", "bignum.hpp", "gf_host.hpp", "gf_const.hpp", "task_pool.hpp"]
 # gfx950 (MI355X) only: the kernels use gfx950 instructions (16-byte global_load_lds, v_bitop3)
 # and up to 160 KiB of LDS per workgroup; kernels_bs.hip stops any other target with #error
 ARCH = "gfx950"
@@ -57,11 +57,27 @@ def _includes(path: str, seen: set) -> None:
                         _includes(h, seen)
 
 
+_COMPILER_ID: str | None = None
+
+
+def _compiler_id() -> str:
+    """The compiler an object was built with (HIPCC and its --version), part of the object key:
+    a ROCm upgrade or another HIPCC must not link old objects into a new library."""
+    global _COMPILER_ID
+    if _COMPILER_ID is None:
+        try:
+            out = subprocess.run([HIPCC, "--version"], capture_output=True, text=True, timeout=60).stdout
+        except (OSError, subprocess.SubprocessError) as e:
+            out = f"unavailable: {e}"
+        _COMPILER_ID = HIPCC + "\n" + out
+    return _COMPILER_ID
+
+
 def _obj_key(src: str, flags: list) -> str:
     path = os.path.join(CSRC, src)
     deps: set = set()
     _includes(path, deps)
-    h = hashlib.sha256(" ".join(flags).encode())
+    h = hashlib.sha256(_compiler_id().encode() + b"\0" + " ".join(flags).encode())
     for p in [path, *sorted(deps)]:
         with open(p, "rb") as f:
             h.update(p.encode() + f.read())
@@ -96,6 +112,9 @@ def build(force: bool = False, verbose: bool = False, defines: dict | None = Non
         key = _obj_key(src, flags)
         if not force and os.path.exists(obj) and _read(obj + ".key") == key:
             continue
+        for stale in (obj, obj + ".key"):  # a failed compile must leave no object its key matches
+            if os.path.exists(stale):
+                os.remove(stale)
         cmd = [HIPCC, *flags, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))

@@ -26,7 +26,6 @@
 #include <utility>
 #include <vector>
 
-#include "copy_pool.hpp"
 #include "task_pool.hpp"
 #include "bignum.hpp"
 #include "gf_host.hpp"
@@ -559,9 +558,12 @@ struct sec_ctx {
     DevBuf syn;         // syndrome rows of device-mode syndrome decodes
     size_t bn_part_stride = 0;
     Slot slots[kSlots];
-    std::unique_ptr<sec::CopyPool> pool;
-    std::unique_ptr<sec::TaskPool> tasks;  // sec_encode_pieces: piece copies and host SHA-1
-    PinBuf piece_par;                      // sec_encode_pieces: the parity, before the piece copies
+    // host threads (staging copies, joins, sec_encode_pieces' piece copies and SHA-1): the
+    // process's pool of this context's size, shared with every other context of that size
+    std::shared_ptr<sec::TaskPool> tasks;
+    // sec_encode_pieces: the parity of one sub-batch before its piece copies, two sub-batches in
+    // turn, each at most max(SEC_SLAB_BYTES, one chunk's parity)
+    PinBuf piece_par[2];
     // SEC_F_HOST encode / decode calls by path (sec_ctx_host_paths)
     int64_t zero_copy_calls = 0, registered_calls = 0, staged_calls = 0;
     int64_t syn_chunks = 0, direct_chunks = 0, fused_chunks = 0;  // decodes by method (sec_ctx_decode_paths)
@@ -588,25 +590,20 @@ int set_dev(const sec_ctx *ctx)
     return SEC_OK;
 }
 
+// O_COPY_THREADS, or half the CPUs this process may use (affinity and cgroup quota), at most 7
 int host_threads(const sec_ctx *ctx)
 {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    return ctx->opt[O_COPY_THREADS] ? (int)ctx->opt[O_COPY_THREADS] : (int)std::min(7u, std::max(1u, hw / 2));
-}
-
-sec::CopyPool &pool(sec_ctx *ctx)
-{
-    if (!ctx->pool)
-        ctx->pool.reset(new sec::CopyPool(host_threads(ctx)));
-    return *ctx->pool;
+    return ctx->opt[O_COPY_THREADS] ? (int)ctx->opt[O_COPY_THREADS] : sec::default_pool_threads();
 }
 
 sec::TaskPool &tasks(sec_ctx *ctx)
 {
     if (!ctx->tasks)
-        ctx->tasks.reset(new sec::TaskPool(host_threads(ctx)));
+        ctx->tasks = sec::shared_pool(host_threads(ctx));
     return *ctx->tasks;
 }
+
+sec::TaskPool &pool(sec_ctx *ctx) { return tasks(ctx); }
 
 int slots_init(sec_ctx *ctx)
 {
@@ -625,7 +622,7 @@ int slot_retire(sec_ctx *ctx, Slot &s)
         return SEC_OK;
     s.busy = false;
     CK(hipEventSynchronize(s.done));
-    pool(ctx).run(s.scatter);
+    pool(ctx).run_copies(s.scatter);
     s.scatter.clear();
     return SEC_OK;
 }
@@ -1401,7 +1398,7 @@ int run_pipeline(sec_ctx *ctx, Plan &plan, Gather gather, Scatter scatter, Launc
         }
         std::vector<sec::CopyJob> jobs;
         gather(sp, sl.in.c(), jobs);
-        pool(ctx).run(jobs);
+        pool(ctx).run_copies(jobs);
         CK(hipStreamWaitEvent(sl.s, ctx->meta_ev, 0));
         if (on_pins) {
             RC(launch(sp, (uint8_t *)sl.in.p, (uint8_t *)sl.out.p, sl.s));
@@ -1686,8 +1683,8 @@ void sec_ctx_destroy(sec_ctx *ctx)
             (void)hipStreamDestroy(s.s);
     }
     ctx->tasks.reset();
-    ctx->pool.reset();
-    ctx->piece_par.release();
+    for (PinBuf &b : ctx->piece_par)
+        b.release();
     ctx->pin.release();
     ctx->enc_tabs.buf.release();
     ctx->dec_tabs.buf.release();
@@ -1746,10 +1743,8 @@ int sec_ctx_set_option(sec_ctx *ctx, const char *name, int64_t value)
     ctx->opt.v[i] = value;
     for (Plan *p : {&ctx->enc_plan, &ctx->dec_plan, &ctx->sha_plan, &ctx->bn_plan})
         p->valid = false;
-    if (i == O_COPY_THREADS) {
-        ctx->pool.reset();
+    if (i == O_COPY_THREADS)
         ctx->tasks.reset();
-    }
     return SEC_OK;
 }
 
@@ -2214,7 +2209,7 @@ int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
         return SEC_OK;
     if (nchunks >= (int64_t)UINT32_MAX)
         return SEC_EINVAL;
-    uint64_t total_par = 0;
+    uint64_t max_par = 0;
     for (int64_t i = 0; i < nchunks; ++i) {  // easyfec / _fec preconditions (as encode_impl)
         const sec_enc_chunk &c = chunks[i];
         if (c.k < 1 || c.m < c.k || c.m > 256)
@@ -2224,21 +2219,31 @@ int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             return SEC_EBLOCKLEN;
         if (B >= (1ull << 31))
             return SEC_ESIZE;
-        total_par += (uint64_t)(c.m - c.k) * B;
+        max_par = std::max<uint64_t>(max_par, (uint64_t)(c.m - c.k) * B);
     }
     for (int64_t i = 0, pb = 0; i < nchunks; pb += chunks[i++].m)  // a buffer for every non-empty piece
         for (int j = 0; j < chunks[i].m; ++j)
             if (!pieces[pb + j] && enc_B(chunks[i]) > 0)
                 return SEC_EINVAL;
     RC(set_dev(ctx));
-    RC(ctx->piece_par.ensure(std::max<uint64_t>(total_par, 1)));
+    // The parity goes through pinned scratch in sub-batches of at most `cap` bytes (a chunk whose
+    // own parity is larger alone), two scratch buffers in turn: sub-batch s + 1 encodes while the
+    // task threads copy and hash sub-batch s's parity pieces.  Locked memory stays bounded by
+    // 2 cap whatever the call's size (one allocation of the whole call's parity).
+    const uint64_t cap = std::max<uint64_t>((uint64_t)ctx->opt[O_SLAB_BYTES], max_par);
     sec::TaskPool &tp = tasks(ctx);
-    sec::TaskPool::Group data, par;
+    sec::TaskPool::Group data, par[2];
+    bool par_failed = false;
     std::vector<sec_enc_chunk> tmp(chunks, chunks + nchunks);
-    uint64_t pb = 0, po = 0;
+    std::vector<uint64_t> first_piece((size_t)nchunks);
+    uint64_t pb = 0;
     for (int64_t i = 0; i < nchunks; ++i) {
         const sec_enc_chunk &c = chunks[i];
         const uint64_t B = enc_B(c);
+        first_piece[i] = pb;
+        for (int j = 0; j < c.m && B == 0; ++j)  // an empty chunk: every piece is b"" (no buffer)
+            if (digests)
+                (void)sec::sha1_padded(nullptr, 0, 0, digests + (pb + j) * 20);
         for (int j = 0; j < c.k && B > 0; ++j) {
             const uint64_t start = (uint64_t)j * B;
             const uint64_t av = c.n > start ? std::min<uint64_t>(B, c.n - start) : 0;
@@ -2254,35 +2259,54 @@ int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
                 return !dig || sec::sha1_padded(dst, B, B, dig);
             });
         }
-        tmp[i].parity_off = po;
-        tmp[i].parity_stride = B;
-        po += (uint64_t)(c.m - c.k) * B;
         pb += (uint64_t)c.m;
     }
     int rc = SEC_OK;
-    if (total_par)
-        rc = encode_impl(ctx, tmp.data(), nchunks, in, (uint8_t *)ctx->piece_par.p, nullptr,
-                         SEC_F_HOST | (flags & SEC_F_STAGED), false);
-    if (rc == SEC_OK) {
-        pb = 0;
-        for (int64_t i = 0; i < nchunks; ++i) {
-            const sec_enc_chunk &c = chunks[i];
-            const uint64_t B = enc_B(c);
-            for (int r = 0; r < c.m - c.k && B > 0; ++r) {
-                uint8_t *dst = pieces[pb + c.k + r];
-                const uint8_t *src = (const uint8_t *)ctx->piece_par.p + tmp[i].parity_off + (uint64_t)r * B;
-                uint8_t *dig = digests ? digests + (pb + c.k + r) * 20 : nullptr;
-                tp.submit(par, [=] {
-                    memcpy(dst, src, B);
-                    return !dig || sec::sha1_padded(dst, B, B, dig);
-                });
-            }
-            pb += (uint64_t)c.m;
+    int buf = 0;
+    for (int64_t c0 = 0; c0 < nchunks && rc == SEC_OK;) {
+        // the next sub-batch [c0, c1): chunks whose parity sums to at most cap
+        int64_t c1 = c0;
+        uint64_t po = 0;
+        while (c1 < nchunks) {
+            const sec_enc_chunk &c = chunks[c1];
+            const uint64_t B = enc_B(c), p = (uint64_t)(c.m - c.k) * B;
+            if (c1 > c0 && po + p > cap)
+                break;
+            tmp[c1].parity_off = po;
+            tmp[c1].parity_stride = B;
+            po += p;
+            ++c1;
         }
+        if (po) {
+            par_failed |= !tp.wait(par[buf]);  // the scratch's previous pieces are copied out
+            par[buf].failed.store(false);
+            PinBuf &scratch = ctx->piece_par[buf];
+            rc = scratch.ensure(po);
+            if (rc == SEC_OK)
+                rc = encode_impl(ctx, tmp.data() + c0, c1 - c0, in, (uint8_t *)scratch.p, nullptr,
+                                 SEC_F_HOST | (flags & SEC_F_STAGED), false);
+            for (int64_t i = c0; i < c1 && rc == SEC_OK; ++i) {
+                const sec_enc_chunk &c = chunks[i];
+                const uint64_t B = enc_B(c);
+                for (int r = 0; r < c.m - c.k && B > 0; ++r) {
+                    uint8_t *dst = pieces[first_piece[i] + c.k + r];
+                    const uint8_t *src = (const uint8_t *)scratch.p + tmp[i].parity_off + (uint64_t)r * B;
+                    uint8_t *dig = digests ? digests + (first_piece[i] + c.k + r) * 20 : nullptr;
+                    tp.submit(par[buf], [=] {
+                        memcpy(dst, src, B);
+                        return !dig || sec::sha1_padded(dst, B, B, dig);
+                    });
+                }
+            }
+            buf ^= 1;
+        }
+        c0 = c1;
     }
-    const bool ok_data = tp.wait(data), ok_par = tp.wait(par);  // both waited: no task outlives the call
-    const bool ok = ok_data && ok_par;
-    if (rc == SEC_OK && !ok)
+    // every group waited: no task outlives the call
+    const bool ok_data = tp.wait(data);
+    for (sec::TaskPool::Group &g : par)
+        par_failed |= !tp.wait(g);
+    if (rc == SEC_OK && (!ok_data || par_failed))
         rc = SEC_EINVAL;  // OpenSSL failed (no other cause)
     return rc;
 }
@@ -2855,7 +2879,7 @@ int decode_core(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
         RC(launch_decode_sub(ctx, plan, plan.subs[0], blocks, out, ctx->stream(), ctx->syn.as<uint8_t>()));
         RC(timing_end(ctx, t0, 1, ctx->stream()));
         if (nocopy)  // the present primaries, host to host, while the kernels run
-            pool(ctx).run(joins);
+            pool(ctx).run_copies(joins);
         if (!(flags & SEC_F_ASYNC))
             CK(hipStreamSynchronize(ctx->stream()));
         return SEC_OK;
@@ -2908,7 +2932,7 @@ int decode_core(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
     };
     RC(run_pipeline(ctx, plan, gather, scatter, launch, true));
     if (join)  // the present primaries, host to host
-        pool(ctx).run(joins);
+        pool(ctx).run_copies(joins);
     return SEC_OK;
 }
 }  // namespace
@@ -3036,7 +3060,7 @@ int sec_host_copy(sec_ctx *ctx, const sec_copy *jobs, int64_t njobs)
         cj.push_back(sec::CopyJob{(void *)(uintptr_t)jobs[i].dst, (const void *)(uintptr_t)jobs[i].src,
                                   (size_t)jobs[i].len});
     }
-    pool(ctx).run(cj);
+    pool(ctx).run_copies(cj);
     return SEC_OK;
 }
 

@@ -5,10 +5,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <memory>
 #include <random>
+#include <thread>
 #include <vector>
 
-#include "copy_pool.hpp"
 #include "gf_host.hpp"
 #include "task_pool.hpp"
 
@@ -55,7 +57,7 @@ static void test_matrices()
 static void test_copy_pool()
 {
     std::mt19937_64 rng(7);
-    sec::CopyPool pool(5);
+    sec::TaskPool pool(5);
     for (int round = 0; round < 40; ++round) {
         const int njobs = 1 + (int)(rng() % 40);
         std::vector<std::vector<char>> src(njobs), dst(njobs);
@@ -68,10 +70,38 @@ static void test_copy_pool()
                 src[j][i] = (char)rng();
             jobs.push_back(sec::CopyJob{dst[j].data(), src[j].data(), n});
         }
-        pool.run(jobs);
+        pool.run_copies(jobs);
         for (int j = 0; j < njobs; ++j)
             EXPECT(src[j] == dst[j]);
     }
+}
+
+// copies from several threads at once through one shared pool (contexts of one process share it)
+static void test_shared_pool_concurrent()
+{
+    std::shared_ptr<sec::TaskPool> a = sec::shared_pool(4), b = sec::shared_pool(4);
+    EXPECT(a.get() == b.get());
+    EXPECT(sec::shared_pool(3).get() != a.get());
+    EXPECT(sec::usable_cpus() >= 1);
+    EXPECT(sec::default_pool_threads() >= 1 && sec::default_pool_threads() <= 7);
+    std::vector<std::thread> th;
+    std::atomic<int> bad{0};
+    for (int t = 0; t < 6; ++t)
+        th.emplace_back([&, t] {
+            std::mt19937_64 rng(100 + t);
+            for (int round = 0; round < 6; ++round) {
+                const size_t n = (5u << 20) + rng() % (3u << 20);
+                std::vector<char> src(n), dst(n, 0), zero(n, 1);
+                for (size_t i = 0; i < n; i += 512)
+                    src[i] = (char)rng();
+                a->run_copies({sec::CopyJob{dst.data(), src.data(), n}, sec::CopyJob{zero.data(), nullptr, n}});
+                if (dst != src || zero != std::vector<char>(n, 0))
+                    ++bad;
+            }
+        });
+    for (auto &x : th)
+        x.join();
+    EXPECT(bad.load() == 0);
 }
 
 static void test_task_pool_sha1()
@@ -124,6 +154,7 @@ int main()
 {
     test_matrices();
     test_copy_pool();
+    test_shared_pool_concurrent();
     test_task_pool_sha1();
     if (fails)
         return 1;

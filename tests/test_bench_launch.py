@@ -110,3 +110,93 @@ def test_bench_gpus1_c2c3_nests_c4_c5_with_cpu_baselines():
         assert s["n_gpus"] == 1 and s["roofline"]["bound"] == "hbm" and s["roofline"]["achieved"] > 0
         assert s["cpu_baseline"]["value"] > 0 and what in s["cpu_baseline"]["sample"]
     assert len(j["lib_digest"]) == 64
+
+
+# ---- the N > 1 lines exactly as the driver's 8-GPU node will parse them ----
+def _check_in_process(ip, n, c5_bytes):
+    sys.path.insert(0, ROOT)
+    import bench
+    from storb_amd.dist import partition
+
+    h = ip["c2c3"]
+    assert h["n_gpus"] == n and h["devices"] == list(range(n)) and h["scaling"] == "weak"
+    assert h["value"] > 0 and h["ms_per_step"] > 0 and "EngineGroup" in h["launch"]
+    c5 = ip["c5"]
+    sizes = bench.c5_sizes(c5_bytes)
+    assert c5["n_gpus"] == n and c5["scaling"] == "strong" and c5["value"] > 0
+    assert c5["per_device_chunks"] == [hi - lo for lo, hi in partition(sizes, n)]
+    assert sum(c5["per_device_chunks"]) == len(sizes)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_gpus_n_headline_line_with_in_process(n):
+    """`bench.py --gpus N`: the headline line with c4 / c5 nested and, after them, the in-process
+    form (EngineGroup over N stub engines) nested as `in_process`."""
+    c5_bytes = 8 << 20
+    p, lines = _run(["--gpus", str(n), "--steps", "1", "--warmup", "1", "--chunks", "2", "--no-cpu", "--no-e2e",
+                     "--c4-chunks", str(2 * n), "--c5-bytes", str(c5_bytes), "--c5-steps", "1"], timeout=540)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(lines) == 1, p.stdout
+    j = json.loads(lines[0])
+    assert j["metric"] == "GiB/s device-resident RS encode+decode, 1 MiB chunks, 1/2/4/8 MI355X"
+    assert j["n_gpus"] == n and j["config"]["world_size"] == n and j["config"]["backend"] == "gloo"
+    assert j["config"]["per_rank_chunks"] == [2] * n and j["scaling"] == "weak"
+    assert j["value"] == pytest.approx(2 * 2 * n * (1 << 20) / (j["ms_per_step"] / 1e3) / (1 << 30), rel=0.02)
+    assert j["c4"]["n_gpus"] == n and j["c4"]["config"]["per_rank_chunks"] == [2] * n
+    assert j["c5"]["n_gpus"] == n and j["cpu_baseline"] is None
+    sys.path.insert(0, ROOT)
+    import bench
+    from storb_amd.dist import partition
+
+    sizes = bench.c5_sizes(c5_bytes)
+    parts = partition(sizes, n)
+    assert j["c5"]["config"]["per_rank_chunks"] == [hi - lo for lo, hi in parts]
+    # C5's split balances bytes: no rank holds more than the average plus one chunk
+    per = [sum(sizes[lo:hi]) for lo, hi in parts]
+    assert sum(per) == sum(sizes) and max(per) <= sum(sizes) / n + max(sizes)
+    assert "error" not in j["in_process"], j["in_process"]
+    _check_in_process(j["in_process"], n, c5_bytes)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("workload", ["c4", "c5"])
+def test_bench_gpus8_c4_c5_lines(workload):
+    args = ["--gpus", "8", "--workload", workload, "--steps", "1", "--warmup", "1", "--no-cpu", "--no-e2e"]
+    args += ["--c4-chunks", "64"] if workload == "c4" else ["--c5-bytes", str(16 << 20)]
+    p, lines = _run(args, timeout=540)
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 8 and j["config"]["world_size"] == 8
+    if workload == "c4":
+        assert j["config"]["per_rank_chunks"] == [8] * 8 and j["config"]["chunks_total"] == 64
+    else:
+        sys.path.insert(0, ROOT)
+        import bench
+        from storb_amd.dist import partition
+
+        sizes = bench.c5_sizes(16 << 20)
+        assert j["config"]["per_rank_chunks"] == [hi - lo for lo, hi in partition(sizes, 8)]
+
+
+def test_c4_default_job_splits_8_x_8192():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    shares = [bench.c4_share(r, 8) for r in range(8)]
+    assert [hi - lo for lo, hi in shares] == [8192] * 8
+    assert shares[0][0] == 0 and shares[-1][1] == 65536
+    assert all(shares[i][1] == shares[i + 1][0] for i in range(7))
+
+
+@pytest.mark.timeout(300)
+def test_bench_in_process_mode_stub():
+    """`bench.py --gpus 4 --in-process`: one process, the line's value is the in-process headline."""
+    c5_bytes = 8 << 20
+    p, lines = _run(["--gpus", "4", "--in-process", "--steps", "1", "--warmup", "1", "--chunks", "2",
+                     "--c5-bytes", str(c5_bytes), "--c5-steps", "1"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 4 and j["config"]["world_size"] == 1 and "in-process x4" in j["config"]["parallelism"]
+    assert j["value"] == j["in_process"]["c2c3"]["value"]
+    _check_in_process(j["in_process"], 4, c5_bytes)

@@ -222,3 +222,80 @@ def test_reassembly_threads_concurrent():
     for t in ts:
         t.join()
     assert not errors, errors
+
+
+def test_pieces_parity_over_slab_and_empty_chunks():
+    """The call's parity far above SEC_SLAB_BYTES (64 KiB here): sub-batches through two bounded
+    pinned scratch buffers, a chunk whose own parity exceeds the cap alone; empty chunks' pieces
+    hash as b"" (ADVICE r05)."""
+    from storb_amd.engine import Engine
+
+    rng = random.Random(5)
+    cases = _shapes_and_chunks(rng)
+    for k, m in ((2, 3), (4, 6)):
+        cases.insert(rng.randrange(len(cases)), ((k, m, 0, 0), b""))
+    eng = Engine(options={"SEC_SLAB_BYTES": 1 << 16})
+    try:
+        for _ in range(2):  # scratch reused across calls
+            bufs, addrs = [], []
+            for (k, m, B, _), _ in cases:
+                row = [np.empty(max(B, 1), np.uint8) for _ in range(m)]
+                bufs.append(row)
+                addrs += [a.ctypes.data for a in row]
+            dig = np.zeros(20 * len(addrs), np.uint8)
+            eng.encode_pieces_into([c for _, c in cases], [(k, m) for (k, m, _, _), _ in cases], addrs, dig)
+            j = 0
+            for ((k, m, B, _), c), row in zip(cases, bufs):
+                want = cfec.easy_encode(c, k, m) if c else [b""] * m
+                if c:
+                    assert [r.tobytes() for r in row] == want, (k, m, len(c))
+                for w in want:
+                    assert dig[20 * j:20 * (j + 1)].tobytes() == hashlib.sha1(w).digest(), (k, m, len(c), j)
+                    j += 1
+    finally:
+        eng.close()
+
+
+def test_library_threads_bounded_over_many_contexts():
+    """32 caller threads, each with its own context (get_engine), encode pieces at once: the
+    library's host threads are one shared pool sized from this process's CPUs, not a pool per
+    context (VERDICT r05 next #5)."""
+    import os
+    import threading
+
+    def nthreads():
+        return len(os.listdir("/proc/self/task"))
+
+    get_engine()  # this thread's context and the runtime's own threads exist before the count
+    base = nthreads()
+    rng = random.Random(9)
+    chunk = rng.randbytes(3 << 20)
+    errors, ready = [], threading.Barrier(32)
+    peak = [0]
+
+    def work():
+        try:
+            eng = get_engine()
+            ready.wait()
+            k, m = 8, 12
+            B = -(-len(chunk) // k)
+            row = [np.empty(B, np.uint8) for _ in range(m)]
+            dig = np.zeros(20 * m, np.uint8)
+            for _ in range(3):
+                eng.encode_pieces_into([chunk], [(k, m)], [a.ctypes.data for a in row], dig)
+                peak[0] = max(peak[0], nthreads())
+            assert [r.tobytes() for r in row] == cfec.easy_encode(chunk, k, m)
+            eng.close()
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errors.append(e)
+
+    th = [threading.Thread(target=work) for _ in range(32)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[0]
+    cpus = len(os.sched_getaffinity(0))
+    # the 32 callers themselves, one pool of <= 7, and a few runtime threads; a pool per
+    # context would add 7 per caller
+    assert peak[0] - base <= 32 + 7 + 8, (peak[0], base, cpus)
