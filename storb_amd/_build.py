@@ -15,6 +15,9 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libstorbec.so")
+# A/B and calibration builds (tools/sweep.py): outside the package, so the product's lib/ holds
+# only the library the product loads
+VARIANT_DIR = os.path.join(ROOT, "build", "variants")
 INCLUDE = os.path.join(ROOT, "include")
 SOURCES = ["kernels.hip", "kernels_bs.hip", "bignum.hip", "api.cpp"]
 HEADERS = ["kernels.hpp", "bignum.hpp", "gf_host.hpp", "gf_const.hpp", "task_pool.hpp"]
@@ -84,11 +87,16 @@ def _obj_key(src: str, flags: list) -> str:
     return h.hexdigest()
 
 
+def variant_lib(tag: str) -> str:
+    """Where the A/B variant `tag` (build(defines=..., tag=tag)) lies."""
+    return os.path.join(VARIANT_DIR, f"libstorbec_{tag}.so")
+
+
 def build(force: bool = False, verbose: bool = False, defines: dict | None = None, tag: str | None = None) -> str:
     """Compile libstorbec.so (or, with `tag`, an A/B variant libstorbec_<tag>.so built with
     extra -D `defines`, used by tools/sweep.py)."""
-    os.makedirs(LIBDIR, exist_ok=True)
-    lib = LIB if not tag else os.path.join(LIBDIR, f"libstorbec_{tag}.so")
+    lib = LIB if not tag else variant_lib(tag)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
     defs = [f"-D{k}={v}" for k, v in sorted((defines or {}).items())]
     stamp = lib + ".stamp"
     dig = _digest() + " ".join(defs)
@@ -99,7 +107,7 @@ def build(force: bool = False, verbose: bool = False, defines: dict | None = Non
     tmp = lib + ".tmp"
     # one hipcc per source, in parallel (the device code of each file is compiled on its own
     # anyway), then one link
-    objdir = os.path.join(LIBDIR, "obj_" + (tag or "lib"))
+    objdir = os.path.join(os.path.dirname(lib), "obj_" + (tag or "lib"))
     os.makedirs(objdir, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
              f"-I{INCLUDE}", *defs]

@@ -137,6 +137,7 @@ enum Opt {
     O_COPY_THREADS,      // 0 rule, or host copy-pool threads
     O_REGISTER_MIN,      // page-lock pageable host buffers for calls moving >= this many bytes (0: never)
     O_HOST_JOIN,         // 0: the GPU writes every byte of a host reassembly
+    O_BS_PAIR,           // zfec(64,96) encode: 1 two-wave workgroups sharing each block's subsets, 0 interleaved groups
     O_COUNT
 };
 
@@ -157,6 +158,7 @@ constexpr OptSpec kOpts[O_COUNT] = {
     {"SEC_COPY_THREADS", 0, 0, 256},
     {"SEC_REGISTER_MIN", (int64_t)4 << 20, 0, (int64_t)1 << 62},
     {"SEC_HOST_JOIN", 1, 0, 1},
+    {"SEC_BS_PAIR", 1, 0, 1},
 };
 
 struct Options {
@@ -417,6 +419,7 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
 // has.  (Round 4's A/B forms -- one launch per group, (32,48) in 8-row groups, shared-transpose
 // wave pairs, LDS-staged small chunks -- are archived: tools/archive/.)
 constexpr int kBsAllGroups = 99;  // Group::U of an interleaved launch of every row group
+constexpr int kBsPair = 98;       // Group::U of a two-wave launch, both row groups of a span per workgroup
 constexpr int kSolveLds = 1 << 16;  // phase-2 tile map keys of sec_solve_bs_lds_kernel launches
 constexpr int kSynWg2 = 1 << 16;    // phase-1 tile map keys of sec_syndrome_bs_pair_kernel launches
 
@@ -437,6 +440,12 @@ int bs_shape(const Options &o, int k, int m, uint64_t B)
 
 void add_bs_work(const Options &o, Bins &bins, uint32_t chunk, uint64_t B, int shape)
 {
+    if (sec_bs_groups(shape) > 1 && o[O_BS_PAIR]) {  // (64,96): one two-wave workgroup per span
+        auto &bin = bins[{3, shape, kBsPair, 128, 0}];
+        for (uint64_t t0 = 0; t0 < B; t0 += sec_bs_span())
+            bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
+        return;
+    }
     const int lanes = o.lanes(O_BS_LANES);
     const uint64_t step = (uint64_t)sec_bs_span() * (lanes / 64);
     // two row groups ((64,96)): one launch, flatten() interleaves the groups; else group 0
@@ -901,8 +910,8 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
     for (const Group &g : sp.groups) {
-        int e = g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsAllGroups ? -1 : g.U, g.lanes, in, par, dd,
-                                                   dt + g.first, g.count, s)
+        int e = g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsPair ? -2 : g.U == kBsAllGroups ? -1 : g.U,
+                                                   g.lanes, in, par, dd, dt + g.first, g.count, s)
                             : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
         if (e)
             return hip_fail((hipError_t)e, g.mfma == 3 ? "sec_encode_bs_kernel" : "sec_encode_kernel");

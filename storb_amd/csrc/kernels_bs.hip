@@ -455,6 +455,141 @@ __global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs2_kernel(c
         bs_span<K, M, NR, NR, D, false>(in, par, d, s, lring);
 }
 
+// ---- zfec(64,96) encode: both row groups of a span in one two-wave workgroup ----------------
+// The interleaved kernel above runs each 16-row group as its own wave, so both waves of a span
+// transpose all 64 blocks and form their plane subsets: 70 of each block's 198 VALU are done
+// twice, and the kernel is VALU-bound (SQ_ACTIVE_INST_VALU 51 % of each wave's cycles at two
+// waves per SIMD, i.e. the SIMD's VALU nearly saturated; profiles/r06_pmc.json).  Here wave g
+// (group g) loads, transposes and forms the subsets of the blocks j = 2i + g only, publishes the
+// 30 subset XORs through LDS, and takes the other wave's for the blocks 2i + 1 - g: 163 VALU per
+// block instead of 198, one barrier per pair of blocks, each block read from HBM once (no L2
+// re-read).  LDS: two steps of both waves' 8 x 16 bytes per lane, 32 KiB per workgroup.
+// SEC_BS_PAIR_PLANES (build knob, A/B): publish the 8 transposed planes instead (2 LDS stores and
+// loads per block instead of 8; the taker forms the subsets itself: 174 VALU per block).
+#ifndef SEC_BS_PAIR_PLANES
+#define SEC_BS_PAIR_PLANES 0
+#endif
+
+struct PairXchg {
+    u32x4 v[2][2][8][64];  // [step & 1][publishing wave][dword quad][lane]
+};
+
+__device__ __forceinline__ void barrier_lds()
+{
+    // own LDS stores done, then the workgroup barrier; no vmcnt wait (the loads in flight stay)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int K, int M, int G, int NR, int D, int I>
+__device__ __forceinline__ void pair_step(u32 (&acc)[NR * 8], u32 (&ring)[D][8], PairXchg &xb, const u8 *src, u64 B,
+                                          u32 pa, u32 pb, u32 valid)
+{
+    constexpr int J = 2 * I + G, O = 2 * I + 1 - G;  // own block, the other wave's block
+    const u32 l = threadIdx.x & 63;
+    u32 x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        x[i] = ring[I % D][i];
+    if constexpr (I + D < K / 2)
+        load_block<true>(ring[I % D], src + (u64)(2 * (I + D) + G) * B, pa, pb, valid, 2 * (I + D) + G == K - 1);
+    transpose8(x);
+    u32x4(&mine)[8][64] = xb.v[I & 1][G];
+    u32x4(&theirs)[8][64] = xb.v[I & 1][1 - G];
+    u32 lo[16], hi[16];
+#if SEC_BS_PAIR_PLANES
+    mine[0][l] = u32x4{x[0], x[1], x[2], x[3]};
+    mine[1][l] = u32x4{x[4], x[5], x[6], x[7]};
+    subsets(x[0], x[1], x[2], x[3], lo);
+    subsets(x[4], x[5], x[6], x[7], hi);
+#else
+    subsets(x[0], x[1], x[2], x[3], lo);
+    subsets(x[4], x[5], x[6], x[7], hi);
+    mine[0][l] = u32x4{lo[1], lo[2], lo[3], lo[4]};
+    mine[1][l] = u32x4{lo[5], lo[6], lo[7], lo[8]};
+    mine[2][l] = u32x4{lo[9], lo[10], lo[11], lo[12]};
+    mine[3][l] = u32x4{lo[13], lo[14], lo[15], hi[1]};
+    mine[4][l] = u32x4{hi[2], hi[3], hi[4], hi[5]};
+    mine[5][l] = u32x4{hi[6], hi[7], hi[8], hi[9]};
+    mine[6][l] = u32x4{hi[10], hi[11], hi[12], hi[13]};
+    mine[7][l] = u32x4{hi[14], hi[15], 0u, 0u};
+#endif
+    block_rows<K, M, G * NR, J, I == 0>(std::make_integer_sequence<int, NR * 8>{}, acc, lo, hi);
+    barrier_lds();  // both waves' step-I subsets are in LDS (and both finished reading step I-1's)
+    u32 lo2[16], hi2[16];
+#if SEC_BS_PAIR_PLANES
+    const u32x4 t0 = theirs[0][l], t1 = theirs[1][l];
+    subsets(t0.x, t0.y, t0.z, t0.w, lo2);
+    subsets(t1.x, t1.y, t1.z, t1.w, hi2);
+#else
+    const u32x4 t0 = theirs[0][l], t1 = theirs[1][l], t2 = theirs[2][l], t3 = theirs[3][l], t4 = theirs[4][l],
+                t5 = theirs[5][l], t6 = theirs[6][l], t7 = theirs[7][l];
+    lo2[0] = hi2[0] = 0;
+    lo2[1] = t0.x, lo2[2] = t0.y, lo2[3] = t0.z, lo2[4] = t0.w;
+    lo2[5] = t1.x, lo2[6] = t1.y, lo2[7] = t1.z, lo2[8] = t1.w;
+    lo2[9] = t2.x, lo2[10] = t2.y, lo2[11] = t2.z, lo2[12] = t2.w;
+    lo2[13] = t3.x, lo2[14] = t3.y, lo2[15] = t3.z, hi2[1] = t3.w;
+    hi2[2] = t4.x, hi2[3] = t4.y, hi2[4] = t4.z, hi2[5] = t4.w;
+    hi2[6] = t5.x, hi2[7] = t5.y, hi2[8] = t5.z, hi2[9] = t5.w;
+    hi2[10] = t6.x, hi2[11] = t6.y, hi2[12] = t6.z, hi2[13] = t6.w;
+    hi2[14] = t7.x, hi2[15] = t7.y;
+#endif
+    block_rows<K, M, G * NR, O, false>(std::make_integer_sequence<int, NR * 8>{}, acc, lo2, hi2);
+}
+
+template <int K, int M, int G, int NR, int D, int... Is>
+__device__ __forceinline__ void pair_steps(std::integer_sequence<int, Is...>, u32 (&acc)[NR * 8], u32 (&ring)[D][8],
+                                           PairXchg &xb, const u8 *src, u64 B, u32 pa, u32 pb, u32 valid)
+{
+    (pair_step<K, M, G, NR, D, Is>(acc, ring, xb, src, B, pa, pb, valid), ...);
+}
+
+template <int K, int M, int G, int NR, int D>
+__device__ __forceinline__ void bs_pair_span(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d,
+                                             u32 s, PairXchg &xb)
+{
+    static_assert(K % 2 == 0 && D >= 1 && D <= K / 2, "pair encode shape");
+    const u32 B = d.B;
+    const u32 lane = (threadIdx.x & 63) * 16;
+    const u32 pa = min(s + lane, B - 16), pb = min(s + 1024 + lane, B - 16);
+    const u8 *src = in + d.in_off;
+    u32 ring[D][8];
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        load_block<true>(ring[j], src + (u64)(2 * j + G) * B, pa, pb, d.valid, 2 * j + G == K - 1);
+    u32 acc[NR * 8];
+    pair_steps<K, M, G, NR, D>(std::make_integer_sequence<int, K / 2>{}, acc, ring, xb, src, B, pa, pb, d.valid);
+    u8 *dst = par + d.par_off;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        u32 y[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            y[i] = acc[r * 8 + i];
+        transpose8(y);
+        u8 *o = dst + (u64)(G * NR + r) * d.par_stride;
+        st16(o + pa, y[0], y[1], y[2], y[3]);
+        st16(o + pb, y[4], y[5], y[6], y[7]);
+    }
+}
+
+// One span per workgroup (tile t0), wave g = row group g.
+template <int K, int M, int NR, int D>
+__global__ __launch_bounds__(128) void sec_encode_bs_pair_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+                                                                 const sec::EncDesc *__restrict__ descs,
+                                                                 const sec::Tile *__restrict__ tiles)
+{
+    static_assert(M - K == 2 * NR, "two row groups");
+    const sec::Tile tl = tiles[blockIdx.x];
+    const sec::EncDesc d = descs[tl.chunk];
+    if (tl.t0 >= d.B)  // the whole workgroup: both waves leave before any barrier
+        return;
+    __shared__ PairXchg xb;
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 64)
+        bs_pair_span<K, M, 0, NR, D>(in, par, d, tl.t0, xb);
+    else
+        bs_pair_span<K, M, 1, NR, D>(in, par, d, tl.t0, xb);
+}
+
 // ---- decode: syndromes of the present parity rows, then a Cauchy solve (wide decodes) --------
 // A decode that lost e data blocks L and holds e parity rows S instead: for a parity row r in S,
 //     s_r = p_r ^ XOR_{present j} c[r][j] * d_j  =  XOR_{l in L} c[r][l] * d_l,
@@ -772,6 +907,122 @@ __device__ __forceinline__ ItemAddrs item_addrs(const SynCtx &c)
     return ItemAddrs{addr(t), NI > 64 ? addr(64 + t) : 0};
 }
 
+// ---- phase 1's LDS ring in rank order (SEC_SYN_RANK, build knob; 0 = the ring above) ----------
+// The ring above gives every item a slot, absent ones included (a lost data block's slot reads a
+// present block again), so with half the blocks lost half the ring's depth holds no work and a
+// wave waits on memory for most of its life (sec_syndrome_bs_pair_kernel, 32 lost: SQ_WAIT_ANY 54 %
+// of wave cycles, profiles/r06_pmc.json).  Here the ring holds only the items a wave works on: the
+// present data blocks but K-1 and the group's present parity rows, in item order ("ranks"), so D
+// slots are D items of work ahead.  Rank r lies in slot r % D; its block address comes from a
+// per-lane table (lane r: rank r) by a run-time readlane.  Past the last rank the refills re-read
+// the last item (an L2 hit) into the slot just consumed, so every consume issues exactly two loads
+// and the wait is the compile-time s_waitcnt vmcnt(2 (D - 1)) whatever the erasure pattern.  Data
+// block K-1 (possibly short: the byte path) is read into registers before any ring load, so every
+// ring load is younger than it.
+#ifndef SEC_SYN_RANK
+#define SEC_SYN_RANK 1
+#endif
+
+struct RankRing {
+    u64 a, b;  // lane r: the block address of rank r (a) and of rank 64 + r (b)
+    u32 n;     // ranks
+};
+
+template <int K, int NR, int R0>
+__device__ __forceinline__ bool ring_item(const SynCtx &c, u32 it)
+{
+    constexpr u32 NI = K + NR;
+    if (it >= NI || it == (u32)K - 1)
+        return false;
+    return it < (u32)K ? ((c.dmask >> it) & 1) : ((c.pmask >> (R0 + it - K)) & 1);
+}
+
+template <int K, int NR, int R0, class Ring>
+__device__ __forceinline__ RankRing rank_ring(Ring &ring, u32 w, const SynCtx &c)
+{
+    const u32 t = threadIdx.x & 63;
+    const bool h0 = ring_item<K, NR, R0>(c, t), h1 = ring_item<K, NR, R0>(c, 64 + t);
+    const u64 m0 = __builtin_amdgcn_ballot_w64(h0), m1 = __builtin_amdgcn_ballot_w64(h1);
+    const u32 n0 = (u32)__builtin_popcountll(m0);
+    auto below = [&](u64 m) { return __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u)); };
+    auto addr = [&](u32 it) -> u64 {
+        const u32 slot = it < (u32)K ? it : it + R0;
+        return (u64)(uintptr_t)(c.blocks + c.off[c.slot0 + slot]);
+    };
+    // the table goes through slot 0 of the wave's ring (1 KiB = 128 addresses) before any load
+    u64 *tbl = reinterpret_cast<u64 *>(&ring.v[w][0][0][0]);
+    if (h0)
+        tbl[below(m0)] = addr(t);
+    if (h1)
+        tbl[n0 + below(m1)] = addr(64 + t);
+    RankRing rr{tbl[t], tbl[64 + t], n0 + (u32)__builtin_popcountll(m1)};
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the first loads overwrite it
+    return rr;
+}
+
+// rank min(r, n - 1)'s two halves into `slot`
+template <class Ring>
+__device__ __forceinline__ void rank_issue(Ring &ring, u32 w, const RankRing &rr, const SynCtx &c, u32 r, u32 slot)
+{
+    r = min(r, rr.n - 1);
+    const u64 v = r < 64 ? rr.a : rr.b;
+    const u32 lo = __builtin_amdgcn_readlane((u32)v, r & 63), hi = __builtin_amdgcn_readlane((u32)(v >> 32), r & 63);
+    const u8 *blk = reinterpret_cast<const u8 *>(((u64)hi << 32) | lo);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + c.pa),
+                                     (__attribute__((address_space(3))) void *)&ring.v[w][slot][0][0], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + c.pb),
+                                     (__attribute__((address_space(3))) void *)&ring.v[w][slot][1][0], 16, 0, 0);
+}
+
+template <int K, int M, int R0, int NR, int D, bool FUSED, int J, class Ring>
+__device__ __forceinline__ void syn_item_rank(u32 (&acc)[NR * 8], Ring &ring, u32 w, u32 (&xs)[8], const SynCtx &c,
+                                              const RankRing &rr, u32 &p, u8 *orow0, u32 B, u32 last, bool copies,
+                                              u8 *syn, u32 &q)
+{
+    if (!item_present<K, NR, R0>(c, J))
+        return;
+    u32 x[8];
+    if constexpr (J == K - 1) {
+        wait_vm<2 * D>();  // the ring's 2 D loads in flight are all younger than block K-1's
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            x[i] = xs[i];
+    } else {
+        wait_vm<2 * (D - 1)>();  // rank p has landed
+        const u32 slot = p % D;
+        const u32x4 a = ring.v[w][slot][0][threadIdx.x & 63], b = ring.v[w][slot][1][threadIdx.x & 63];
+        x[0] = a.x;
+        x[1] = a.y;
+        x[2] = a.z;
+        x[3] = a.w;
+        x[4] = b.x;
+        x[5] = b.y;
+        x[6] = b.z;
+        x[7] = b.w;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read before it is refilled
+        rank_issue(ring, w, rr, c, p + D, slot);
+        ++p;
+    }
+    syn_process<K, M, R0, NR, FUSED, J>(acc, x, c, orow0, B, last, copies, syn, q);
+}
+
+template <int K, int M, int R0, int NR, int D, bool FUSED, class Ring, int... Js>
+__device__ __forceinline__ void syn_items_rank(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], Ring &ring,
+                                               u32 w, const SynCtx &c, u8 *orow0, u32 B, u32 last, bool copies,
+                                               u8 *syn, u32 &q)
+{
+    u32 xs[8];
+    if (item_present<K, NR, R0>(c, K - 1))
+        load_syn_item<K, NR, R0, K - 1>(xs, c);
+    asm volatile("" ::: "memory");  // block K-1's loads are issued before (older than) every ring load
+    const RankRing rr = rank_ring<K, NR, R0>(ring, w, c);
+#pragma unroll
+    for (u32 r = 0; r < (u32)D; ++r)
+        rank_issue(ring, w, rr, c, r, r);
+    u32 p = 0;
+    (syn_item_rank<K, M, R0, NR, D, FUSED, Js>(acc, ring, w, xs, c, rr, p, orow0, B, last, copies, syn, q), ...);
+}
+
 template <int K, int M, int R0, int NR, int D, class Ring>
 __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__restrict__ out, u8 *__restrict__ syn,
                                          const sec::SynDesc &d, const sec::SynSlots &sl, u32 s, bool copies,
@@ -791,11 +1042,16 @@ __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__re
     if constexpr (K >= 32) {
         constexpr int DL = SEC_FUSED_LDS_RING;
         const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if SEC_SYN_RANK
+        syn_items_rank<K, M, R0, NR, DL, false>(std::make_integer_sequence<int, K + NR>{}, acc, lring, w, c,
+                                                out + d.out_off, B, d.last, copies, syn + d.syn_off, q);
+#else
         u32 xs[8];
         const ItemAddrs ia = item_addrs<K, NR, R0>(c);
         lds_first<K, NR, R0, DL>(std::make_integer_sequence<int, DL>{}, lring, w, xs, c, ia);
         syn_items_lds<K, M, R0, NR, DL, false>(std::make_integer_sequence<int, K + NR>{}, acc, lring, w, xs, c, ia,
                                                out + d.out_off, B, d.last, copies, syn + d.syn_off, q);
+#endif
     } else
 #endif
     {
@@ -1025,6 +1281,49 @@ __global__ __launch_bounds__(256) SEC_SOLVE_WAVES_ATTR void sec_solve_bs_kernel(
 // waves, wave w solving 8-row group w: the e rows (2 KiB each) come into LDS once by
 // global_load_lds (spread over the waves), then every wave reads them from LDS.  LDS = e rounded
 // up to 8 rows x 2 KiB (dynamic), at most 64 KiB.
+// s_waitcnt vmcnt(v) for the largest v in {0, 2, 4, 6, 8, 12} not above n (n wave-uniform): a
+// run-time count as one asm statement (a ladder of scalar branches the compiler does not see, so
+// it costs no registers); waiting for fewer outstanding loads than n is stricter, never wrong
+__device__ __forceinline__ void wait_vm_le(u32 n)
+{
+    asm volatile("s_cmp_ge_u32 %0, 12\n\t"
+                 "s_cbranch_scc1 1f\n\t"
+                 "s_cmp_ge_u32 %0, 8\n\t"
+                 "s_cbranch_scc1 2f\n\t"
+                 "s_cmp_ge_u32 %0, 6\n\t"
+                 "s_cbranch_scc1 3f\n\t"
+                 "s_cmp_ge_u32 %0, 4\n\t"
+                 "s_cbranch_scc1 4f\n\t"
+                 "s_cmp_ge_u32 %0, 2\n\t"
+                 "s_cbranch_scc1 5f\n\t"
+                 "s_waitcnt vmcnt(0)\n\t"
+                 "s_branch 9f\n"
+                 "1:\n\t"
+                 "s_waitcnt vmcnt(12)\n\t"
+                 "s_branch 9f\n"
+                 "2:\n\t"
+                 "s_waitcnt vmcnt(8)\n\t"
+                 "s_branch 9f\n"
+                 "3:\n\t"
+                 "s_waitcnt vmcnt(6)\n\t"
+                 "s_branch 9f\n"
+                 "4:\n\t"
+                 "s_waitcnt vmcnt(4)\n\t"
+                 "s_branch 9f\n"
+                 "5:\n\t"
+                 "s_waitcnt vmcnt(2)\n"
+                 "9:" ::"s"(n)
+                 : "scc", "memory");
+}
+
+// The syndrome rows come into LDS in chunks of 8 (16 halves of 1 KiB, 16 / W per wave, all issued
+// up front); SEC_SOLVE_PIPE (build knob, A/B): 1 = a wave starts on chunk c once chunk c has
+// landed (its own loads waited, then a barrier), so the first rows are solved while the rest are
+// in flight; 0 = every row waited before the first is solved.
+#ifndef SEC_SOLVE_PIPE
+#define SEC_SOLVE_PIPE 1
+#endif
+
 template <int K, int M, int R0, int NR, int J>
 __device__ __forceinline__ void solve_item_lds(u32 (&acc)[NR * 8], const u32x4 (*sy)[2][64], uint64_t pmask,
                                                uint64_t lost, u32 lane)
@@ -1032,6 +1331,14 @@ __device__ __forceinline__ void solve_item_lds(u32 (&acc)[NR * 8], const u32x4 (
     if (!((pmask >> J) & 1))
         return;
     const u32 q = (u32)__builtin_popcountll(pmask & ((1ull << J) - 1ull));
+#if SEC_SOLVE_PIPE
+    if ((q & 7) == 0) {  // the first row of chunk q / 8: its loads (every wave's) have landed
+        constexpr u32 per = 16 / (K / NR);  // each wave's loads per chunk
+        const u32 chunks = ((u32)__builtin_popcountll(pmask) + 7) / 8;
+        wait_vm_le(per * (chunks - 1 - (q >> 3)));
+        __syncthreads();
+    }
+#endif
     const u32x4 a = sy[q][0][lane], b = sy[q][1][lane];
     u32 lo[16], hi[16];
     subsets(a.x, a.y, a.z, a.w, lo);
@@ -1086,12 +1393,31 @@ __global__ __launch_bounds__(64 * (K / NR)) void sec_solve_bs_lds_kernel(const u
     const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const u8 *base = syn + d.syn_off + s + 16 * lane;  // rows hold whole spans: no clamping
     const u64 stride = sec::syn_stride(d.B);
-    const u32 n = 2 * (u32)__builtin_popcountll(d.pmask);  // 1 KiB halves of the e rows
+    const u32 e = (u32)__builtin_popcountll(d.pmask);
+#if SEC_SOLVE_PIPE
+    // chunk c = rows [8c, 8c + 8) = halves [16c, 16c + 16); wave w loads halves 16c + w + W t.  A
+    // chunk's rows past e (the LDS holds e rounded up to 8 rows) load row e - 1 again, so every
+    // wave issues the same count per chunk and a chunk's wait is a count of later chunks' loads.
+    static_assert(16 % W == 0, "waves per chunk");
+    const u32 chunks = (e + 7) / 8;
+    for (u32 c = 0; c < chunks; ++c)
+        for (u32 t = 0; t < 16 / W; ++t) {
+            const u32 i = 16 * c + w + W * t, row = min(i >> 1, e - 1);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(base + (u64)row * stride + (i & 1) * 1024),
+                                             (__attribute__((address_space(3))) void *)&sy[i >> 1][i & 1][0], 16, 0, 0);
+        }
+    if (!((d.lost >> (w * NR)) & ((1ull << NR) - 1ull))) {  // no lost row in this wave's group
+        wait_vm<0>();  // its loads have landed before it leaves (a finished wave leaves the barriers)
+        return;
+    }
+#else
+    const u32 n = 2 * e;  // 1 KiB halves of the e rows
     for (u32 i = w; i < n; i += W)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(base + (u64)(i >> 1) * stride + (i & 1) * 1024),
                                          (__attribute__((address_space(3))) void *)&sy[i >> 1][i & 1][0], 16, 0, 0);
     wait_vm<0>();
     __syncthreads();
+#endif
     solve_groups_lds<K, M, NR>(std::make_integer_sequence<int, W>{}, w, sy, d, masks, out, s, lane);
 }
 
@@ -1148,11 +1474,16 @@ __device__ __forceinline__ void fused_span(const u8 *__restrict__ blocks, u8 *__
     if constexpr (K >= 32) {
         constexpr int DL = SEC_FUSED_LDS_RING;
         const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if SEC_SYN_RANK
+        syn_items_rank<K, M, RP0, NRP, DL, true>(std::make_integer_sequence<int, K + NRP>{}, acc, lring, w, c,
+                                                 out + d.out_off, B, d.last, copies, nullptr, q);
+#else
         u32 xs[8];
         const ItemAddrs ia = item_addrs<K, NRP, RP0>(c);
         lds_first<K, NRP, RP0, DL>(std::make_integer_sequence<int, DL>{}, lring, w, xs, c, ia);
         syn_items_lds<K, M, RP0, NRP, DL, true>(std::make_integer_sequence<int, K + NRP>{}, acc, lring, w, xs, c, ia,
                                                 out + d.out_off, B, d.last, copies, nullptr, q);
+#endif
     } else
 #endif
     {
@@ -1196,7 +1527,10 @@ hipError_t launch_bs(int lanes, const u8 *in, u8 *par, const sec::EncDesc *d, co
 {
     void *a = nullptr, *b = nullptr;
     sec_next_launch_events(&a, &b);  // kernel timing (sec_ctx_set_timing) rides on the dispatch
-    if constexpr (R0 < 0)
+    if constexpr (R0 == -2)
+        hipExtLaunchKernelGGL((sec_encode_bs_pair_kernel<K, M, NR, D>), dim3(nt), dim3(128), 0, s, (hipEvent_t)a,
+                              (hipEvent_t)b, 0, in, par, d, t);
+    else if constexpr (R0 < 0)
         hipExtLaunchKernelGGL((sec_encode_bs2_kernel<K, M, NR, D>), dim3(nt), dim3(lanes), 0, s, (hipEvent_t)a,
                               (hipEvent_t)b, 0, in, par, d, t);
     else
@@ -1213,6 +1547,10 @@ hipError_t launch_bs(int lanes, const u8 *in, u8 *par, const sec::EncDesc *d, co
 #define RING_K(k, d) (SEC_BS_RING < (k) ? SEC_BS_RING : (k))
 #else
 #define RING_K(k, d) (d)
+#endif
+// own blocks in flight per wave of the pair kernel
+#ifndef SEC_BS_PAIR_RING
+#define SEC_BS_PAIR_RING 2
 #endif
 struct BsShape {
     int k, m, nr;
@@ -1241,11 +1579,15 @@ int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uin
 {
     if (ntiles == 0)
         return hipSuccess;
-    if (lanes < 64 || lanes > 256 || lanes % 64 || shape < 0 || shape >= kNShapes || group < -1)
+    if (lanes < 64 || lanes > 256 || lanes % 64 || shape < 0 || shape >= kNShapes || group < -2)
         return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
     // group -1: every row group in one launch (sec_encode_bs2_kernel, the two-group (64,96)),
-    // tiles carry r0; 0: the one-group shapes
+    // tiles carry r0; -2: both groups of a span in one two-wave workgroup (sec_encode_bs_pair_kernel,
+    // one tile per span); 0: the one-group shapes
+    if (group == -2)
+        return shape == 4 ? launch_bs<64, 96, -2, 16, RING_K(64, SEC_BS_PAIR_RING)>(128, in, par, descs, t, ntiles, s)
+                          : hipErrorInvalidValue;
     switch (shape * 4 + group + 1) {
     case 1: return launch_bs<10, 14, 0, 4, RING_K(10, 5)>(lanes, in, par, descs, t, ntiles, s);
     case 5: return launch_bs<8, 12, 0, 4, RING_K(8, 4)>(lanes, in, par, descs, t, ntiles, s);

@@ -39,7 +39,7 @@ def run(reps: int, libs: str = "base", extra: bool = False):
     from storb_amd.engine import Engine
 
     tags = libs.split(",")
-    engs = {t: Engine(0, lib_path=_build.LIB if t == "base" else os.path.join(_build.LIBDIR, f"libstorbec_{t}.so"))
+    engs = {t: Engine(0, lib_path=_build.LIB if t == "base" else _build.variant_lib(t))
             for t in tags}
     sizes_all = np.array(bench.c5_sizes(), dtype=np.int64)
     res = {"config": f"C5 sizes (bench.c5_sizes) by class, RS(8,3), decode {ERASED} erased reassemble, "

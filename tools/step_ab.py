@@ -47,7 +47,7 @@ def main():
     from storb_amd import _build
     from storb_amd.engine import Engine
 
-    libs = {t: (_build.LIB if t == "base" else os.path.join(_build.LIBDIR, f"libstorbec_{t}.so")) for t in tags}
+    libs = {t: (_build.LIB if t == "base" else _build.variant_lib(t)) for t in tags}
     torch.cuda.set_device(0)
     nch, n, k, m = 1024, bench.CHUNK, bench.K, bench.M
     g = torch.Generator(device="cuda:0")

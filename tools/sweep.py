@@ -107,13 +107,13 @@ VARIANTS = {
 
 
 def build(tags):
-    """tag -> library; a tag "prev" is storb_amd/lib/libstorbec_prev.so as it lies (an earlier
+    """tag -> library; a tag "prev" is build/variants/libstorbec_prev.so as it lies (an earlier
     build kept for an A/B against the current sources), never rebuilt."""
     from storb_amd import _build
 
     libs = {t: _build.build(defines=VARIANTS[t], tag=t) for t in tags if t != "prev"}
     if "prev" in tags:
-        libs["prev"] = os.path.join(ROOT, "storb_amd", "lib", "libstorbec_prev.so")
+        libs["prev"] = _build.variant_lib("prev")
     return libs
 
 

@@ -100,15 +100,15 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="direct@SEC_SYN=0,syn@SEC_SYN=1,auto",
                     help="name@OPT=V+OPT2=V2[/tag]: context options per variant, optionally a prebuilt variant library "
-                         "storb_amd/lib/libstorbec_<tag>.so (storb_amd._build.build(defines=..., tag=...))")
+                         "build/variants/libstorbec_<tag>.so (storb_amd._build.build(defines=..., tag=...))")
     ap.add_argument("--cases", default="")
     ap.add_argument("--modes", default="reassemble,recover_only", help="decode modes to run (PMC passes: one)")
     a = ap.parse_args()
-    variants = []  # (name, env, lib path or None); "name@ENV=V+ENV2=V2/tag": storb_amd/lib/libstorbec_<tag>.so
+    variants = []  # (name, env, lib path or None); "name@ENV=V+ENV2=V2/tag": build/variants/libstorbec_<tag>.so
     for v in a.variants.split(","):
         v, _, tag = v.partition("/")
         name, _, env = v.partition("@")
-        lib = os.path.join(ROOT, "storb_amd", "lib", f"libstorbec_{tag}.so") if tag else None
+        lib = __import__("storb_amd._build", fromlist=["x"]).variant_lib(tag) if tag else None
         variants.append((name, {kv.split("=")[0]: int(kv.split("=")[1]) for kv in env.split("+")} if env else {}, lib))
     sel = [c for c in CASES if not a.cases or any(t in c[0] for t in a.cases.split(";"))]
     for name, k, m, n, nch, e, *seed in sel:

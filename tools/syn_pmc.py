@@ -4,7 +4,10 @@ sec_* decode kernel, dispatches, mean duration, HBM bytes per dispatch (read = 2
 1024 on gfx950, write = WRITE_SIZE x 1024; MI355X_MICROARCH.md) and the SQ wave-state fractions
 (SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_VALU over SQ_WAVE_CYCLES).  Not product code.
 
-    python tools/syn_pmc.py gpurun_out/<fetch dir> <write dir> <sq dir> <trace dir>
+    python tools/syn_pmc.py gpurun_out/<fetch dir> <write dir> <sq dir> <trace dir> [<more sq dirs>...]
+
+Every counter of the SQ passes is also reported as its mean per dispatch (`per_dispatch`), so a
+pass of instruction counts (SQ_INSTS_*, SQC_ICACHE_*, SQ_IFETCH) reads off directly.
 """
 
 import csv
@@ -42,6 +45,10 @@ def per_dispatch(d):
 def main():
     fetch, write, sq, trace = sys.argv[1:5]
     f, w, s = per_dispatch(fetch), per_dispatch(write), per_dispatch(sq)
+    for extra in sys.argv[5:]:
+        for k, cs in per_dispatch(extra).items():
+            for c, x in cs.items():
+                s[k][c] = x
     dur = defaultdict(list)
     for r in rows(trace, "*kernel_trace*.csv"):
         k = short(r.get("Kernel_Name", ""))
@@ -60,6 +67,8 @@ def main():
         for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY"):
             if cyc and s[k].get(c):
                 e[c.lower() + "_frac"] = round(sum(s[k][c]) / cyc, 3)
+        if s[k]:
+            e["per_dispatch"] = {c: round(sum(x) / len(x)) for c, x in sorted(s[k].items())}
         if dur.get(k):
             e["dispatches"] = len(dur[k])
             e["mean_ms"] = round(sum(dur[k]) / len(dur[k]), 4)
