@@ -459,7 +459,7 @@ __global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs2_kernel(c
 // The interleaved kernel above runs each 16-row group as its own wave, so both waves of a span
 // transpose all 64 blocks and form their plane subsets: 70 of each block's 198 VALU are done
 // twice, and the kernel is VALU-bound (SQ_ACTIVE_INST_VALU 51 % of each wave's cycles at two
-// waves per SIMD, i.e. the SIMD's VALU nearly saturated; profiles/r06_pmc.json).  Here wave g
+// waves per SIMD, i.e. the SIMD's VALU nearly saturated; profiles/r06_pmc_enc.json).  Here wave g
 // (group g) loads, transposes and forms the subsets of the blocks j = 2i + g only, publishes the
 // 30 subset XORs through LDS, and takes the other wave's for the blocks 2i + 1 - g: 163 VALU per
 // block instead of 198, one barrier per pair of blocks, each block read from HBM once (no L2
@@ -911,14 +911,18 @@ __device__ __forceinline__ ItemAddrs item_addrs(const SynCtx &c)
 // The ring above gives every item a slot, absent ones included (a lost data block's slot reads a
 // present block again), so with half the blocks lost half the ring's depth holds no work and a
 // wave waits on memory for most of its life (sec_syndrome_bs_pair_kernel, 32 lost: SQ_WAIT_ANY 54 %
-// of wave cycles, profiles/r06_pmc.json).  Here the ring holds only the items a wave works on: the
+// of wave cycles, profiles/r06_pmc_syn32.json).  Here the ring holds only the items a wave works on: the
 // present data blocks but K-1 and the group's present parity rows, in item order ("ranks"), so D
 // slots are D items of work ahead.  Rank r lies in slot r % D; its block address comes from a
 // per-lane table (lane r: rank r) by a run-time readlane.  Past the last rank the refills re-read
 // the last item (an L2 hit) into the slot just consumed, so every consume issues exactly two loads
 // and the wait is the compile-time s_waitcnt vmcnt(2 (D - 1)) whatever the erasure pattern.  Data
 // block K-1 (possibly short: the byte path) is read into registers before any ring load, so every
-// ring load is younger than it.
+// ring load is younger than it.  Measured neutral (sec_syndrome_bs_pair_kernel 573 / 544 us at 32 /
+// 24 lost against the round-5 ring's 567 / 545, profiles/r06_phase_stats_*.csv): the ring depth
+// is not what holds phase 1 back.  Letting the waits count the wave's own stores (so the ring runs
+// at its full depth in the copying wave) made it slower, 621 / 572 us (archived:
+// tools/archive/kernels_bs_r06_store_waits.diff).
 #ifndef SEC_SYN_RANK
 #define SEC_SYN_RANK 1
 #endif
@@ -1319,9 +1323,10 @@ __device__ __forceinline__ void wait_vm_le(u32 n)
 // The syndrome rows come into LDS in chunks of 8 (16 halves of 1 KiB, 16 / W per wave, all issued
 // up front); SEC_SOLVE_PIPE (build knob, A/B): 1 = a wave starts on chunk c once chunk c has
 // landed (its own loads waited, then a barrier), so the first rows are solved while the rest are
-// in flight; 0 = every row waited before the first is solved.
+// in flight; 0 = every row waited before the first is solved (default: the pipelined form took
+// 446 / 368 us against 409 / 330 at 32 / 24 lost, profiles/r06_phase_stats_*.csv).
 #ifndef SEC_SOLVE_PIPE
-#define SEC_SOLVE_PIPE 1
+#define SEC_SOLVE_PIPE 0
 #endif
 
 template <int K, int M, int R0, int NR, int J>
