@@ -85,6 +85,11 @@ enum sec_status {
                           Page-locking takes the process's memory-map lock, so it stalls
                           while other threads fault in or free memory: one 8 MiB encode
                           beside storb's piece copies took 6.4 ms locked, 0.55 ms staged */
+#define SEC_F_GPU_PARITY_IDS 16u /* sec_encode_pieces with digests only: the parity pieces'
+                          SHA-1 ids come from the GPU (sec_sha1_kernel on the parity while it
+                          is device-resident, one lane per piece, sub-batches of up to
+                          SEC_SLAB_BYTES_DIGEST input bytes) while the host threads hash the
+                          data pieces; without it the host threads hash every piece  */
 
 typedef struct sec_ctx sec_ctx;
 
@@ -235,7 +240,7 @@ int sec_encode_digest_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t n
  * and hashed on the context's host threads while the calling thread runs the GPU encode, the
  * parity pieces right after it; the call returns when every piece and digest is written.
  * Preconditions and errors as sec_encode_batch; SEC_EINVAL for a NULL piece buffer of a
- * non-empty chunk. */
+ * non-empty chunk.  Flags: SEC_F_HOST (required), SEC_F_STAGED, SEC_F_GPU_PARITY_IDS. */
 int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
                       uint8_t *const *pieces, uint8_t *digests, unsigned flags);
 

@@ -36,6 +36,7 @@ SEC_F_HOST = 1
 SEC_F_ASYNC = 2
 SEC_F_RECOVER = 4
 SEC_F_STAGED = 8
+SEC_F_GPU_PARITY_IDS = 16
 
 # zfec precondition failures (raised by zfec as zfec.Error)
 PRECONDITION_CODES = {SEC_EKM, SEC_EBLOCKLEN, SEC_ENBLOCKS, SEC_ESHARENUM, SEC_EDUPSHARE, SEC_EPADLEN, SEC_ESIZE}

@@ -781,7 +781,9 @@ int check_sharenums(int k, int m, const int32_t *s)
 uint64_t enc_B(const sec_enc_chunk &c) { return (c.n + (uint64_t)c.k - 1) / (uint64_t)c.k; }
 
 // ---- encode plan ------------------------------------------------------------
-int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, bool host, bool digest)
+// digest: 0 none, 1 every block's SHA-1 (sec_encode_digest_batch), 2 the parity blocks' only
+// (sec_encode_pieces with SEC_F_GPU_PARITY_IDS: digest slot s of a chunk's m - k)
+int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, bool host, int digest)
 {
     Plan &plan = ctx->enc_plan;
     TableCache &tc = ctx->enc_tabs;
@@ -866,7 +868,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             d.valid = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(valid, (int64_t)B));
             d.pad = 0;
             if (digest) {  // data blocks from the input (padding synthesised), then parity
-                for (int j = 0; j < c.k; ++j) {
+                for (int j = 0; j < c.k && digest == 1; ++j) {
                     const int64_t av = (int64_t)c.n - (int64_t)j * (int64_t)B;
                     msgs.push_back(sec::MsgDesc{d.in_off + (uint64_t)j * B, B,
                                                 (uint64_t)std::max<int64_t>(0, std::min<int64_t>(av, (int64_t)B)), 0,
@@ -874,7 +876,7 @@ int build_encode_plan(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
                 }
                 for (int r = 0; r < p; ++r)
                     msgs.push_back(sec::MsgDesc{d.par_off + (uint64_t)r * d.par_stride, B, B, 1, 0});
-                dig += (uint64_t)c.m;
+                dig += (uint64_t)(digest == 1 ? c.m : p);
             }
             sp.in_bytes += c.n;
             sp.out_bytes += (uint64_t)p * B;
@@ -2077,7 +2079,7 @@ bool host_direct(sec_ctx *ctx, const std::vector<HostRange> &rs, HostLock &lock,
 
 // sec_encode_batch (digests == nullptr, digest == false) and sec_encode_digest_batch.
 int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in, uint8_t *parity,
-                uint8_t *digests, unsigned flags, bool digest)
+                uint8_t *digests, unsigned flags, int digest)
 {
     if (!ctx || nchunks < 0 || (nchunks > 0 && !chunks) || (flags & ~(SEC_F_HOST | SEC_F_ASYNC | SEC_F_STAGED)) ||
         ((flags & SEC_F_STAGED) && !(flags & SEC_F_HOST)))
@@ -2138,7 +2140,7 @@ int encode_impl(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, cons
         memcpy(key.data(), chunks, sizeof(sec_enc_chunk) * (size_t)nchunks);
     }
     // ASYNC and STAGED do not change the plan
-    const unsigned kflags = (flags & ~(SEC_F_ASYNC | SEC_F_STAGED)) | (digest ? 0x10000u : 0u);
+    const unsigned kflags = (flags & ~(SEC_F_ASYNC | SEC_F_STAGED)) | ((unsigned)digest << 16);
     key.insert(key.end(), (const uint8_t *)&kflags, (const uint8_t *)&kflags + sizeof(unsigned));
     if (!(plan.valid && plan.gen == ctx->enc_tabs.gen && plan.key == key)) {
         plan.valid = false;
@@ -2192,13 +2194,13 @@ extern "C" {
 int sec_encode_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
                      uint8_t *parity, unsigned flags)
 {
-    return encode_impl(ctx, chunks, nchunks, in, parity, nullptr, flags, false);
+    return encode_impl(ctx, chunks, nchunks, in, parity, nullptr, flags, 0);
 }
 
 int sec_encode_digest_batch(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
                             uint8_t *parity, uint8_t *digests, unsigned flags)
 {
-    return encode_impl(ctx, chunks, nchunks, in, parity, digests, flags, true);
+    return encode_impl(ctx, chunks, nchunks, in, parity, digests, flags, 1);
 }
 
 // easyfec's Encoder.encode output for every chunk, as pieces in caller buffers: the k data
@@ -2212,8 +2214,10 @@ int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
                       uint8_t *const *pieces, uint8_t *digests, unsigned flags)
 {
     if (!ctx || nchunks < 0 || (nchunks > 0 && (!chunks || !pieces)) || !(flags & SEC_F_HOST) ||
-        (flags & ~(SEC_F_HOST | SEC_F_STAGED)))
+        (flags & ~(SEC_F_HOST | SEC_F_STAGED | SEC_F_GPU_PARITY_IDS)))
         return SEC_EINVAL;
+    // parity ids on the GPU: only with digests (else the flag changes nothing)
+    const bool gpu_ids = digests && (flags & SEC_F_GPU_PARITY_IDS);
     if (nchunks == 0)
         return SEC_OK;
     if (nchunks >= (int64_t)UINT32_MAX)
@@ -2239,7 +2243,11 @@ int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
     // own parity is larger alone), two scratch buffers in turn: sub-batch s + 1 encodes while the
     // task threads copy and hash sub-batch s's parity pieces.  Locked memory stays bounded by
     // 2 cap whatever the call's size (one allocation of the whole call's parity).
-    const uint64_t cap = std::max<uint64_t>((uint64_t)ctx->opt[O_SLAB_BYTES], max_par);
+    // With gpu_ids the GPU hashes a sub-batch's parity pieces in one chain time (one lane per
+    // piece), so the sub-batches are SEC_SLAB_BYTES_DIGEST: as many pieces in flight as it allows.
+    const uint64_t cap =
+        std::max<uint64_t>((uint64_t)ctx->opt[gpu_ids ? O_SLAB_BYTES_DIGEST : O_SLAB_BYTES], max_par);
+    std::vector<uint8_t> par_dig;  // gpu_ids: a sub-batch's parity digests, chunk by chunk
     sec::TaskPool &tp = tasks(ctx);
     sec::TaskPool::Group data, par[2];
     bool par_failed = false;
@@ -2291,16 +2299,35 @@ int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
             par[buf].failed.store(false);
             PinBuf &scratch = ctx->piece_par[buf];
             rc = scratch.ensure(po);
-            if (rc == SEC_OK)
+            if (rc == SEC_OK && gpu_ids) {
+                // parity and its ids in one staged call: the SHA-1 kernel runs on the device
+                // parity right after the encode (slots: each chunk's m - k, in chunk order)
+                uint64_t np = 0;
+                for (int64_t i = c0; i < c1; ++i)
+                    np += (uint64_t)(chunks[i].m - chunks[i].k);
+                try {
+                    par_dig.resize((size_t)np * 20);
+                } catch (const std::bad_alloc &) {
+                    rc = SEC_ENOMEM;
+                }
+                if (rc == SEC_OK)
+                    rc = encode_impl(ctx, tmp.data() + c0, c1 - c0, in, (uint8_t *)scratch.p, par_dig.data(),
+                                     SEC_F_HOST | (flags & SEC_F_STAGED), 2);
+                for (int64_t i = c0, q = 0; i < c1 && rc == SEC_OK; ++i)
+                    for (int r = 0; r < chunks[i].m - chunks[i].k; ++r, ++q)
+                        if (enc_B(chunks[i]) > 0)  // (an empty chunk's ids are sha1(b"") from above)
+                            memcpy(digests + (first_piece[i] + chunks[i].k + r) * 20, par_dig.data() + q * 20, 20);
+            } else if (rc == SEC_OK) {
                 rc = encode_impl(ctx, tmp.data() + c0, c1 - c0, in, (uint8_t *)scratch.p, nullptr,
-                                 SEC_F_HOST | (flags & SEC_F_STAGED), false);
+                                 SEC_F_HOST | (flags & SEC_F_STAGED), 0);
+            }
             for (int64_t i = c0; i < c1 && rc == SEC_OK; ++i) {
                 const sec_enc_chunk &c = chunks[i];
                 const uint64_t B = enc_B(c);
                 for (int r = 0; r < c.m - c.k && B > 0; ++r) {
                     uint8_t *dst = pieces[first_piece[i] + c.k + r];
                     const uint8_t *src = (const uint8_t *)scratch.p + tmp[i].parity_off + (uint64_t)r * B;
-                    uint8_t *dig = digests ? digests + (first_piece[i] + c.k + r) * 20 : nullptr;
+                    uint8_t *dig = digests && !gpu_ids ? digests + (first_piece[i] + c.k + r) * 20 : nullptr;
                     tp.submit(par[buf], [=] {
                         memcpy(dst, src, B);
                         return !dig || sec::sha1_padded(dst, B, B, dig);

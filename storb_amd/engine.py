@@ -23,7 +23,8 @@ import weakref
 import numpy as np
 
 from . import _lib
-from ._lib import COPY_DTYPE, DEC_DTYPE, ENC_DTYPE, MSG_DTYPE, SEC_F_ASYNC, SEC_F_HOST, SEC_F_RECOVER, SEC_F_STAGED
+from ._lib import (COPY_DTYPE, DEC_DTYPE, ENC_DTYPE, MSG_DTYPE, SEC_F_ASYNC, SEC_F_GPU_PARITY_IDS, SEC_F_HOST,
+                   SEC_F_RECOVER, SEC_F_STAGED)
 
 
 class Error(Exception):
@@ -307,12 +308,13 @@ class Engine:
         return out, layout
 
     def encode_pieces_into(self, chunks, shapes, piece_addrs, digests: np.ndarray | None = None,
-                           staged: bool = False) -> None:
+                           staged: bool = False, gpu_parity_ids: bool = False) -> None:
         """easyfec's Encoder.encode output for every chunk written to caller buffers
         (sec_encode_pieces): piece_addrs[M_c + j] = the address of a writable B-byte buffer for
         piece j of chunk c (M_c = sum of m over the chunks before c); digests (optional, a
         writable uint8 array of 20 bytes per piece) receives each piece's SHA-1, computed on the
-        library's host threads while the GPU encodes.  shapes: [(k, m)] per chunk."""
+        library's host threads while the GPU encodes (``gpu_parity_ids``: the parity pieces' on
+        the GPU, SEC_F_GPU_PARITY_IDS).  shapes: [(k, m)] per chunk."""
         n = len(chunks)
         descs = np.zeros(n, dtype=ENC_DTYPE)
         keep = []
@@ -327,7 +329,7 @@ class Engine:
             raise ValueError("encode_pieces_into: one piece address per piece")
         if digests is not None and digests.size < 20 * pa.size:
             raise ValueError("encode_pieces_into: digests needs 20 bytes per piece")
-        flags = SEC_F_HOST | (SEC_F_STAGED if staged else 0)
+        flags = SEC_F_HOST | (SEC_F_STAGED if staged else 0) | (SEC_F_GPU_PARITY_IDS if gpu_parity_ids else 0)
         if n:
             self._check(self.lib.sec_encode_pieces(self._ctx, _ptr(descs), n, None, _ptr(pa),
                                                    None if digests is None else _ptr(digests), flags))

@@ -104,6 +104,18 @@ STREAM_WINDOW_BYTES = 64 << 20  # chunk bytes per GPU call in the *_stream pipel
 # the GPU ids are off by default.
 GPU_PIECE_IDS = False
 STREAM_WINDOW_IDS_BYTES = 256 << 20
+# Round 6: with the host ids, the parity pieces' ids from the GPU instead
+# (sec_encode_pieces SEC_F_GPU_PARITY_IDS: the SHA-1 kernel on the device-resident parity, one
+# lane per piece, while the library's host threads hash only the data pieces), in windows of
+# STREAM_WINDOW_PARITY_IDS_BYTES so that hundreds of parity pieces share one chain time.
+# Measured on the 1 GiB upload (8 MiB chunks, zfec(16,24); profiles/r06_parity_ids.json): 3.96 /
+# 6.21 / 6.70 / 7.13 GiB/s at 64 / 256 / 512 / 1024 MiB windows against 5.97 / 6.82 / 6.82 / 6.91
+# with every id on the host threads.  Taking a third of the hashing off the host buys nothing:
+# the upload is bound by the host's memory work on the fresh piece buffers (first touch, copies),
+# and the GPU path adds a staged 512 MiB slab per window.  Off (F1 closed as host-only for the
+# upload; the flag stays in the ABI, tested).
+GPU_PARITY_IDS = False
+STREAM_WINDOW_PARITY_IDS_BYTES = 512 << 20
 STREAM_WORKERS = 4  # single-thread workers (one engine each) the *_stream pipelines are spread over
 
 
@@ -469,10 +481,11 @@ class _Done:
         return False
 
 
-def _encode_pieces(chunks: list, shapes: list, ids: bool):
+def _encode_pieces(chunks: list, shapes: list, ids: bool, gpu_parity_ids: bool = False):
     """Every chunk's m pieces as new bytes objects, filled by the library (sec_encode_pieces:
     the k data slices, zero-padded, then the parity), and with `ids` each piece's SHA-1 hex
-    (the library's host threads, OpenSSL: hashlib's bytes).  Returns (pieces, ids or None)."""
+    (the library's host threads, OpenSSL: hashlib's bytes; with `gpu_parity_ids` the parity
+    pieces' from the GPU SHA-1 kernel).  Returns (pieces, ids or None)."""
     objs, addrs = [], []
     for (k, m, B, _) in shapes:
         row = []
@@ -485,7 +498,8 @@ def _encode_pieces(chunks: list, shapes: list, ids: bool):
     # staged, not page-locked: the library's threads fault in the new pieces meanwhile, and locking
     # waits on the same memory-map lock (6.4 against 0.55 ms for one 8 MiB chunk on MI355X,
     # profiles/r03_upload_ab.jsonl)
-    get_engine().encode_pieces_into(chunks, [(k, m) for (k, m, _, _) in shapes], addrs, dig, staged=True)
+    get_engine().encode_pieces_into(chunks, [(k, m) for (k, m, _, _) in shapes], addrs, dig, staged=True,
+                                    gpu_parity_ids=ids and gpu_parity_ids)
     pieces = [[_finalize(b) for b, _ in row] for row in objs]
     hexes = None
     if ids:
@@ -825,8 +839,8 @@ def _encode_window(window: list, first_idx: int, piece_ids: bool):
             out = [_build(first_idx + i, k, m, B, padlen, len(c), ps)
                    for i, (c, (k, m, B, padlen), ps) in enumerate(zip(window, shapes, pieces))]
             return list(zip(out, ids)), err
-        if HOST_PIECES:  # ids by the library's host threads (OpenSSL), pieces in the same call
-            pieces, ids = _encode_pieces(list(window), shapes, True)
+        if HOST_PIECES:  # ids by the library's host threads (OpenSSL; parity ids on the GPU), pieces in the same call
+            pieces, ids = _encode_pieces(list(window), shapes, True, GPU_PARITY_IDS)
             out = [_build(first_idx + i, k, m, B, padlen, len(c), ps)
                    for i, (c, (k, m, B, padlen), ps) in enumerate(zip(window, shapes, pieces))]
             return list(zip(out, ids)), err
@@ -858,11 +872,14 @@ def encode_chunks_stream(chunks: Iterable[bytes], first_chunk_idx: int = 0, *, p
     `devices` / ``use_devices``: windows round robin over those devices, two per device in
     flight).  Yields ``EncodedChunk`` per chunk in order (chunk i gets index first_chunk_idx + i),
     or with ``piece_ids=True`` ``(EncodedChunk, [piece_hash of each of its m pieces])``; those ids
-    come from the GPU (GPU_PIECE_IDS) for windows of large pieces, whose default window is then
+    come from the library's host threads for the data pieces and from the GPU for the parity
+    pieces (GPU_PARITY_IDS; default window STREAM_WINDOW_PARITY_IDS_BYTES), or all from the GPU
+    (GPU_PIECE_IDS) for windows of large pieces, whose default window is then
     STREAM_WINDOW_IDS_BYTES."""
     wb = window_bytes
     if wb is None:
-        wb = STREAM_WINDOW_IDS_BYTES if piece_ids and GPU_PIECE_IDS else STREAM_WINDOW_BYTES
+        wb = (STREAM_WINDOW_IDS_BYTES if piece_ids and GPU_PIECE_IDS else
+              STREAM_WINDOW_PARITY_IDS_BYTES if piece_ids and HOST_PIECES and GPU_PARITY_IDS else STREAM_WINDOW_BYTES)
 
     def numbered():  # (window, index of its first chunk)
         idx = first_chunk_idx

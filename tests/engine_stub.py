@@ -62,7 +62,7 @@ class OracleHostEngine(Engine):
                 d[20 * j:20 * (j + 1)] = np.frombuffer(hashlib.sha1(blk).digest(), np.uint8)
                 j += 1
 
-    def encode_pieces_into(self, chunks, shapes, piece_addrs, digests=None, staged=False):
+    def encode_pieces_into(self, chunks, shapes, piece_addrs, digests=None, staged=False, gpu_parity_ids=False):
         """sec_encode_pieces on the oracle: every piece written to its address, its SHA-1 beside."""
         from oracle import cfec
 

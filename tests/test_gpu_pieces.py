@@ -31,7 +31,7 @@ def _shapes_and_chunks(rng):
     return out
 
 
-def _run(cases, digests=True):
+def _run(cases, digests=True, gpu_parity_ids=False):
     eng = get_engine()
     bufs, addrs = [], []
     for (k, m, B, _), _ in cases:
@@ -39,22 +39,57 @@ def _run(cases, digests=True):
         bufs.append(row)
         addrs += [a.ctypes.data for a in row]
     dig = np.zeros(20 * len(addrs), np.uint8) if digests else None
-    eng.encode_pieces_into([c for _, c in cases], [(k, m) for (k, m, _, _), _ in cases], addrs, dig)
+    eng.encode_pieces_into([c for _, c in cases], [(k, m) for (k, m, _, _), _ in cases], addrs, dig,
+                           gpu_parity_ids=gpu_parity_ids)
     return bufs, dig
 
 
-def test_pieces_and_ids_vs_oracle():
+@pytest.mark.parametrize("gpu_parity_ids", [False, True])
+def test_pieces_and_ids_vs_oracle(gpu_parity_ids):
+    """Every piece against the oracle, every id against hashlib; with gpu_parity_ids the parity
+    pieces' ids come from the GPU SHA-1 kernel (SEC_F_GPU_PARITY_IDS), the data pieces' from the
+    host threads, in one call over every shape (including m == k and an empty chunk)."""
     rng = random.Random(1)
     cases = _shapes_and_chunks(rng)
+    if gpu_parity_ids:
+        cases.append(((2, 3, 0, 0), b""))  # B = 0: every piece b"", ids sha1(b"")
     rng.shuffle(cases)  # shapes interleaved in one call
-    bufs, dig = _run(cases)
+    bufs, dig = _run(cases, gpu_parity_ids=gpu_parity_ids)
     j = 0
     for ((k, m, B, padlen), c), row in zip(cases, bufs):
-        want = cfec.easy_encode(c, k, m)
+        want = cfec.easy_encode(c, k, m) if c else [b""] * m
         assert [r.tobytes() for r in row] == want, (k, m, len(c))
         for w in want:
             assert dig[20 * j:20 * (j + 1)].tobytes() == hashlib.sha1(w).digest(), (k, m, len(c), j)
             j += 1
+
+
+def test_gpu_parity_ids_many_sub_batches():
+    """SEC_F_GPU_PARITY_IDS over more parity than one SEC_SLAB_BYTES_DIGEST sub-batch (the option
+    lowered to 1 MiB on a fresh engine): ids still land in each piece's own slot."""
+    from storb_amd.engine import Engine
+
+    rng = random.Random(5)
+    eng = Engine(0, options={"SEC_SLAB_BYTES_DIGEST": 1 << 20})
+    try:
+        cases = [(piece.chunk_shape(n), rng.randbytes(n)) for n in [(1 << 20) + 7, 600_001, 2 << 20, 1 << 20, 99_999]]
+        bufs, addrs = [], []
+        for (k, m, B, _), _ in cases:
+            row = [np.empty(B, np.uint8) for _ in range(m)]
+            bufs.append(row)
+            addrs += [a.ctypes.data for a in row]
+        dig = np.zeros(20 * len(addrs), np.uint8)
+        eng.encode_pieces_into([c for _, c in cases], [(k, m) for (k, m, _, _), _ in cases], addrs, dig,
+                               gpu_parity_ids=True)
+        j = 0
+        for ((k, m, B, _), c), row in zip(cases, bufs):
+            want = cfec.easy_encode(c, k, m)
+            assert [r.tobytes() for r in row] == want
+            for w in want:
+                assert dig[20 * j:20 * (j + 1)].tobytes() == hashlib.sha1(w).digest(), (k, m, len(c), j)
+                j += 1
+    finally:
+        eng.close()
 
 
 def test_pieces_without_ids_and_repeat_calls():
@@ -98,7 +133,9 @@ def test_encode_chunk_host_pieces_same_as_round4_path(n):
     assert [piece.piece_hash(p.data) for p in b.pieces] == [hashlib.sha1(p.data).hexdigest() for p in b.pieces]
 
 
-def test_encode_chunks_and_stream_host_pieces():
+@pytest.mark.parametrize("gpu_parity_ids", [False, True])
+def test_encode_chunks_and_stream_host_pieces(gpu_parity_ids, monkeypatch):
+    monkeypatch.setattr(piece, "GPU_PARITY_IDS", gpu_parity_ids)
     rng = random.Random(5)
     chunks = [rng.randbytes(rng.choice([3, 4096, 100_000, 300_001, 1 << 20])) for _ in range(12)]
     ecs = piece.encode_chunks(chunks, 4)

@@ -46,12 +46,17 @@ def main():
     ap.add_argument("--mib", type=int, default=1024)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--gpu-ids", action="store_true", help="also: piece ids from the GPU SHA-1, per window")
+    ap.add_argument("--parity-ids", action="store_true",
+                    help="only the upload stream: host ids vs GPU parity ids (GPU_PARITY_IDS) at 64..1024 MiB windows, "
+                         "rounds interleaved, ids checked against hashlib")
     ap.add_argument("--ab", action="store_true",
                     help="A/B in one process, rounds interleaved: STREAM_WORKERS 1 vs the default (a single stream "
                          "should not care), and encode_chunk's id hashing on fill vs after all pieces")
     a = ap.parse_args()
     if a.ab:
         return ab(a)
+    if a.parity_ids:
+        return parity_ids(a)
     from storb_amd import piece
 
     data = np.random.default_rng(3).integers(0, 256, a.mib << 20, dtype=np.uint8).tobytes()
@@ -128,6 +133,39 @@ def main():
             res[f"download_stream_{label}{sfx}"] = round(len(data) / best(down_stream, a.reps) / GIB, 3)
         Engine.LIBRARY_JOIN = True
     print(json.dumps(res, indent=1))
+
+
+def parity_ids(a):
+    """Upload stream (encode_chunks_stream(piece_ids=True)) with every id on the host threads
+    against the parity ids from the GPU, per window size; median over 3 rounds of best-of-reps."""
+    import hashlib
+
+    from storb_amd import piece
+
+    data = np.random.default_rng(3).integers(0, 256, a.mib << 20, dtype=np.uint8).tobytes()
+    cs = piece.piece_length(len(data))
+    parts = [data[o:o + cs] for o in range(0, len(data), cs)]
+    res = {}
+    for rnd in range(3):
+        for wm in (64, 256, 512, 1024):
+            for gp in (False, True):
+                def up(wm=wm, gp=gp):
+                    old = piece.GPU_PARITY_IDS
+                    piece.GPU_PARITY_IDS = gp
+                    try:
+                        return list(piece.encode_chunks_stream(iter(parts), piece_ids=True, window_bytes=wm << 20))
+                    finally:
+                        piece.GPU_PARITY_IDS = old
+                if rnd == 0:
+                    got = up()
+                    for ec, ids in got:
+                        assert ids == [hashlib.sha1(p.data).hexdigest() for p in ec.pieces]
+                    del got
+                res.setdefault(f"window_{wm}MiB_{'gpu_parity' if gp else 'host'}_ids", []).append(
+                    len(data) / best(up, a.reps) / GIB)
+    print(json.dumps({"object_bytes": len(data), "chunk_bytes": cs, "shape": list(piece.chunk_shape(cs)[:2]),
+                      "unit": "GiB/s, median of 3 rounds of best-of-%d" % a.reps,
+                      **{k: round(float(np.median(v)), 3) for k, v in res.items()}}, indent=1))
 
 
 def ab(a):
