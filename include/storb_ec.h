@@ -314,6 +314,11 @@ int sec_host_unregister(sec_ctx *ctx, void *hptr);
 /* SEC_F_HOST encode / decode calls so far on this context: zero-copy on the caller's pinned
  * buffers, zero-copy on pages the call locked itself, and staged. */
 int sec_ctx_host_paths(sec_ctx *ctx, int64_t *zero_copy, int64_t *registered, int64_t *staged);
+/* Pinned staging memory of the whole process (all contexts): bytes lent to host-mode calls in
+ * progress, and idle bytes the library keeps for the next call (at most 512 MiB; the rest is
+ * freed).  A context holds none between calls: its slabs and parity scratch are borrowed per
+ * call from one process-wide pool.  Either pointer may be NULL. */
+int sec_host_pinned_bytes(int64_t *loaned, int64_t *idle);
 /* Chunks with a lost data block decoded so far on this context, by method: `syndrome` (the
  * wide-decode path: bit-sliced syndromes of the present parity rows, then the e x e solve) and
  * `direct` (the decode matrix rows over all k blocks).  Which one a chunk takes is the library's

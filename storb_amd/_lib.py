@@ -115,6 +115,7 @@ _SIGS = {
     "sec_host_unregister": (ctypes.c_int, [_vp, _vp]),
     "sec_ctx_host_paths": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                           ctypes.POINTER(ctypes.c_int64)]),
+    "sec_host_pinned_bytes": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "sec_ctx_decode_paths": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "sec_ctx_decode_methods": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),

@@ -85,18 +85,99 @@ struct DevBuf {
     template <class T> T *as(size_t off = 0) const { return reinterpret_cast<T *>((char *)p + off); }
 };
 
+// Process-wide pool of pinned host buffers (hipHostMalloc; page-locked and mapped for every
+// device).  The staging buffers of host-mode calls (the pipeline slots' slabs, sec_encode_pieces'
+// parity scratch) are borrowed from it for the call and given back when the call returns, so a
+// context holds no locked memory between calls however many contexts a process opens (one per
+// caller thread: engine.get_engine); the pool keeps at most kPinKeep bytes of idle buffers for
+// the next call (reused without a new hipHostMalloc) and frees the rest, largest first.
+// sec_host_pinned_bytes reports both figures.  The pool is never destroyed (its buffers go with
+// the process), so no hipHostFree runs after the HIP runtime's teardown.
+constexpr size_t kPinKeep = (size_t)512 << 20;
+
+class PinPool {
+  public:
+    static PinPool &get()
+    {
+        static PinPool *pool = new PinPool;
+        return *pool;
+    }
+    // the smallest idle buffer of >= want bytes, else a new one; nullptr if hipHostMalloc fails
+    void *take(size_t want, size_t *cap)
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            auto it = idle_.lower_bound(want);
+            if (it != idle_.end()) {
+                void *p = it->second;
+                *cap = it->first;
+                idle_bytes_ -= it->first;
+                loaned_ += it->first;
+                idle_.erase(it);
+                return p;
+            }
+        }
+        void *p = nullptr;
+        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess)
+            return nullptr;
+        std::lock_guard<std::mutex> lk(mu_);
+        *cap = want;
+        loaned_ += want;
+        return p;
+    }
+    void give(void *p, size_t cap)
+    {
+        std::vector<void *> drop;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            loaned_ -= cap;
+            idle_.emplace(cap, p);
+            idle_bytes_ += cap;
+            while (idle_bytes_ > kPinKeep && !idle_.empty()) {
+                auto last = std::prev(idle_.end());
+                idle_bytes_ -= last->first;
+                drop.push_back(last->second);
+                idle_.erase(last);
+            }
+        }
+        for (void *q : drop)
+            (void)hipHostFree(q);
+    }
+    void stats(int64_t *loaned, int64_t *idle)
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (loaned)
+            *loaned = (int64_t)loaned_;
+        if (idle)
+            *idle = (int64_t)idle_bytes_;
+    }
+
+  private:
+    std::mutex mu_;
+    std::multimap<size_t, void *> idle_;
+    size_t idle_bytes_ = 0, loaned_ = 0;
+};
+
+// A pinned host buffer.  pooled (default): borrowed from PinPool, given back by release();
+// else its own hipHostMalloc (the context's small metadata staging).
 struct PinBuf {
     void *p = nullptr;
     size_t cap = 0;
+    bool pooled = true;
     int ensure(size_t bytes)
     {
         if (bytes <= cap)
             return SEC_OK;
-        if (p)
-            CK(hipHostFree(p));
-        p = nullptr;
-        cap = 0;
+        release();
         size_t want = std::max(bytes, (size_t)1 << 16);
+        if (pooled) {
+            p = PinPool::get().take(want, &cap);
+            if (!p) {
+                cap = 0;
+                return SEC_ENOMEM;
+            }
+            return SEC_OK;
+        }
         if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
             p = nullptr;
             return SEC_ENOMEM;
@@ -106,8 +187,12 @@ struct PinBuf {
     }
     void release()
     {
-        if (p)
-            (void)hipHostFree(p);
+        if (p) {
+            if (pooled)
+                PinPool::get().give(p, cap);
+            else
+                (void)hipHostFree(p);
+        }
         p = nullptr;
         cap = 0;
     }
@@ -558,7 +643,7 @@ struct sec_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending[4];
     std::vector<hipEvent_t> ev_pool;
     hipEvent_t stop_ev = nullptr;  // between timing_begin and timing_end of an attached launch
-    PinBuf pin;  // metadata image staging
+    PinBuf pin{nullptr, 0, false};  // metadata image staging (its own, not pooled: small, every call)
     hipEvent_t pin_ev = nullptr, meta_ev = nullptr;
     TableCache enc_tabs, dec_tabs;
     Plan enc_plan, dec_plan, sha_plan, bn_plan;
@@ -1424,6 +1509,10 @@ int run_pipeline(sec_ctx *ctx, Plan &plan, Gather gather, Scatter scatter, Launc
     }
     for (size_t j = 0; j < (size_t)kSlots; ++j)
         RC(slot_retire(ctx, ctx->slots[(i + j) % kSlots]));
+    for (Slot &sl : ctx->slots) {  // nothing in flight: the slabs go back to the process pool
+        sl.in.release();
+        sl.out.release();
+    }
     return SEC_OK;
 }
 
@@ -2344,6 +2433,8 @@ int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
         par_failed |= !tp.wait(g);
     if (rc == SEC_OK && (!ok_data || par_failed))
         rc = SEC_EINVAL;  // OpenSSL failed (no other cause)
+    for (PinBuf &b : ctx->piece_par)  // every task waited: the scratch goes back to the process pool
+        b.release();
     return rc;
 }
 
@@ -3051,6 +3142,12 @@ int sec_ctx_decode_methods(sec_ctx *ctx, int64_t *fused, int64_t *pair, int64_t 
         *two_kernel = ctx->syn_chunks - ctx->fused_chunks;
     if (direct)
         *direct = ctx->direct_chunks;
+    return SEC_OK;
+}
+
+int sec_host_pinned_bytes(int64_t *loaned, int64_t *idle)
+{
+    PinPool::get().stats(loaned, idle);
     return SEC_OK;
 }
 

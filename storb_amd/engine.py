@@ -589,6 +589,17 @@ def choose_blocks(k: int, m: int, sharenums) -> list[int] | None:
     return pick[:k].tolist()
 
 
+def pinned_bytes() -> tuple[int, int]:
+    """(loaned, idle): the process's pinned staging memory lent to host-mode calls in progress,
+    and kept idle for the next call (sec_host_pinned_bytes; contexts hold none between calls)."""
+    lib = _lib.load()
+    a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+    rc = lib.sec_host_pinned_bytes(ctypes.byref(a), ctypes.byref(b))
+    if rc:
+        raise ECRuntimeError(f"sec_host_pinned_bytes: {rc}")
+    return a.value, b.value
+
+
 def option_names() -> list[str]:
     """Every context option the library knows (sec_option_name)."""
     lib = _lib.load()
