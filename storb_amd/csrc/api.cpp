@@ -222,7 +222,6 @@ enum Opt {
     O_COPY_THREADS,      // 0 rule, or host copy-pool threads
     O_REGISTER_MIN,      // page-lock pageable host buffers for calls moving >= this many bytes (0: never)
     O_HOST_JOIN,         // 0: the GPU writes every byte of a host reassembly
-    O_BS_PAIR,           // zfec(64,96) encode: 1 two-wave workgroups sharing each block's subsets, 0 interleaved groups
     O_COUNT
 };
 
@@ -243,7 +242,6 @@ constexpr OptSpec kOpts[O_COUNT] = {
     {"SEC_COPY_THREADS", 0, 0, 256},
     {"SEC_REGISTER_MIN", (int64_t)4 << 20, 0, (int64_t)1 << 62},
     {"SEC_HOST_JOIN", 1, 0, 1},
-    {"SEC_BS_PAIR", 1, 0, 1},
 };
 
 struct Options {
@@ -498,12 +496,13 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
 // (C4's zfec(10,14), C5's (8,11), the policy's (8,12), (16,24), (32,48), (64,96)): every
 // position [0, B) of a chunk with B >= 16, ragged end included, so such a chunk gets no
 // sec_encode_kernel tile.  Tiles of SEC_BS_LANES lanes (default 256 = 8 KiB of each block).
-// A shape of several row groups ((64,96): 2 x 16 rows) runs them in one launch, a run of 8
-// tiles of each group in turn, so the tiles that read the same blocks share an XCD's L2.
-// SEC_BS = 0 turns the kernel off (then the v_perm rows), SEC_BS = 1 uses it for every shape it
-// has.  (Round 4's A/B forms -- one launch per group, (32,48) in 8-row groups, shared-transpose
-// wave pairs, LDS-staged small chunks -- are archived: tools/archive/.)
-constexpr int kBsAllGroups = 99;  // Group::U of an interleaved launch of every row group
+// The shape of two row groups ((64,96): 2 x 16 rows) runs both groups of a span in one two-wave
+// workgroup that shares each block's plane subsets through LDS (round 6; it replaced one launch
+// interleaving runs of 8 tiles of each group so that the tiles reading the same blocks shared
+// an XCD's L2: +3-16 %, profiles/r06_enc_ab.jsonl).  SEC_BS = 0 turns the kernel off (then the
+// v_perm rows), SEC_BS = 1 uses it for every shape it has.  (The A/B forms -- one launch per
+// group, (32,48) in 8-row groups, the interleaved launch, LDS-staged small chunks -- are
+// archived: tools/archive/.)
 constexpr int kBsPair = 98;       // Group::U of a two-wave launch, both row groups of a span per workgroup
 constexpr int kSolveLds = 1 << 16;  // phase-2 tile map keys of sec_solve_bs_lds_kernel launches
 constexpr int kSynWg2 = 1 << 16;    // phase-1 tile map keys of sec_syndrome_bs_pair_kernel launches
@@ -525,7 +524,7 @@ int bs_shape(const Options &o, int k, int m, uint64_t B)
 
 void add_bs_work(const Options &o, Bins &bins, uint32_t chunk, uint64_t B, int shape)
 {
-    if (sec_bs_groups(shape) > 1 && o[O_BS_PAIR]) {  // (64,96): one two-wave workgroup per span
+    if (sec_bs_groups(shape) > 1) {  // (64,96): one two-wave workgroup per span
         auto &bin = bins[{3, shape, kBsPair, 128, 0}];
         for (uint64_t t0 = 0; t0 < B; t0 += sec_bs_span())
             bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
@@ -533,23 +532,9 @@ void add_bs_work(const Options &o, Bins &bins, uint32_t chunk, uint64_t B, int s
     }
     const int lanes = o.lanes(O_BS_LANES);
     const uint64_t step = (uint64_t)sec_bs_span() * (lanes / 64);
-    // two row groups ((64,96)): one launch, flatten() interleaves the groups; else group 0
-    auto &bin = bins[{3, shape, sec_bs_groups(shape) > 1 ? kBsAllGroups : 0, lanes, 0}];
+    auto &bin = bins[{3, shape, 0, lanes, 0}];
     for (uint64_t t0 = 0; t0 < B; t0 += step)
         bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
-}
-
-// Tiles of an interleaved bit-sliced launch: runs of 8 positions, each run once per row group
-// (tile r0 = the group's first row), so a position's tiles are 8 workgroups apart (one XCD).
-void bs_interleave(int shape, const std::vector<sec::Tile> &pos, std::vector<sec::Tile> &out)
-{
-    const int ng = sec_bs_groups(shape), nr = sec_bs_rows(shape);
-    for (size_t i = 0; i < pos.size(); i += 8) {
-        const size_t e = std::min(pos.size(), i + 8);
-        for (int g = 0; g < ng; ++g)
-            for (size_t j = i; j < e; ++j)
-                out.push_back(sec::Tile{pos[j].chunk, pos[j].t0, (uint32_t)(g * nr), 0});
-    }
 }
 
 // XCD order.  Workgroup b of a launch is dispatched to XCD b % 8, so with the tiles in chunk
@@ -586,10 +571,7 @@ void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile
         if (kv.second.empty())
             continue;
         const size_t first = tiles.size();
-        if (std::get<0>(kv.first) == 3 && std::get<2>(kv.first) == kBsAllGroups)
-            bs_interleave(std::get<1>(kv.first), kv.second, tiles);
-        else
-            tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
+        tiles.insert(tiles.end(), kv.second.begin(), kv.second.end());
         groups.push_back(Group{std::get<1>(kv.first), std::get<2>(kv.first), std::get<3>(kv.first),
                                std::get<4>(kv.first), (uint32_t)first, (uint32_t)(tiles.size() - first),
                                std::get<0>(kv.first)});
@@ -997,8 +979,8 @@ int launch_encode_sub(sec_ctx *ctx, const Plan &plan, const SubPlan &sp, const u
     const sec::Tile *dt = plan.meta.as<sec::Tile>(sp.off_tiles);
     const uint32_t *tabs = ctx->enc_tabs.buf.as<uint32_t>();
     for (const Group &g : sp.groups) {
-        int e = g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsPair ? -2 : g.U == kBsAllGroups ? -1 : g.U,
-                                                   g.lanes, in, par, dd, dt + g.first, g.count, s)
+        int e = g.mfma == 3 ? sec_launch_encode_bs(g.rows, g.U == kBsPair ? -2 : g.U, g.lanes, in, par, dd,
+                                                   dt + g.first, g.count, s)
                             : sec_launch_encode(g.rows, g.U, g.wide, g.lanes, in, par, dd, dt + g.first, g.count, tabs, s);
         if (e)
             return hip_fail((hipError_t)e, g.mfma == 3 ? "sec_encode_bs_kernel" : "sec_encode_kernel");
@@ -2813,8 +2795,6 @@ int join_staged(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
     sec::TaskPool &tp = tasks(ctx);
     sec::TaskPool::Group g;
     std::vector<sec_dec_chunk> sub(chunks, chunks + nchunks);
-    for (const sec_dec_chunk &c : sub)
-        submit_row_copies(tp, g, c, sharenums, block_offs, block_avail, blocks, out);
     --ctx->staged_calls;  // the rows-only call counts this call's host path
     uint64_t nsl = 0;
     for (const sec_dec_chunk &c : sub)
@@ -2836,11 +2816,17 @@ int join_staged(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
             }
         }
     }
+    // The output's ranges are page-locked (or found unlockable) BEFORE the task threads start
+    // writing it: no registration of pages other threads are first-touching at the same time
+    // (round 6: one GPU run of tests/test_gpu_pieces.py::test_native_join_decode_host returned
+    // a wrong recovered chunk with the copies submitted first; not reproduced since).
     HostLock probe(ctx->stream());
     const bool from_out =
         probe.acquire(decode_ranges(sub.data(), (int64_t)sub.size(), sharenums, offs2.data(), avail2.data(), nullptr,
                                     out, false),
                       ctx->opt[O_REGISTER_MIN], !(flags & SEC_F_STAGED), true) != 0;
+    for (const sec_dec_chunk &c : sub)
+        submit_row_copies(tp, g, c, sharenums, block_offs, block_avail, blocks, out);
     int rc;
     if (from_out) {
         tp.wait(g);  // the present primaries are in `out` now

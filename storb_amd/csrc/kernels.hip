@@ -314,24 +314,8 @@ constexpr u32 lds_tab_bytes(u32 lanes) { return lds_tab<R, DEC>() ? lanes / 64 *
 #ifndef SEC_WIDE_BATCH
 #define SEC_WIDE_BATCH 8
 #endif
-//   SEC_FIXED_K                 A/B only: the k <= KB kernels assume every chunk has this k
-//                               (compile-time block count: no per-block branches, counted
-//                               waits); valid only for workloads of that single k
-#ifndef SEC_FIXED_K
-#define SEC_FIXED_K 0
-#endif
-//   SEC_DEC_WAVES / SEC_ENC_WAVES  A/B: minimum waves per SIMD the compiler must leave room
-//                               for (amdgpu_waves_per_eu, i.e. a VGPR cap) on the tile kernels
-#if defined(SEC_DEC_WAVES) && SEC_DEC_WAVES > 0
-#define SEC_DEC_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SEC_DEC_WAVES)))
-#else
-#define SEC_DEC_WAVES_ATTR
-#endif
-#if defined(SEC_ENC_WAVES) && SEC_ENC_WAVES > 0
-#define SEC_ENC_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SEC_ENC_WAVES)))
-#else
-#define SEC_ENC_WAVES_ATTR
-#endif
+//   (Rounds 1-5 also tried, and archived: a compile-time k for single-shape workloads, VGPR caps
+//   through amdgpu_waves_per_eu, LDS padding to cap the decode's workgroups per CU.)
 // Blocks (slots) per batch of a tile kernel: KB * U = the batch's 16 B vectors per lane
 template <int U, bool W, bool DEC>
 constexpr int batch_blocks()
@@ -383,7 +367,7 @@ __device__ __forceinline__ void encode_ragged(const u8 *__restrict__ in, u8 *__r
                                            const sec::Tile &tl, const u32 *__restrict__ tabs);
 
 template <int R, int U, bool W>
-__global__ __launch_bounds__(sec::max_lanes(R, U)) SEC_ENC_WAVES_ATTR void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+__global__ __launch_bounds__(sec::max_lanes(R, U)) void sec_encode_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
                                                          const sec::EncDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
                                                          const u32 *__restrict__ tabs)
@@ -401,7 +385,7 @@ template <int R, int U, bool W>
 __device__ __forceinline__ void encode_main(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d,
                                             const sec::Tile &tl, const u32 *__restrict__ tabs, u32 t)
 {
-    const u32 B = d.B, k = (!W && SEC_FIXED_K > 0) ? (u32)SEC_FIXED_K : d.k, valid = d.valid;
+    const u32 B = d.B, k = d.k, valid = d.valid;
     const u32 step = blockDim.x * sec::kLaneBytes;  // bytes one u-step of the workgroup covers
     u32 pos[U];
 #pragma unroll
@@ -558,7 +542,7 @@ __device__ __forceinline__ void decode_ragged(const u8 *__restrict__ blocks, u8 
 // KBX > 0: slots per load batch fixed at KBX (the plan sends only chunks with k <= KBX; fewer
 // live registers, more waves): recover-only and copy-free decodes, see api.cpp dec_small_kb
 template <int R, int U, bool W, int KBX>
-__global__ __launch_bounds__(sec::max_lanes(R, U)) SEC_DEC_WAVES_ATTR void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+__global__ __launch_bounds__(sec::max_lanes(R, U)) void sec_decode_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                          const sec::DecDesc *__restrict__ descs,
                                                          const sec::Tile *__restrict__ tiles,
                                                          const u32 *__restrict__ tabs,
@@ -620,7 +604,7 @@ __device__ __forceinline__ void decode_main(const u8 *__restrict__ blocks, u8 *_
                                             const u32 *__restrict__ tabs,
                                                          const sec::DecSlots sl)
 {
-    const u32 B = d.B, k = (!W && SEC_FIXED_K > 0) ? (u32)SEC_FIXED_K : d.k, valid = d.valid;
+    const u32 B = d.B, k = d.k, valid = d.valid;
     const u32 step = blockDim.x * sec::kLaneBytes;  // bytes one u-step of the workgroup covers
     u32 pos[U];
 #pragma unroll
@@ -1134,18 +1118,13 @@ hipError_t launch_enc(const u8 *in, u8 *par, const sec::EncDesc *descs, const se
                       lds_tab_bytes<batch_blocks<U, W, false>(), R, false>(lanes), s, in, par, descs, tiles, tabs);
 }
 
-// SEC_DEC_LDS_PAD (build knob, A/B): extra dynamic LDS bytes per decode workgroup, which caps
-// the workgroups a CU holds (160 KiB / pad) and so the waves per SIMD
-#ifndef SEC_DEC_LDS_PAD
-#define SEC_DEC_LDS_PAD 0
-#endif
 template <int R, int U, bool W, int KBX>
 hipError_t launch_dec(const u8 *blocks, u8 *out, const sec::DecDesc *descs, const sec::Tile *tiles, u32 ntiles,
                       const u32 *tabs, sec::DecSlots sl, u32 lanes, hipStream_t s)
 {
     constexpr int KB = KBX > 0 ? KBX : batch_blocks<U, W, true>();
     return launch_shm(sec_decode_kernel<R, U, W, KBX>, dim3(ntiles), dim3(lanes),
-                      lds_tab_bytes<KB, R, true>(lanes) + SEC_DEC_LDS_PAD, s, blocks, out, descs, tiles, tabs, sl);
+                      lds_tab_bytes<KB, R, true>(lanes), s, blocks, out, descs, tiles, tabs, sl);
 }
 
 template <int U, bool W>

@@ -148,10 +148,10 @@ int sec_launch_encode(int rows, int U, int wide, int lanes, const uint8_t *in, u
                       void *stream);
 // Bit-sliced compile-time-matrix encode (kernels_bs.hip) for the shapes sec_bs_shape knows
 // (else -1; rows = 0: the first kernel of that (k, m), else the one of `rows` rows per group):
-// all of [0, B) of chunks with B >= 16, row group `group` of sec_bs_groups(shape) (-1: every
-// group in one launch, each tile's r0 = group * sec_bs_rows(shape); -2, zfec(64,96) only: both
-// groups of one span per two-wave workgroup, one tile per span, `lanes` ignored), tiles of `lanes`
-// (64..256) lanes over lanes / 64 wave spans of sec_bs_span() positions
+// all of [0, B) of chunks with B >= 16: group 0 for the one-group shapes, tiles of `lanes`
+// (64..256) lanes over lanes / 64 wave spans of sec_bs_span() positions; group -2 for zfec(64,96)
+// (two row groups): both groups of one span per two-wave workgroup, one tile per span, `lanes`
+// ignored
 int sec_bs_shape(int k, int m, int rows = 0);
 int sec_bs_groups(int shape);
 int sec_bs_rows(int shape);

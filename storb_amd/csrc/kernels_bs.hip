@@ -105,17 +105,14 @@ __device__ __forceinline__ void transpose8(u32 (&x)[8])
     swap_bits<1, 0x55555555u>(x[6], x[7]);
 }
 
-// Block loads: nontemporal (streaming) in the one-group kernels, where every byte is read
-// once; cached in the interleaved two-group kernel, whose second group reads the blocks again
-// from L2 (measured: (64,96) +5-8 % cached, (16,24) -5 %, (32,48) even; r02_bs_ab.jsonl run 4).
-// SEC_BS_NT_LOAD (build knob, A/B): 0 = cached loads everywhere.
-#ifndef SEC_BS_NT_LOAD
-#define SEC_BS_NT_LOAD 1
-#endif
+// Block loads: nontemporal (streaming) in the one-group encode kernels, where every byte is read
+// once; cached elsewhere (the zfec(64,96) encode and the decode phases, whose blocks a second
+// wave or group reads again from L2; measured (64,96) +5-8 % cached, (16,24) -5 %, (32,48) even;
+// r02_bs_ab.jsonl run 4).
 template <bool NT>
 __device__ __forceinline__ u32x4 ld16(const u8 *p)
 {
-    if constexpr (NT && SEC_BS_NT_LOAD)
+    if constexpr (NT)
         return __builtin_nontemporal_load(reinterpret_cast<const u32x4_u *>(p));
     else
         return *reinterpret_cast<const u32x4_u *>(p);
@@ -238,17 +235,7 @@ __device__ __forceinline__ void all_blocks(std::integer_sequence<int, Js...>, u3
     (one_block<K, M, R0, NR, D, NT, Js>(acc, ring, src, B, pa, pb, valid), ...);
 }
 
-// SEC_BS_WAVES (build knob, A/B): minimum waves per SIMD (amdgpu_waves_per_eu, a VGPR cap)
-#if defined(SEC_BS_WAVES) && SEC_BS_WAVES > 0
-#define SEC_BS_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SEC_BS_WAVES)))
-#else
-#define SEC_BS_WAVES_ATTR
-#endif
-
 // ---- loads through an LDS ring filled by global_load_lds (k >= 32; see phase 1 below) --------
-#ifndef SEC_FUSED_LDS
-#define SEC_FUSED_LDS 1
-#endif
 #ifndef SEC_FUSED_LDS_RING
 #define SEC_FUSED_LDS_RING 8
 #endif
@@ -264,120 +251,12 @@ __device__ __forceinline__ void wait_vm()
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
-// Item addresses, one per lane (lane t: item t in `a`, item 64 + t in `b`), read with a
-// compile-time readlane: a per-item load of the slot table would be a vector load whose wait
-// drains every DMA in flight (the table is not provably unwritten, so it is no scalar load).
-struct ItemAddrs {
-    u64 a, b;
-};
-
-template <int J>
-__device__ __forceinline__ const u8 *item_addr(const ItemAddrs &ia)
-{
-    const u64 v = J < 64 ? ia.a : ia.b;
-    const u32 lo = __builtin_amdgcn_readlane((u32)v, J % 64), hi = __builtin_amdgcn_readlane((u32)(v >> 32), J % 64);
-    return reinterpret_cast<const u8 *>(((u64)hi << 32) | lo);
-}
-
-// loads issued after item J's when J is consumed: 2 per DMA item in (J, J + D)
-template <int K, int NI, int D, int J>
-constexpr int later_dmas()
-{
-    int n = 0;
-    for (int t = J + 1; t < J + D && t < NI; ++t)
-        n += t != K - 1 ? 2 : 0;
-    return n;
-}
-
-#if SEC_FUSED_LDS
-using FusedLds = LdsRing<SEC_FUSED_LDS_RING>;
-#else
-struct FusedLds {};
-#endif
 template <int K>
-using Phase1Lds = std::conditional_t<(K >= 32), FusedLds, char>;  // the LDS ring of k >= 32
-
-// SEC_ENC_LDS (build knob, A/B; default 0 = the register ring): 1 = the (32,48) encode reads its
-// blocks through an LDS ring of SEC_ENC_LDS_RING blocks per wave, 2 = every k >= 32 encode does.
-// Measured (r03_enc_lds_ab.jsonl): (32,48) +8-10 % on 512 KiB chunks but -14 % on 4 MiB and -7 %
-// on 32 MiB chunks; (64,96) -27 % (its two-group kernel takes 257 registers: 1 wave per SIMD),
-// even when capped at 256, and one launch per group with the ring (+20 % over the same without
-// it) still trails the two-group kernel's L2 reuse.
-#ifndef SEC_ENC_LDS
-#define SEC_ENC_LDS 0
-#endif
-#ifndef SEC_ENC_LDS_RING
-#define SEC_ENC_LDS_RING 8
-#endif
-template <int K>
-using EncLds = std::conditional_t<((SEC_ENC_LDS == 1 && K == 32) || (SEC_ENC_LDS == 2 && K >= 32)),
-                                  LdsRing<SEC_ENC_LDS_RING>, char>;
-
-// block J's two DMAs into its ring slot; the short last block K-1 goes to registers instead
-template <int K, int D, int J>
-__device__ __forceinline__ void enc_issue(LdsRing<D> &ring, u32 w, u32 (&xs)[8], const u8 *src, u64 B, u32 pa, u32 pb,
-                                          u32 valid)
-{
-    if constexpr (J == K - 1) {
-        load_block<false>(xs, src + (u64)J * B, pa, pb, valid, true);
-    } else {
-        const u8 *blk = src + (u64)J * B;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + pa),
-                                         (__attribute__((address_space(3))) void *)&ring.v[w][J % D][0][0], 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + pb),
-                                         (__attribute__((address_space(3))) void *)&ring.v[w][J % D][1][0], 16, 0, 0);
-    }
-}
-
-template <int K, int D, int... Js>
-__device__ __forceinline__ void enc_first(std::integer_sequence<int, Js...>, LdsRing<D> &ring, u32 w, u32 (&xs)[8],
-                                          const u8 *src, u64 B, u32 pa, u32 pb, u32 valid)
-{
-    (enc_issue<K, D, Js>(ring, w, xs, src, B, pa, pb, valid), ...);
-}
-
-template <int K, int M, int R0, int NR, int D, int J>
-__device__ __forceinline__ void enc_block_lds(u32 (&acc)[NR * 8], LdsRing<D> &ring, u32 w, u32 (&xs)[8],
-                                              const u8 *src, u64 B, u32 pa, u32 pb, u32 valid)
-{
-    u32 x[8];
-    if constexpr (J == K - 1) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            x[i] = xs[i];
-    } else {
-        wait_vm<later_dmas<K, K, D, J>()>();
-        const u32x4 a = ring.v[w][J % D][0][threadIdx.x & 63], b = ring.v[w][J % D][1][threadIdx.x & 63];
-        x[0] = a.x;
-        x[1] = a.y;
-        x[2] = a.z;
-        x[3] = a.w;
-        x[4] = b.x;
-        x[5] = b.y;
-        x[6] = b.z;
-        x[7] = b.w;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read before it is refilled
-    }
-    if constexpr (J + D < K)
-        enc_issue<K, D, J + D>(ring, w, xs, src, B, pa, pb, valid);
-    transpose8(x);
-    u32 lo[16], hi[16];
-    subsets(x[0], x[1], x[2], x[3], lo);
-    subsets(x[4], x[5], x[6], x[7], hi);
-    block_rows<K, M, R0, J, J == 0>(std::make_integer_sequence<int, NR * 8>{}, acc, lo, hi);
-}
-
-template <int K, int M, int R0, int NR, int D, int... Js>
-__device__ __forceinline__ void enc_blocks_lds(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], LdsRing<D> &ring,
-                                               u32 w, u32 (&xs)[8], const u8 *src, u64 B, u32 pa, u32 pb, u32 valid)
-{
-    (enc_block_lds<K, M, R0, NR, D, Js>(acc, ring, w, xs, src, B, pa, pb, valid), ...);
-}
+using Phase1Lds = std::conditional_t<(K >= 32), LdsRing<SEC_FUSED_LDS_RING>, char>;  // the LDS ring of k >= 32
 
 // One wave's span of one tile: rows [R0, R0 + NR) of the chunk's parity over the lane's pieces.
 template <int K, int M, int R0, int NR, int D, bool NT>
-__device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d, u32 s,
-                                        EncLds<K> &lring)
+__device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restrict__ par, const sec::EncDesc &d, u32 s)
 {
     static_assert(D >= 1 && D <= K, "ring depth");
     const u32 B = d.B;
@@ -388,20 +267,11 @@ __device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restric
     const u8 *src = in + d.in_off;
 
     u32 acc[NR * 8];
-    if constexpr (!std::is_same_v<EncLds<K>, char>) {
-        constexpr int DL = SEC_ENC_LDS_RING;
-        const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        u32 xs[8];
-        enc_first<K, DL>(std::make_integer_sequence<int, DL>{}, lring, w, xs, src, B, pa, pb, d.valid);
-        enc_blocks_lds<K, M, R0, NR, DL>(std::make_integer_sequence<int, K>{}, acc, lring, w, xs, src, B, pa, pb,
-                                         d.valid);
-    } else {
-        u32 ring[D][8];
+    u32 ring[D][8];
 #pragma unroll
-        for (int j = 0; j < D; ++j)
-            load_block<NT>(ring[j], src + (u64)j * B, pa, pb, d.valid, j == K - 1);
-        all_blocks<K, M, R0, NR, D, NT>(std::make_integer_sequence<int, K>{}, acc, ring, src, B, pa, pb, d.valid);
-    }
+    for (int j = 0; j < D; ++j)
+        load_block<NT>(ring[j], src + (u64)j * B, pa, pb, d.valid, j == K - 1);
+    all_blocks<K, M, R0, NR, D, NT>(std::make_integer_sequence<int, K>{}, acc, ring, src, B, pa, pb, d.valid);
 
     u8 *dst = par + d.par_off;
 #pragma unroll
@@ -421,7 +291,7 @@ __device__ __forceinline__ void bs_span(const u8 *__restrict__ in, u8 *__restric
 
 // Rows [R0, R0 + NR) of every tile.
 template <int K, int M, int R0, int NR, int D>
-__global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
+__global__ __launch_bounds__(256) void sec_encode_bs_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
                                                             const sec::EncDesc *__restrict__ descs,
                                                             const sec::Tile *__restrict__ tiles)
 {
@@ -430,29 +300,7 @@ __global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs_kernel(co
     const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
     if (s >= d.B)
         return;
-    __shared__ EncLds<K> lring;
-    bs_span<K, M, R0, NR, D, true>(in, par, d, s, lring);
-}
-
-// Two row groups in one launch, the tile's r0 picking one: the plan puts a run of 8 tiles of
-// group 0 and the same 8 positions of group 1 next in the launch, so each pair lands on one
-// XCD (workgroup b runs on XCD b % 8) at about the same time and the second reads the blocks
-// from that XCD's L2 instead of HBM.
-template <int K, int M, int NR, int D>
-__global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs2_kernel(const u8 *__restrict__ in, u8 *__restrict__ par,
-                                                             const sec::EncDesc *__restrict__ descs,
-                                                             const sec::Tile *__restrict__ tiles)
-{
-    const sec::Tile tl = tiles[blockIdx.x];
-    const sec::EncDesc d = descs[tl.chunk];
-    const u32 s = tl.t0 + (threadIdx.x >> 6) * kSpan;
-    if (s >= d.B)
-        return;
-    __shared__ EncLds<K> lring;  // one ring for both row-group variants
-    if (tl.r0 == 0)
-        bs_span<K, M, 0, NR, D, false>(in, par, d, s, lring);
-    else
-        bs_span<K, M, NR, NR, D, false>(in, par, d, s, lring);
+    bs_span<K, M, R0, NR, D, true>(in, par, d, s);
 }
 
 // ---- zfec(64,96) encode: both row groups of a span in one two-wave workgroup ----------------
@@ -464,11 +312,10 @@ __global__ __launch_bounds__(256) SEC_BS_WAVES_ATTR void sec_encode_bs2_kernel(c
 // 30 subset XORs through LDS, and takes the other wave's for the blocks 2i + 1 - g: 163 VALU per
 // block instead of 198, one barrier per pair of blocks, each block read from HBM once (no L2
 // re-read).  LDS: two steps of both waves' 8 x 16 bytes per lane, 32 KiB per workgroup.
-// SEC_BS_PAIR_PLANES (build knob, A/B): publish the 8 transposed planes instead (2 LDS stores and
-// loads per block instead of 8; the taker forms the subsets itself: 174 VALU per block).
-#ifndef SEC_BS_PAIR_PLANES
-#define SEC_BS_PAIR_PLANES 0
-#endif
+// Against the interleaved one-group-per-wave launch it replaced: 4.09 / 3.85 / 4.37 TB/s on
+// 1 MiB / 256 MiB / 64 MiB ragged chunks against 3.81 / 3.73 / 3.78; publishing the 8 transposed
+// planes instead (the taker forming the subsets) 3.27 / 3.09 / 3.32 (profiles/r06_enc_ab.jsonl;
+// both archived: tools/archive/README.md).
 
 struct PairXchg {
     u32x4 v[2][2][8][64];  // [step & 1][publishing wave][dword quad][lane]
@@ -496,12 +343,6 @@ __device__ __forceinline__ void pair_step(u32 (&acc)[NR * 8], u32 (&ring)[D][8],
     u32x4(&mine)[8][64] = xb.v[I & 1][G];
     u32x4(&theirs)[8][64] = xb.v[I & 1][1 - G];
     u32 lo[16], hi[16];
-#if SEC_BS_PAIR_PLANES
-    mine[0][l] = u32x4{x[0], x[1], x[2], x[3]};
-    mine[1][l] = u32x4{x[4], x[5], x[6], x[7]};
-    subsets(x[0], x[1], x[2], x[3], lo);
-    subsets(x[4], x[5], x[6], x[7], hi);
-#else
     subsets(x[0], x[1], x[2], x[3], lo);
     subsets(x[4], x[5], x[6], x[7], hi);
     mine[0][l] = u32x4{lo[1], lo[2], lo[3], lo[4]};
@@ -512,15 +353,9 @@ __device__ __forceinline__ void pair_step(u32 (&acc)[NR * 8], u32 (&ring)[D][8],
     mine[5][l] = u32x4{hi[6], hi[7], hi[8], hi[9]};
     mine[6][l] = u32x4{hi[10], hi[11], hi[12], hi[13]};
     mine[7][l] = u32x4{hi[14], hi[15], 0u, 0u};
-#endif
     block_rows<K, M, G * NR, J, I == 0>(std::make_integer_sequence<int, NR * 8>{}, acc, lo, hi);
     barrier_lds();  // both waves' step-I subsets are in LDS (and both finished reading step I-1's)
     u32 lo2[16], hi2[16];
-#if SEC_BS_PAIR_PLANES
-    const u32x4 t0 = theirs[0][l], t1 = theirs[1][l];
-    subsets(t0.x, t0.y, t0.z, t0.w, lo2);
-    subsets(t1.x, t1.y, t1.z, t1.w, hi2);
-#else
     const u32x4 t0 = theirs[0][l], t1 = theirs[1][l], t2 = theirs[2][l], t3 = theirs[3][l], t4 = theirs[4][l],
                 t5 = theirs[5][l], t6 = theirs[6][l], t7 = theirs[7][l];
     lo2[0] = hi2[0] = 0;
@@ -532,7 +367,6 @@ __device__ __forceinline__ void pair_step(u32 (&acc)[NR * 8], u32 (&ring)[D][8],
     hi2[6] = t5.x, hi2[7] = t5.y, hi2[8] = t5.z, hi2[9] = t5.w;
     hi2[10] = t6.x, hi2[11] = t6.y, hi2[12] = t6.z, hi2[13] = t6.w;
     hi2[14] = t7.x, hi2[15] = t7.y;
-#endif
     block_rows<K, M, G * NR, O, false>(std::make_integer_sequence<int, NR * 8>{}, acc, lo2, hi2);
 }
 
@@ -815,117 +649,26 @@ __device__ __forceinline__ void syn_items(std::integer_sequence<int, Js...>, u32
 }
 
 // ---- phase 1's loads for k >= 32: an LDS ring filled by global_load_lds (no VGPRs) ----------
-// SEC_FUSED_LDS (build knob): phase 1's blocks stream through a per-wave LDS ring of D slots
-// (two 1 KiB halves each, one global_load_lds_dwordx4 per half: lane l's 16 bytes land at
-// slot + 16 l), so D blocks are in flight without ring registers.  Every item issues its two
-// loads, an absent one from the chunk's first present data block (just read: an L2 hit), so
-// the loads issued after an item's are a compile-time count N and the wait for it is a plain
-// `s_waitcnt vmcnt(N)`: loads complete in order, so at most N outstanding retires it whatever
-// stores are in flight (a run-time count needs a branch per wait, which cost 80 VGPRs).  Data
-// block K-1 (possibly short, read in place) keeps the register path and is not counted
-// (waiting for fewer loads is stricter).  Used for k >= 32 (zfec(32,48), (64,96)), where it
-// measured +0-5 % reassembling and +7-16 % recover-only over the register ring; the small-k
-// shapes keep the register ring (LDS ring -8 % on (32,48) with 8 lost, -9 % (16,24), -20 % C4;
-// the direct decode is chosen there anyway), r03_syn_ab_lds.jsonl.
-template <int K, int NR, int R0, int D, int J, class Ring>
-__device__ __forceinline__ void lds_issue(Ring &ring, u32 w, u32 (&xs)[8], const SynCtx &c, const ItemAddrs &ia)
-{
-    const bool here = item_present<K, NR, R0>(c, J);
-    if constexpr (J == K - 1) {  // register path (short block k-1)
-        if (here)
-            load_syn_item<K, NR, R0, J>(xs, c);
-    } else {
-        const u8 *blk = item_addr<J>(ia);  // absent items: the first present data block
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + c.pa),
-                                         (__attribute__((address_space(3))) void *)&ring.v[w][J % D][0][0], 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(blk + c.pb),
-                                         (__attribute__((address_space(3))) void *)&ring.v[w][J % D][1][0], 16, 0, 0);
-    }
-}
-
-template <int K, int NR, int R0, int D, class Ring, int... Js>
-__device__ __forceinline__ void lds_first(std::integer_sequence<int, Js...>, Ring &ring, u32 w, u32 (&xs)[8],
-                                          const SynCtx &c, const ItemAddrs &ia)
-{
-    (lds_issue<K, NR, R0, D, Js>(ring, w, xs, c, ia), ...);
-}
-
-template <int K, int M, int R0, int NR, int D, bool FUSED, int J, class Ring>
-__device__ __forceinline__ void syn_item_lds(u32 (&acc)[NR * 8], Ring &ring, u32 w, u32 (&xs)[8],
-                                             const SynCtx &c, const ItemAddrs &ia, u8 *orow0, u32 B, u32 last,
-                                             bool copies, u8 *syn, u32 &q)
-{
-    constexpr int NI = K + NR;
-    u32 x[8];
-    if constexpr (J == K - 1) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            x[i] = xs[i];
-    } else {
-        wait_vm<later_dmas<K, NI, D, J>()>();
-        const u32x4 a = ring.v[w][J % D][0][threadIdx.x & 63], b = ring.v[w][J % D][1][threadIdx.x & 63];
-        x[0] = a.x;
-        x[1] = a.y;
-        x[2] = a.z;
-        x[3] = a.w;
-        x[4] = b.x;
-        x[5] = b.y;
-        x[6] = b.z;
-        x[7] = b.w;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read before it is refilled
-    }
-    if constexpr (J + D < NI)
-        lds_issue<K, NR, R0, D, J + D>(ring, w, xs, c, ia);
-    if (!item_present<K, NR, R0>(c, J))
-        return;
-    syn_process<K, M, R0, NR, FUSED, J>(acc, x, c, orow0, B, last, copies, syn, q);
-}
-
-template <int K, int M, int R0, int NR, int D, bool FUSED, class Ring, int... Js>
-__device__ __forceinline__ void syn_items_lds(std::integer_sequence<int, Js...>, u32 (&acc)[NR * 8], Ring &ring,
-                                              u32 w, u32 (&xs)[8], const SynCtx &c, const ItemAddrs &ia, u8 *orow0,
-                                              u32 B, u32 last, bool copies, u8 *syn, u32 &q)
-{
-    (syn_item_lds<K, M, R0, NR, D, FUSED, Js>(acc, ring, w, xs, c, ia, orow0, B, last, copies, syn, q), ...);
-}
-
-// lane t: item t's block (data t, or parity row R0 + t - K) and item 64 + t's; an absent item's
-// loads read the first present data block (before k-1: e < k - 1)
-template <int K, int NR, int R0>
-__device__ __forceinline__ ItemAddrs item_addrs(const SynCtx &c)
-{
-    constexpr int NI = K + NR;
-    const u32 t = threadIdx.x & 63;
-    const u32 first = (u32)__builtin_ctzll(c.dmask);
-    auto addr = [&](u32 it) -> u64 {
-        if (it >= (u32)NI)
-            return 0;
-        const bool here = it < (u32)K ? ((c.dmask >> it) & 1) : ((c.pmask >> (R0 + it - K)) & 1);
-        const u32 slot = !here ? first : it < (u32)K ? it : it + R0;
-        return (u64)(uintptr_t)(c.blocks + c.off[c.slot0 + slot]);
-    };
-    return ItemAddrs{addr(t), NI > 64 ? addr(64 + t) : 0};
-}
-
-// ---- phase 1's LDS ring in rank order (SEC_SYN_RANK, build knob; 0 = the ring above) ----------
-// The ring above gives every item a slot, absent ones included (a lost data block's slot reads a
-// present block again), so with half the blocks lost half the ring's depth holds no work and a
-// wave waits on memory for most of its life (sec_syndrome_bs_pair_kernel, 32 lost: SQ_WAIT_ANY 54 %
-// of wave cycles, profiles/r06_pmc_syn32.json).  Here the ring holds only the items a wave works on: the
-// present data blocks but K-1 and the group's present parity rows, in item order ("ranks"), so D
-// slots are D items of work ahead.  Rank r lies in slot r % D; its block address comes from a
-// per-lane table (lane r: rank r) by a run-time readlane.  Past the last rank the refills re-read
-// the last item (an L2 hit) into the slot just consumed, so every consume issues exactly two loads
-// and the wait is the compile-time s_waitcnt vmcnt(2 (D - 1)) whatever the erasure pattern.  Data
-// block K-1 (possibly short: the byte path) is read into registers before any ring load, so every
-// ring load is younger than it.  Measured neutral (sec_syndrome_bs_pair_kernel 573 / 544 us at 32 /
-// 24 lost against the round-5 ring's 567 / 545, profiles/r06_phase_stats_*.csv): the ring depth
-// is not what holds phase 1 back.  Letting the waits count the wave's own stores (so the ring runs
-// at its full depth in the copying wave) made it slower, 621 / 572 us (archived:
-// tools/archive/kernels_bs_r06_store_waits.diff).
-#ifndef SEC_SYN_RANK
-#define SEC_SYN_RANK 1
-#endif
+// Phase 1's items stream through a per-wave LDS ring of D slots (two 1 KiB halves each, one
+// global_load_lds_dwordx4 per half: lane l's 16 bytes land at slot + 16 l), so D items are in
+// flight without ring registers.  Against the register ring: +0-5 % reassembling, +7-16 %
+// recover-only on zfec(32,48) / (64,96); the small-k shapes keep the register ring (LDS ring -8 %
+// on (32,48) with 8 lost, -9 % (16,24), -20 % C4; the direct decode is chosen there anyway),
+// r03_syn_ab_lds.jsonl.  The ring holds only the items a wave works on: the present data blocks
+// but K-1 and the group's present parity rows, in item order ("ranks"), so D slots are D items of
+// work ahead.  Rank r lies in slot r % D; its block address comes from a per-lane table (lane r:
+// rank r) by a run-time readlane.  Past the last rank the refills re-read the last item (an L2
+// hit) into the slot just consumed, so every consume issues exactly two loads and the wait is
+// the compile-time s_waitcnt vmcnt(2 (D - 1)) whatever the erasure pattern: loads complete in
+// order, so at most that many outstanding retires the slot's, whatever stores are in flight.
+// Data block K-1 (possibly short: the byte path) is read into registers before any ring load,
+// so every ring load is younger than it.  Round 6 put the ring in rank order (round 5 gave
+// every item a slot, absent ones re-reading a present block): neutral, 573 / 544 us at 32 / 24
+// lost against 567 / 545 (profiles/r06_phase_stats_*.csv).  Letting the waits count the wave's
+// own stores (so the ring runs at its full depth in the copying wave) made it slower, 621 /
+// 572 us (tools/archive/kernels_bs_r06_store_waits.diff), and so did one ring shared by the
+// pair's two waves with each block read once, 606 / 621 us
+// (tools/archive/kernels_bs_r06_syn_share.diff): the ring depth is not what holds phase 1 back.
 
 struct RankRing {
     u64 a, b;  // lane r: the block address of rank r (a) and of rank 64 + r (b)
@@ -1042,23 +785,12 @@ __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__re
         acc[i] = 0;
     // syndrome row of this group's first present parity row: the present rows below R0
     u32 q = (u32)__builtin_popcountll(d.pmask & ((1ull << R0) - 1ull));
-#if SEC_FUSED_LDS
     if constexpr (K >= 32) {
         constexpr int DL = SEC_FUSED_LDS_RING;
         const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if SEC_SYN_RANK
         syn_items_rank<K, M, R0, NR, DL, false>(std::make_integer_sequence<int, K + NR>{}, acc, lring, w, c,
                                                 out + d.out_off, B, d.last, copies, syn + d.syn_off, q);
-#else
-        u32 xs[8];
-        const ItemAddrs ia = item_addrs<K, NR, R0>(c);
-        lds_first<K, NR, R0, DL>(std::make_integer_sequence<int, DL>{}, lring, w, xs, c, ia);
-        syn_items_lds<K, M, R0, NR, DL, false>(std::make_integer_sequence<int, K + NR>{}, acc, lring, w, xs, c, ia,
-                                               out + d.out_off, B, d.last, copies, syn + d.syn_off, q);
-#endif
-    } else
-#endif
-    {
+    } else {
         u32 ring[D][8];
         load_syn_first<K, NR, R0>(std::make_integer_sequence<int, D>{}, ring, c);
         syn_items<K, M, R0, NR, D, false>(std::make_integer_sequence<int, K + NR>{}, acc, ring, c, out + d.out_off,
@@ -1066,23 +798,10 @@ __device__ __forceinline__ void syn_span(const u8 *__restrict__ blocks, u8 *__re
     }
 }
 
-// SEC_SYN_WAVES / SEC_SOLVE_WAVES (build knobs, A/B): minimum waves per SIMD of the syndrome /
-// solve kernels (amdgpu_waves_per_eu, a register cap); 0 = the compiler's choice.
-#if defined(SEC_SYN_WAVES) && SEC_SYN_WAVES > 0
-#define SEC_SYN_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SEC_SYN_WAVES)))
-#else
-#define SEC_SYN_WAVES_ATTR
-#endif
-#if defined(SEC_SOLVE_WAVES) && SEC_SOLVE_WAVES > 0
-#define SEC_SOLVE_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SEC_SOLVE_WAVES)))
-#else
-#define SEC_SOLVE_WAVES_ATTR
-#endif
-
 // The scaled syndromes go to `syn` as bit planes; sec_solve_bs_kernel then solves for the lost
 // blocks.
 template <int K, int M, int NR, int D>
-__global__ __launch_bounds__(256) SEC_SYN_WAVES_ATTR void sec_syndrome_bs_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
+__global__ __launch_bounds__(256) void sec_syndrome_bs_kernel(const u8 *__restrict__ blocks, u8 *__restrict__ out,
                                                               u8 *__restrict__ syn,
                                                               const sec::SynDesc *__restrict__ descs,
                                                               const sec::Tile *__restrict__ tiles,
@@ -1112,7 +831,7 @@ __global__ __launch_bounds__(256) SEC_SYN_WAVES_ATTR void sec_syndrome_bs_kernel
 // from HBM (1.55 GB read per GiB decoded at e = 32 where the blocks are 1.07,
 // profiles/r04_syn_pmc.json); here the two waves read them together and the second read hits L2.
 template <int K, int M, int NR, int D>
-__global__ __launch_bounds__(128) SEC_SYN_WAVES_ATTR void sec_syndrome_bs_pair_kernel(
+__global__ __launch_bounds__(128) void sec_syndrome_bs_pair_kernel(
     const u8 *__restrict__ blocks, u8 *__restrict__ out, u8 *__restrict__ syn, const sec::SynDesc *__restrict__ descs,
     const sec::Tile *__restrict__ tiles, const sec::SynSlots sl)
 {
@@ -1264,7 +983,7 @@ __device__ __forceinline__ void solve_group(std::integer_sequence<int, Gs...>, u
 
 // Tiles carry the row group's first data row in r0 (groups of NR rows).
 template <int K, int M, int NR, int D>
-__global__ __launch_bounds__(256) SEC_SOLVE_WAVES_ATTR void sec_solve_bs_kernel(const u8 *__restrict__ syn, u8 *__restrict__ out,
+__global__ __launch_bounds__(256) void sec_solve_bs_kernel(const u8 *__restrict__ syn, u8 *__restrict__ out,
                                                            const sec::SolveDesc *__restrict__ descs,
                                                            const sec::Tile *__restrict__ tiles,
                                                            const uint64_t *__restrict__ masks)
@@ -1285,49 +1004,10 @@ __global__ __launch_bounds__(256) SEC_SOLVE_WAVES_ATTR void sec_solve_bs_kernel(
 // waves, wave w solving 8-row group w: the e rows (2 KiB each) come into LDS once by
 // global_load_lds (spread over the waves), then every wave reads them from LDS.  LDS = e rounded
 // up to 8 rows x 2 KiB (dynamic), at most 64 KiB.
-// s_waitcnt vmcnt(v) for the largest v in {0, 2, 4, 6, 8, 12} not above n (n wave-uniform): a
-// run-time count as one asm statement (a ladder of scalar branches the compiler does not see, so
-// it costs no registers); waiting for fewer outstanding loads than n is stricter, never wrong
-__device__ __forceinline__ void wait_vm_le(u32 n)
-{
-    asm volatile("s_cmp_ge_u32 %0, 12\n\t"
-                 "s_cbranch_scc1 1f\n\t"
-                 "s_cmp_ge_u32 %0, 8\n\t"
-                 "s_cbranch_scc1 2f\n\t"
-                 "s_cmp_ge_u32 %0, 6\n\t"
-                 "s_cbranch_scc1 3f\n\t"
-                 "s_cmp_ge_u32 %0, 4\n\t"
-                 "s_cbranch_scc1 4f\n\t"
-                 "s_cmp_ge_u32 %0, 2\n\t"
-                 "s_cbranch_scc1 5f\n\t"
-                 "s_waitcnt vmcnt(0)\n\t"
-                 "s_branch 9f\n"
-                 "1:\n\t"
-                 "s_waitcnt vmcnt(12)\n\t"
-                 "s_branch 9f\n"
-                 "2:\n\t"
-                 "s_waitcnt vmcnt(8)\n\t"
-                 "s_branch 9f\n"
-                 "3:\n\t"
-                 "s_waitcnt vmcnt(6)\n\t"
-                 "s_branch 9f\n"
-                 "4:\n\t"
-                 "s_waitcnt vmcnt(4)\n\t"
-                 "s_branch 9f\n"
-                 "5:\n\t"
-                 "s_waitcnt vmcnt(2)\n"
-                 "9:" ::"s"(n)
-                 : "scc", "memory");
-}
 
-// The syndrome rows come into LDS in chunks of 8 (16 halves of 1 KiB, 16 / W per wave, all issued
-// up front); SEC_SOLVE_PIPE (build knob, A/B): 1 = a wave starts on chunk c once chunk c has
-// landed (its own loads waited, then a barrier), so the first rows are solved while the rest are
-// in flight; 0 = every row waited before the first is solved (default: the pipelined form took
-// 446 / 368 us against 409 / 330 at 32 / 24 lost, profiles/r06_phase_stats_*.csv).
-#ifndef SEC_SOLVE_PIPE
-#define SEC_SOLVE_PIPE 0
-#endif
+// Every syndrome row lands before the first is solved.  Round 6 tried starting on each chunk of
+// 8 rows once it had landed (a wave's own loads waited, then a barrier per chunk): 446 / 368 us at
+// 32 / 24 lost against 409 / 330 (profiles/r06_phase_stats_*.csv; tools/archive/README.md).
 
 template <int K, int M, int R0, int NR, int J>
 __device__ __forceinline__ void solve_item_lds(u32 (&acc)[NR * 8], const u32x4 (*sy)[2][64], uint64_t pmask,
@@ -1336,14 +1016,6 @@ __device__ __forceinline__ void solve_item_lds(u32 (&acc)[NR * 8], const u32x4 (
     if (!((pmask >> J) & 1))
         return;
     const u32 q = (u32)__builtin_popcountll(pmask & ((1ull << J) - 1ull));
-#if SEC_SOLVE_PIPE
-    if ((q & 7) == 0) {  // the first row of chunk q / 8: its loads (every wave's) have landed
-        constexpr u32 per = 16 / (K / NR);  // each wave's loads per chunk
-        const u32 chunks = ((u32)__builtin_popcountll(pmask) + 7) / 8;
-        wait_vm_le(per * (chunks - 1 - (q >> 3)));
-        __syncthreads();
-    }
-#endif
     const u32x4 a = sy[q][0][lane], b = sy[q][1][lane];
     u32 lo[16], hi[16];
     subsets(a.x, a.y, a.z, a.w, lo);
@@ -1399,30 +1071,12 @@ __global__ __launch_bounds__(64 * (K / NR)) void sec_solve_bs_lds_kernel(const u
     const u8 *base = syn + d.syn_off + s + 16 * lane;  // rows hold whole spans: no clamping
     const u64 stride = sec::syn_stride(d.B);
     const u32 e = (u32)__builtin_popcountll(d.pmask);
-#if SEC_SOLVE_PIPE
-    // chunk c = rows [8c, 8c + 8) = halves [16c, 16c + 16); wave w loads halves 16c + w + W t.  A
-    // chunk's rows past e (the LDS holds e rounded up to 8 rows) load row e - 1 again, so every
-    // wave issues the same count per chunk and a chunk's wait is a count of later chunks' loads.
-    static_assert(16 % W == 0, "waves per chunk");
-    const u32 chunks = (e + 7) / 8;
-    for (u32 c = 0; c < chunks; ++c)
-        for (u32 t = 0; t < 16 / W; ++t) {
-            const u32 i = 16 * c + w + W * t, row = min(i >> 1, e - 1);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(base + (u64)row * stride + (i & 1) * 1024),
-                                             (__attribute__((address_space(3))) void *)&sy[i >> 1][i & 1][0], 16, 0, 0);
-        }
-    if (!((d.lost >> (w * NR)) & ((1ull << NR) - 1ull))) {  // no lost row in this wave's group
-        wait_vm<0>();  // its loads have landed before it leaves (a finished wave leaves the barriers)
-        return;
-    }
-#else
     const u32 n = 2 * e;  // 1 KiB halves of the e rows
     for (u32 i = w; i < n; i += W)
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(base + (u64)(i >> 1) * stride + (i & 1) * 1024),
                                          (__attribute__((address_space(3))) void *)&sy[i >> 1][i & 1][0], 16, 0, 0);
     wait_vm<0>();
     __syncthreads();
-#endif
     solve_groups_lds<K, M, NR>(std::make_integer_sequence<int, W>{}, w, sy, d, masks, out, s, lane);
 }
 
@@ -1475,23 +1129,12 @@ __device__ __forceinline__ void fused_span(const u8 *__restrict__ blocks, u8 *__
     for (int i = 0; i < NRP * 8; ++i)
         acc[i] = 0;
     u32 q = 0;  // every present parity row is in this group
-#if SEC_FUSED_LDS
     if constexpr (K >= 32) {
         constexpr int DL = SEC_FUSED_LDS_RING;
         const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if SEC_SYN_RANK
         syn_items_rank<K, M, RP0, NRP, DL, true>(std::make_integer_sequence<int, K + NRP>{}, acc, lring, w, c,
                                                  out + d.out_off, B, d.last, copies, nullptr, q);
-#else
-        u32 xs[8];
-        const ItemAddrs ia = item_addrs<K, NRP, RP0>(c);
-        lds_first<K, NRP, RP0, DL>(std::make_integer_sequence<int, DL>{}, lring, w, xs, c, ia);
-        syn_items_lds<K, M, RP0, NRP, DL, true>(std::make_integer_sequence<int, K + NRP>{}, acc, lring, w, xs, c, ia,
-                                                out + d.out_off, B, d.last, copies, nullptr, q);
-#endif
-    } else
-#endif
-    {
+    } else {
         u32 ring[D][8];
         load_syn_first<K, NRP, RP0>(std::make_integer_sequence<int, D>{}, ring, c);
         syn_items<K, M, RP0, NRP, D, true>(std::make_integer_sequence<int, K + NRP>{}, acc, ring, c,
@@ -1535,9 +1178,6 @@ hipError_t launch_bs(int lanes, const u8 *in, u8 *par, const sec::EncDesc *d, co
     if constexpr (R0 == -2)
         hipExtLaunchKernelGGL((sec_encode_bs_pair_kernel<K, M, NR, D>), dim3(nt), dim3(128), 0, s, (hipEvent_t)a,
                               (hipEvent_t)b, 0, in, par, d, t);
-    else if constexpr (R0 < 0)
-        hipExtLaunchKernelGGL((sec_encode_bs2_kernel<K, M, NR, D>), dim3(nt), dim3(lanes), 0, s, (hipEvent_t)a,
-                              (hipEvent_t)b, 0, in, par, d, t);
     else
         hipExtLaunchKernelGGL((sec_encode_bs_kernel<K, M, R0, NR, D>), dim3(nt), dim3(lanes), 0, s, (hipEvent_t)a,
                               (hipEvent_t)b, 0, in, par, d, t);
@@ -1547,12 +1187,6 @@ hipError_t launch_bs(int lanes, const u8 *in, u8 *par, const sec::EncDesc *d, co
 // Shapes: (k, m, rows per launch).  Ring depths from the register budget (8 NR accumulators
 // + 8 D ring dwords per lane) and A/Bs: zfec(16,24) keeps 10 of its 16 blocks in flight
 // (182 VGPRs; +2-8 % over 4 on 1 and 16 MiB chunks), C4 5 (10: -2 %), the 16-row groups 2;
-// SEC_BS_RING (build knob, A/B) sets one depth for every shape.
-#ifdef SEC_BS_RING
-#define RING_K(k, d) (SEC_BS_RING < (k) ? SEC_BS_RING : (k))
-#else
-#define RING_K(k, d) (d)
-#endif
 // own blocks in flight per wave of the pair kernel
 #ifndef SEC_BS_PAIR_RING
 #define SEC_BS_PAIR_RING 2
@@ -1584,22 +1218,20 @@ int sec_launch_encode_bs(int shape, int group, int lanes, const uint8_t *in, uin
 {
     if (ntiles == 0)
         return hipSuccess;
-    if (lanes < 64 || lanes > 256 || lanes % 64 || shape < 0 || shape >= kNShapes || group < -2)
+    if (lanes < 64 || lanes > 256 || lanes % 64 || shape < 0 || shape >= kNShapes || (group != 0 && group != -2))
         return hipErrorInvalidValue;
     hipStream_t s = (hipStream_t)stream;
-    // group -1: every row group in one launch (sec_encode_bs2_kernel, the two-group (64,96)),
-    // tiles carry r0; -2: both groups of a span in one two-wave workgroup (sec_encode_bs_pair_kernel,
-    // one tile per span); 0: the one-group shapes
+    // group -2: both groups of a span in one two-wave workgroup (sec_encode_bs_pair_kernel, the
+    // two-group zfec(64,96), one tile per span); 0: the one-group shapes
     if (group == -2)
-        return shape == 4 ? launch_bs<64, 96, -2, 16, RING_K(64, SEC_BS_PAIR_RING)>(128, in, par, descs, t, ntiles, s)
+        return shape == 4 ? launch_bs<64, 96, -2, 16, SEC_BS_PAIR_RING>(128, in, par, descs, t, ntiles, s)
                           : hipErrorInvalidValue;
     switch (shape * 4 + group + 1) {
-    case 1: return launch_bs<10, 14, 0, 4, RING_K(10, 5)>(lanes, in, par, descs, t, ntiles, s);
-    case 5: return launch_bs<8, 12, 0, 4, RING_K(8, 4)>(lanes, in, par, descs, t, ntiles, s);
-    case 9: return launch_bs<16, 24, 0, 8, RING_K(16, 10)>(lanes, in, par, descs, t, ntiles, s);
-    case 13: return launch_bs<32, 48, 0, 16, RING_K(32, 2)>(lanes, in, par, descs, t, ntiles, s);
-    case 16: return launch_bs<64, 96, -1, 16, RING_K(64, 2)>(lanes, in, par, descs, t, ntiles, s);
-    case 21: return launch_bs<8, 11, 0, 3, RING_K(8, 4)>(lanes, in, par, descs, t, ntiles, s);
+    case 1: return launch_bs<10, 14, 0, 4, 5>(lanes, in, par, descs, t, ntiles, s);
+    case 5: return launch_bs<8, 12, 0, 4, 4>(lanes, in, par, descs, t, ntiles, s);
+    case 9: return launch_bs<16, 24, 0, 8, 10>(lanes, in, par, descs, t, ntiles, s);
+    case 13: return launch_bs<32, 48, 0, 16, 2>(lanes, in, par, descs, t, ntiles, s);
+    case 21: return launch_bs<8, 11, 0, 3, 4>(lanes, in, par, descs, t, ntiles, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -1617,11 +1249,9 @@ hipError_t launch_syn(int lanes, const u8 *blocks, u8 *out, u8 *syn, const sec::
 }
 
 // phase-2 rows per group: (10,14) 10, (8,*) 8, the rest 16
-// SEC_SOLVE_NR (build knob, A/B): rows per phase-2 group of the k >= 32 shapes (16 or 8)
-#ifndef SEC_SOLVE_NR
-#define SEC_SOLVE_NR 8
-#endif
-constexpr int solve_nr(int k) { return k <= 16 ? k : SEC_SOLVE_NR; }
+// (k >= 32 in groups of 8 rows; groups of 16, four waves per span: -9 % at 32 lost, +4-6 % on
+// random 16-30 % losses, profiles/r06_syn_ab_rank_pipe_snr16.jsonl)
+constexpr int solve_nr(int k) { return k <= 16 ? k : 8; }
 
 template <int K, int M, int D>
 hipError_t launch_solve(int lanes, const u8 *syn, u8 *out, const sec::SolveDesc *d, const sec::Tile *t, u32 nt,
@@ -1750,12 +1380,12 @@ int sec_launch_syndrome_bs(int shape, int lanes, const uint8_t *blocks, uint8_t 
     hipStream_t s = (hipStream_t)stream;
     switch (shape) {  // ring depths as the encode's (kernels' register budgets are alike); the
                       // 16-row groups' SEC_SYN_RING (build knob, A/B)
-    case 0: return launch_syn<10, 14, 4, RING_K(10, 5)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
-    case 1: return launch_syn<8, 12, 4, RING_K(8, 4)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
-    case 2: return launch_syn<16, 24, 8, RING_K(16, 10)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 0: return launch_syn<10, 14, 4, 5>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 1: return launch_syn<8, 12, 4, 4>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 2: return launch_syn<16, 24, 8, 10>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
     case 3: return launch_syn<32, 48, 16, SEC_SYN_RING>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
     case 4: return launch_syn<64, 96, 16, SEC_SYN_RING>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
-    case 5: return launch_syn<8, 11, 3, RING_K(8, 4)>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
+    case 5: return launch_syn<8, 11, 3, 4>(lanes, blocks, out, syn, descs, t, ntiles, sl, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -106,7 +106,7 @@ def test_options_listed_with_defaults_and_no_environment_reads():
     # round 5 archived the A/B-only options with their kernels: at most 12
     # remain, each forcing a shipped path or sizing the host pipeline
     assert len(names) <= 12, names
-    for gone in ("SEC_BS_LDS", "SEC_DEC_LDS", "SEC_SYN_PAIR", "SEC_SOLVE_LDS", "SEC_SYN_WG2",
+    for gone in ("SEC_BS_LDS", "SEC_DEC_LDS", "SEC_BS_PAIR", "SEC_SYN_PAIR", "SEC_SOLVE_LDS", "SEC_SYN_WG2",
                  "SEC_TILE_U", "SEC_STAGE_DMA", "SEC_EXACT_LANES", "SEC_RAGGED_KERNEL"):
         assert gone not in names, gone
     lib = _lib.load()

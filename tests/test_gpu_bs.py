@@ -7,7 +7,7 @@ The kernel serves zfec(10,14) (BASELINE C4), (8,11) (C5's RS(8,3)) and the polic
 zero padding read past `valid`.  Cases: B from 16 bytes to several tiles, B just under / at /
 over one span, not a multiple of 16 or of the span, padlen 0 and k-1, mixed with shapes the
 kernel does not serve in one batch, 64 / 128 / 256-lane tiles, (64,96)'s two row groups in one
-two-wave workgroup per span (the default) or in the interleaved one-group-per-wave launch, (32,48) in one pass or two groups, host (staged) and
+two-wave workgroup per span sharing each block's plane subsets, host (staged) and
 device-resident calls with a padded parity stride; "off" (SEC_BS=0) is the v_perm / xb path
 for the same chunks.
 """
@@ -44,8 +44,6 @@ MODES = {
     "all128": {"SEC_BS": 1, "SEC_BS_LANES": 128},
     "all64": {"SEC_BS": 1, "SEC_BS_LANES": 64},
     "off": {"SEC_BS": 0},
-    # zfec(64,96) in the interleaved one-group-per-wave kernel instead of the two-wave pair kernel
-    "bs2": {"SEC_BS_PAIR": 0},
 }
 
 
@@ -76,13 +74,13 @@ def test_encode_bit_sliced_shapes_host(mode):
     eng.close()
 
 
-@pytest.mark.parametrize("k,m,pair", [(k, m, 1) for k, m in BS_SHAPES] + [(64, 96, 0)])
-def test_encode_bit_sliced_device_padded_stride(k, m, pair):
+@pytest.mark.parametrize("k,m", BS_SHAPES)
+def test_encode_bit_sliced_device_padded_stride(k, m):
     """Device-resident chunks back to back (unaligned block starts), parity blocks at a stride
     larger than B: the kernel writes exactly [0, B) of each parity block and nothing between."""
     from storb_amd.engine import Engine
 
-    engine = Engine(0, options={"SEC_BS": 1, "SEC_BS_PAIR": pair})
+    engine = Engine(0, options={"SEC_BS": 1})
     rng = random.Random(k * 7 + m)
     n = 4096 * k + 2 * k + 3 if k > 3 else 40000
     B = -(-n // k)

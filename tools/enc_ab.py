@@ -4,7 +4,10 @@ device-resident.  Rates are TB/s of algorithmic bytes (n read + (m - k) B writte
 HIP-event kernel time of the encode call.  Every variant's parity is compared with the first
 variant's (the GPU suite checks the kernels against the oracle).  Not product code.
 
-    python tools/enc_ab.py [--rounds 3] [--reps 5] [--variants "pair,bs2@SEC_BS_PAIR=0,planes/planes"]
+    python tools/enc_ab.py [--rounds 3] [--reps 5] [--variants "cur,r05/r05"]
+
+(Round 6 compared the pair kernel with the interleaved launch through the context option
+SEC_BS_PAIR, since archived with that kernel; a variant is now a prebuilt library.)
 """
 
 from __future__ import annotations
@@ -39,7 +42,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="pair,bs2@SEC_BS_PAIR=0",
+    ap.add_argument("--variants", default="cur,r05/r05",
                     help="name@OPT=V+OPT2=V2[/tag]: context options per variant, optionally a prebuilt variant "
                          "library build/variants/libstorbec_<tag>.so")
     ap.add_argument("--cases", default="")

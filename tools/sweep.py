@@ -23,6 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 VARIANTS = {
+    # build knobs of kernels.hip / api.cpp that remain (each a measured design parameter; the
+    # A/B-only knobs and their kernels are archived, tools/archive/README.md)
     "base": {},  # defaults: nontemporal loads + stores, 16-vector load batches
     "tmp": {"SEC_NT_LOAD": 0, "SEC_NT_STORE": 0},  # temporal (cached) loads and stores
     "decb8": {"SEC_DEC_BATCH": 8},  # default is 16: all slot loads up front for k * U <= 16
@@ -31,78 +33,35 @@ VARIANTS = {
     "dst0": {"SEC_DEC_ST": 0},
     "est2": {"SEC_ENC_ST": 2},
     "est3": {"SEC_ENC_ST": 3},
-    "nogf": {"SEC_PROBE_NOGF": 1},
-    "pipe": {"SEC_SOLVE_PIPE": 1},  # (archived: tools/archive/kernels_bs_r05_solve_pipe.diff)  # calibration: the product kernels' traffic with no GF arithmetic
     "est0": {"SEC_ENC_ST": 0},
     "est2dst2": {"SEC_ENC_ST": 2, "SEC_DEC_ST": 2},
     "dst3": {"SEC_DEC_ST": 3},
-    "xcd": {"SEC_XCD_ORDER": 1},  # api.cpp: XCD order for every group (default: decode full tiles)
-    "noxcd": {"SEC_XCD_ORDER": 0},
+    # calibration: the product kernels' traffic with no GF arithmetic (outputs are not parity)
+    "nogf": {"SEC_PROBE_NOGF": 1},
+    "xcd": {"SEC_XCD_ORDER": 1},  # api.cpp: XCD order for every tile group (default off)
     "eb4": {"SEC_ENC_BATCH": 4},
+    "eb8": {"SEC_ENC_BATCH": 8},
     "db8": {"SEC_DEC_BATCH": 8},  # decode KB = 8 / U (valid only for k * U <= 8)
     "db8eb8": {"SEC_DEC_BATCH": 8, "SEC_ENC_BATCH": 8},
     "b4": {"SEC_DEC_BATCH": 4, "SEC_ENC_BATCH": 4},  # KB = 4 / U: valid for k * U <= 4 only
     "decearly": {"SEC_DEC_LATE": 0},  # decode: copies stored as each slot arrives
-    "nowide": {"SEC_WIDE_K": 0},  # A/B only: drops the k > 16 loop (register cost)  # encode: KB * U = 4 vectors per batch
-    "eb8": {"SEC_ENC_BATCH": 8},  # default (-1): XCD order for decode groups of full tiles only
-    "xcd_dst0": {"SEC_XCD_ORDER": 1, "SEC_DEC_ST": 0},
-    "xcd_dst2": {"SEC_XCD_ORDER": 1, "SEC_DEC_ST": 2},
-    # compile-time k (kernels.hip SEC_FIXED_K): valid only on a workload of that one k
-    "fk4": {"SEC_FIXED_K": 4},
-    "fk8": {"SEC_FIXED_K": 8},
-    "fk10": {"SEC_FIXED_K": 10},
     # wide k (W kernels): the earlier 16-vector batches without block pairs for 8-row groups;
     # 4-vector batches; pairs for 8-row groups in the k <= 16 kernels too
     "prevwide": {"SEC_WIDE_BATCH": 16, "SEC_WIDE_PAIR_ROWS": 4},
     "wb4": {"SEC_WIDE_BATCH": 4},
     "pair8": {"SEC_PAIR_ROWS": 8},
-    # launch bound of the > 4-row kernels (VGPR cap: 1024 lanes leave 128), with / without pairs
-    "lb256": {"SEC_LB_WIDE_ROWS": 256},
-    "sha1pf": {"SEC_SHA1_PF": 1},  # SHA-1 next-block prefetch on (the default) / off
-    "sha1nopf": {"SEC_SHA1_PF": 0},
+    "sha1nopf": {"SEC_SHA1_PF": 0},  # SHA-1 next-block prefetch off (default on)
     "sha1d1": {"SEC_SHA1_DEPTH": 1},  # prefetch depth in blocks (default 2)
     "sha1d3": {"SEC_SHA1_DEPTH": 3},
-    "sha1d4": {"SEC_SHA1_DEPTH": 4},
-    "lb256p8": {"SEC_LB_WIDE_ROWS": 256, "SEC_PAIR_ROWS": 8},
-    "lb512p8": {"SEC_LB_WIDE_ROWS": 512, "SEC_PAIR_ROWS": 8},
     # table dwords 1 and 3 from a per-wave LDS copy instead of v_mov from SGPRs (SEC_LDS_TAB)
     # (default 2: encode kernels of 8-row groups only; 1: every tile kernel; 0: none)
     "ldstab": {"SEC_LDS_TAB": 1},
-    "ldstab_fk10": {"SEC_LDS_TAB": 1, "SEC_FIXED_K": 10},
     "noldstab": {"SEC_LDS_TAB": 0},
-    # bit-sliced encode (kernels_bs.hip): one ring depth (blocks in flight) for every shape
-    "bsr2": {"SEC_BS_RING": 2},
-    "bsr3": {"SEC_BS_RING": 3},
-    "bsr4": {"SEC_BS_RING": 4},
-    "bsr6": {"SEC_BS_RING": 6},
-    "bsr8": {"SEC_BS_RING": 8},
-    "bsr10": {"SEC_BS_RING": 10},
-    "bsr12": {"SEC_BS_RING": 12},
-    "bsr16": {"SEC_BS_RING": 16},
-    "bsld": {"SEC_BS_NT_LOAD": 0},  # bit-sliced encode with cached (not streaming) loads
-    "bsw3": {"SEC_BS_WAVES": 3},  # bit-sliced encode capped for 3 waves per SIMD
-    "bsw2": {"SEC_BS_WAVES": 2, "SEC_ENC_LDS": 2},  # (64,96) LDS-ring encode capped at 256 registers
     # syndrome decode ring depths: phase 1 of the 16-row groups, phase 2 (solve), the fused kernel
     "synr4": {"SEC_SYN_RING": 4, "SEC_SOLVE_RING": 4},
     "fr2": {"SEC_FUSED_RING": 2},
-    "fr6": {"SEC_FUSED_RING": 6},
-    "nolds": {"SEC_FUSED_LDS": 0},  # fused syndrome decode: register ring instead of the LDS-DMA ring
+    "fr4": {"SEC_FUSED_RING": 4},
     "lds6": {"SEC_FUSED_LDS_RING": 6},
-    # bit-sliced k >= 32 encode through the LDS-DMA ring (kernels_bs.hip SEC_ENC_LDS; default 0,
-    # the register ring): (32,48) only, every k >= 32; ring depths
-    "noencl": {"SEC_ENC_LDS": 0},
-    "encl1": {"SEC_ENC_LDS": 1},
-    "encl2": {"SEC_ENC_LDS": 2},
-    "encl4": {"SEC_ENC_LDS": 1, "SEC_ENC_LDS_RING": 4},
-    "encl6": {"SEC_ENC_LDS": 1, "SEC_ENC_LDS_RING": 6},
-    # decode workgroups per CU capped through padding LDS (160 KiB per CU): 3 or 2 per CU
-    "dpad3": {"SEC_DEC_LDS_PAD": 50000},
-    "dpad2": {"SEC_DEC_LDS_PAD": 60000},
-    # VGPR caps through amdgpu_waves_per_eu on the tile kernels (decode<2,1> is 104 VGPRs = 4
-    # waves per SIMD, encode<4,1> 109)
-    "dw5": {"SEC_DEC_WAVES": 5},
-    "dw6": {"SEC_DEC_WAVES": 6},
-    "ew5": {"SEC_ENC_WAVES": 5},
 }
 
 
