@@ -94,6 +94,8 @@ struct DevBuf {
 // sec_host_pinned_bytes reports both figures.  The pool is never destroyed (its buffers go with
 // the process), so no hipHostFree runs after the HIP runtime's teardown.
 constexpr size_t kPinKeep = (size_t)512 << 20;
+// Against contexts that keep their staging between calls (round 5), per call and on the 1 GiB
+// streams: level within the boxes' spread (profiles/r06_pin_return_ab.txt).
 
 class PinPool {
   public:
