@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <map>
@@ -1978,6 +1979,7 @@ namespace {
 struct HostRange {
     uintptr_t a;
     uint64_t len;
+    bool out = false;  // the kernels write it (a decode's output, an encode's parity)
 };
 
 std::vector<HostRange> encode_ranges(const sec_enc_chunk *chunks, int64_t nchunks, const uint8_t *in,
@@ -1989,7 +1991,7 @@ std::vector<HostRange> encode_ranges(const sec_enc_chunk *chunks, int64_t nchunk
         const uint64_t B = (c.n + (uint64_t)c.k - 1) / (uint64_t)c.k, p = (uint64_t)(c.m - c.k);
         r.push_back(HostRange{(uintptr_t)in + c.in_off, c.n});
         if (p && B)
-            r.push_back(HostRange{(uintptr_t)parity + c.parity_off, (p - 1) * c.parity_stride + B});
+            r.push_back(HostRange{(uintptr_t)parity + c.parity_off, (p - 1) * c.parity_stride + B, true});
     }
     return r;
 }
@@ -2001,7 +2003,7 @@ std::vector<HostRange> decode_ranges(const sec_dec_chunk *chunks, int64_t nchunk
     std::vector<HostRange> r;
     for (int64_t i = 0; i < nchunks; ++i) {
         const sec_dec_chunk &c = chunks[i];
-        r.push_back(HostRange{(uintptr_t)out + c.out_off, dec_nout(c, sharenums, recover)});
+        r.push_back(HostRange{(uintptr_t)out + c.out_off, dec_nout(c, sharenums, recover), true});
         for (int j = 0; j < c.k; ++j)
             r.push_back(HostRange{(uintptr_t)blocks + block_offs[c.slot0 + j], slot_avail(c, block_avail, j)});
     }
@@ -2088,6 +2090,9 @@ public:
                 return 0;
             if (dry)
                 return 2;
+            for (const HostRange &r : rs)
+                if (r.out && r.len && !pinned(r.a, r.len, &cache))
+                    fault_in(r.a, r.len);
             bool ok = true;
             for (auto &q : merged) {
                 if (tl.touches(q.first, q.second - q.first) ||
@@ -2125,6 +2130,25 @@ public:
 
 private:
     static constexpr uintptr_t kPageMask = 4095;
+
+    // Every page of [a, a + len) the kernels will write and the process has not touched yet
+    // (mincore: not resident) is faulted in writable by the CPU first, by an atomic OR of 0 into
+    // one byte of the range on that page (no value changes, and no store of another thread to
+    // that byte can be lost), so no output page is unbacked when the device maps it.  Round 6
+    // saw one wrong reassembled row whose output pages the host had never touched (DESIGN §5
+    // Round 6).  Resident pages cost nothing but the one mincore call.
+    static void fault_in(uintptr_t a, uint64_t len)
+    {
+        const uintptr_t lo = a & ~kPageMask, hi = (a + len + kPageMask) & ~kPageMask;
+        const size_t np = (hi - lo) >> 12;
+        std::vector<unsigned char> res(np, 0);
+        const bool known = mincore((void *)lo, hi - lo, res.data()) == 0;
+        for (size_t i = 0; i < np; ++i)
+            if (!known || !(res[i] & 1)) {
+                const uintptr_t b = std::max<uintptr_t>(a, lo + (i << 12));
+                (void)__atomic_fetch_or((uint8_t *)b, (uint8_t)0, __ATOMIC_RELAXED);
+            }
+    }
     static constexpr uintptr_t kGap = (uintptr_t)4 << 20;
     void unlock_all(TransientLocks &tl)  // tl.mu held
     {
@@ -2797,6 +2821,8 @@ int join_staged(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
     sec::TaskPool &tp = tasks(ctx);
     sec::TaskPool::Group g;
     std::vector<sec_dec_chunk> sub(chunks, chunks + nchunks);
+    for (const sec_dec_chunk &c : sub)
+        submit_row_copies(tp, g, c, sharenums, block_offs, block_avail, blocks, out);
     --ctx->staged_calls;  // the rows-only call counts this call's host path
     uint64_t nsl = 0;
     for (const sec_dec_chunk &c : sub)
@@ -2818,17 +2844,13 @@ int join_staged(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
             }
         }
     }
-    // The output's ranges are page-locked (or found unlockable) BEFORE the task threads start
-    // writing it: no registration of pages other threads are first-touching at the same time
-    // (round 6: one GPU run of tests/test_gpu_pieces.py::test_native_join_decode_host returned
-    // a wrong recovered chunk with the copies submitted first; not reproduced since).
+    // (a dry run: whether the rows-only call would page-lock these ranges; it locks them itself,
+    // after the copies have landed)
     HostLock probe(ctx->stream());
     const bool from_out =
         probe.acquire(decode_ranges(sub.data(), (int64_t)sub.size(), sharenums, offs2.data(), avail2.data(), nullptr,
                                     out, false),
                       ctx->opt[O_REGISTER_MIN], !(flags & SEC_F_STAGED), true) != 0;
-    for (const sec_dec_chunk &c : sub)
-        submit_row_copies(tp, g, c, sharenums, block_offs, block_avail, blocks, out);
     int rc;
     if (from_out) {
         tp.wait(g);  // the present primaries are in `out` now
