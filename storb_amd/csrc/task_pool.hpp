@@ -270,8 +270,11 @@ inline int usable_cpus()
     return q > 0 ? std::min(n, q) : n;
 }
 
-// The default pool size: half the usable CPUs (the calling threads work too), at most 7
-inline int default_pool_threads() { return std::min(7, std::max(1, usable_cpus() / 2)); }
+// The default pool size: the usable CPUs but two (for the calling threads, which mostly wait
+// on the pool during its calls), at most 14.  Against half the CPUs capped at 7 (rounds 1-5), on
+// a 16-CPU quota: the 1 GiB upload stream (piece copies + SHA-1 ids) +17 to +49 %, an 8 MiB
+// chunk's encode + ids -17 %, downloads and small calls level (profiles/r06_pool_threads_ab.txt).
+inline int default_pool_threads() { return std::min(14, std::max(1, usable_cpus() - 2)); }
 
 // The process's pool of `nthreads` threads, created on first use and shared by every holder; it
 // ends with its last holder.

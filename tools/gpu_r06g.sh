@@ -1,11 +1,12 @@
 #!/bin/bash
-# Round 6: per-call staging returned to the process pool (this build) against contexts that keep
+# Round 6 (VAR=pinkeep, the default): per-call staging returned to the process pool (this build) against contexts that keep
 # their staging between calls (build/variants/libstorbec_pinkeep.so, SEC_PIN_RETURN=0): the
-# small-call profile and the 1 GiB stream rates, each library twice, alternating.
+# small-call profile and the 1 GiB stream rates, each library twice, alternating.  VAR=pool14: the
+# library task pool at 14 threads (SEC_POOL_THREADS_MAX=14, _DIV=1) against 7.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out; mkdir -p $O; cd $R
 export TMPDIR=/tmp
-V=$R/build/variants/libstorbec_pinkeep.so
+V=$R/build/variants/libstorbec_${VAR:-pinkeep}.so
 for i in 1 2; do
   for L in pool keep; do
     if [ $L = keep ]; then export STORB_EC_LIB=$V; else unset STORB_EC_LIB; fi
