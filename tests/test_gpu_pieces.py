@@ -148,6 +148,27 @@ def test_encode_chunks_and_stream_host_pieces(gpu_parity_ids, monkeypatch):
         assert ids == [hashlib.sha1(w).hexdigest() for w in want]
 
 
+def test_native_join_decode_host_fresh_outputs_repeated():
+    """The shape that once returned a wrong chunk: an all-present 8 MiB chunk
+    beside 8 MiB chunks with data piece 0 lost, reassembled into fresh output objects whose lost
+    rows' pages the host never touched before the GPU writes them (page-locked for the call), in
+    several rounds, each against the source bytes."""
+    eng = get_engine()
+    rng = random.Random(21)
+    n = 8 << 20
+    k, m, B, padlen = piece.chunk_shape(n)
+    srcs = [rng.randbytes(n) for _ in range(3)]
+    blocks = [cfec.easy_encode(d, k, m) for d in srcs]
+    items = []
+    for i, (d, bl) in enumerate(zip(srcs, blocks)):
+        lost = () if i == 0 else (0,) if i == 1 else (0, 5)
+        keep = [j for j in range(m) if j not in lost][:k]
+        items.append((k, m, [bl[j] for j in keep], keep, padlen))
+    for _ in range(8):
+        assert eng.decode_host_chunks(items) == srcs
+        assert eng.decode_host(items) == b"".join(srcs)
+
+
 def test_pieces_bytes_are_immutable_objects():
     """The pieces are ordinary bytes objects (filled in place before anyone sees them)."""
     ec = piece.encode_chunk(b"abc" * 50_000, 0)
