@@ -669,7 +669,7 @@ int set_dev(const sec_ctx *ctx)
     return SEC_OK;
 }
 
-// O_COPY_THREADS, or the CPUs this process may use (affinity and cgroup quota) but two, at most 14
+// O_COPY_THREADS, or half the CPUs this process may use (affinity and cgroup quota), at most 7
 int host_threads(const sec_ctx *ctx)
 {
     return ctx->opt[O_COPY_THREADS] ? (int)ctx->opt[O_COPY_THREADS] : sec::default_pool_threads();

@@ -270,11 +270,24 @@ inline int usable_cpus()
     return q > 0 ? std::min(n, q) : n;
 }
 
-// The default pool size: the usable CPUs but two (for the calling threads, which mostly wait
-// on the pool during its calls), at most 14.  Against half the CPUs capped at 7 (rounds 1-5), on
-// a 16-CPU quota: the 1 GiB upload stream (piece copies + SHA-1 ids) +17 to +49 %, an 8 MiB
-// chunk's encode + ids -17 %, downloads and small calls level (profiles/r06_pool_threads_ab.txt).
-inline int default_pool_threads() { return std::min(14, std::max(1, usable_cpus() - 2)); }
+// The default pool size: half the usable CPUs (the calling threads work too), at most 7.
+// SEC_POOL_DIV / SEC_POOL_RESERVE / SEC_POOL_MAX (build knobs, A/B): min(MAX, usable / DIV -
+// RESERVE).  Round 6 measured all but two of a 16-CPU quota (14 threads): the 1 GiB upload
+// stream +17 to +49 %, but C5 end to end from pinned memory 47.3 -> 36.0 GiB/s (more runnable
+// threads than the quota: the cgroup is throttled), profiles/r06_pool_threads_ab.txt.
+#ifndef SEC_POOL_DIV
+#define SEC_POOL_DIV 2
+#endif
+#ifndef SEC_POOL_RESERVE
+#define SEC_POOL_RESERVE 0
+#endif
+#ifndef SEC_POOL_MAX
+#define SEC_POOL_MAX 7
+#endif
+inline int default_pool_threads()
+{
+    return std::min(SEC_POOL_MAX, std::max(1, usable_cpus() / SEC_POOL_DIV - SEC_POOL_RESERVE));
+}
 
 // The process's pool of `nthreads` threads, created on first use and shared by every holder; it
 // ends with its last holder.

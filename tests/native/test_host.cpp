@@ -83,8 +83,8 @@ static void test_shared_pool_concurrent()
     EXPECT(a.get() == b.get());
     EXPECT(sec::shared_pool(3).get() != a.get());
     EXPECT(sec::usable_cpus() >= 1);
-    EXPECT(sec::default_pool_threads() >= 1 && sec::default_pool_threads() <= 14 &&
-           sec::default_pool_threads() <= std::max(1, sec::usable_cpus() - 2));
+    EXPECT(sec::default_pool_threads() >= 1 && sec::default_pool_threads() <= 7 &&
+           sec::default_pool_threads() <= std::max(1, sec::usable_cpus() / 2));
     std::vector<std::thread> th;
     std::atomic<int> bad{0};
     for (int t = 0; t < 6; ++t)
