@@ -640,6 +640,7 @@ struct sec_ctx {
     // host threads (staging copies, joins, sec_encode_pieces' piece copies and SHA-1): the
     // process's pool of this context's size, shared with every other context of that size
     std::shared_ptr<sec::TaskPool> tasks;
+    std::shared_ptr<sec::TaskPool> hash_tasks;  // sec_encode_pieces' piece copies + SHA-1 (SEC_HASH_POOL)
     // sec_encode_pieces: the parity of one sub-batch before its piece copies, two sub-batches in
     // turn, each at most max(SEC_SLAB_BYTES, one chunk's parity)
     PinBuf piece_par[2];
@@ -683,6 +684,24 @@ sec::TaskPool &tasks(sec_ctx *ctx)
 }
 
 sec::TaskPool &pool(sec_ctx *ctx) { return tasks(ctx); }
+
+// sec_encode_pieces' piece copies and SHA-1 ids run on a second shared pool of the usable CPUs but
+// four (at most 12), the staging copies and joins staying on the 7-thread pool.  Against one
+// pool for everything (16-CPU quota): the 1 GiB upload stream 5.0 -> 7.5-7.9 GiB/s, an 8 MiB
+// chunk's encode + ids 1.2 -> 0.8 ms, C5 and the downloads level; one pool of 12-14 threads for
+// everything throttled C5 instead (profiles/r06_hash_pool_ab.txt, r06_pool_threads_ab.txt).
+// SEC_HASH_POOL (build knob, A/B): 0 = everything on the one pool.
+#ifndef SEC_HASH_POOL
+#define SEC_HASH_POOL 1
+#endif
+sec::TaskPool &hash_tasks(sec_ctx *ctx)
+{
+    if (!SEC_HASH_POOL || ctx->opt[O_COPY_THREADS])
+        return tasks(ctx);
+    if (!ctx->hash_tasks)
+        ctx->hash_tasks = sec::shared_pool(std::min(12, std::max(1, sec::usable_cpus() - 4)));
+    return *ctx->hash_tasks;
+}
 
 int slots_init(sec_ctx *ctx)
 {
@@ -1768,6 +1787,7 @@ void sec_ctx_destroy(sec_ctx *ctx)
             (void)hipStreamDestroy(s.s);
     }
     ctx->tasks.reset();
+    ctx->hash_tasks.reset();
     for (PinBuf &b : ctx->piece_par)
         b.release();
     ctx->pin.release();
@@ -1828,8 +1848,10 @@ int sec_ctx_set_option(sec_ctx *ctx, const char *name, int64_t value)
     ctx->opt.v[i] = value;
     for (Plan *p : {&ctx->enc_plan, &ctx->dec_plan, &ctx->sha_plan, &ctx->bn_plan})
         p->valid = false;
-    if (i == O_COPY_THREADS)
+    if (i == O_COPY_THREADS) {
         ctx->tasks.reset();
+        ctx->hash_tasks.reset();
+    }
     return SEC_OK;
 }
 
@@ -2345,7 +2367,7 @@ int sec_encode_pieces(sec_ctx *ctx, const sec_enc_chunk *chunks, int64_t nchunks
     const uint64_t cap =
         std::max<uint64_t>((uint64_t)ctx->opt[gpu_ids ? O_SLAB_BYTES_DIGEST : O_SLAB_BYTES], max_par);
     std::vector<uint8_t> par_dig;  // gpu_ids: a sub-batch's parity digests, chunk by chunk
-    sec::TaskPool &tp = tasks(ctx);
+    sec::TaskPool &tp = hash_tasks(ctx);
     sec::TaskPool::Group data, par[2];
     bool par_failed = false;
     std::vector<sec_enc_chunk> tmp(chunks, chunks + nchunks);
