@@ -703,6 +703,16 @@ sec::TaskPool &hash_tasks(sec_ctx *ctx)
     return *ctx->hash_tasks;
 }
 
+// The host-only joins (chunks with every primary present, a staged reassembly's present rows,
+// sec_host_copy) run on the second pool too; the joins beside zero-copy kernels (C5's path) stay
+// on the first.  The 1 GiB download stream with every data piece present 41-52 -> 53-69 GiB/s,
+// C5's staged decode 14.5 -> 16-17.5, C5 itself and the upload level
+// (profiles/r06_join_pool_ab.txt).  SEC_JOIN_POOL (build knob, A/B): 0 = on the first pool.
+#ifndef SEC_JOIN_POOL
+#define SEC_JOIN_POOL 1
+#endif
+sec::TaskPool &join_tasks(sec_ctx *ctx) { return SEC_JOIN_POOL ? hash_tasks(ctx) : tasks(ctx); }
+
 int slots_init(sec_ctx *ctx)
 {
     for (Slot &s : ctx->slots)
@@ -2840,7 +2850,7 @@ int join_staged(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
                 const uint64_t *block_offs, const uint64_t *block_avail, const uint8_t *blocks, uint8_t *out,
                 unsigned flags)
 {
-    sec::TaskPool &tp = tasks(ctx);
+    sec::TaskPool &tp = join_tasks(ctx);
     sec::TaskPool::Group g;
     std::vector<sec_dec_chunk> sub(chunks, chunks + nchunks);
     for (const sec_dec_chunk &c : sub)
@@ -2937,7 +2947,7 @@ int decode_core(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks, cons
             if (primary_lost(chunks[i], sharenums))
                 sub.push_back(chunks[i]);
         if ((int64_t)sub.size() < nchunks) {
-            sec::TaskPool &tp = tasks(ctx);
+            sec::TaskPool &tp = join_tasks(ctx);
             sec::TaskPool::Group g;
             for (int64_t i = 0; i < nchunks; ++i)
                 if (!primary_lost(chunks[i], sharenums))
@@ -3225,7 +3235,7 @@ int sec_host_copy(sec_ctx *ctx, const sec_copy *jobs, int64_t njobs)
         cj.push_back(sec::CopyJob{(void *)(uintptr_t)jobs[i].dst, (const void *)(uintptr_t)jobs[i].src,
                                   (size_t)jobs[i].len});
     }
-    pool(ctx).run_copies(cj);
+    join_tasks(ctx).run_copies(cj);
     return SEC_OK;
 }
 
