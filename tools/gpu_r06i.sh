@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: library task pool A/Bs (VAR=p12: pool size; VAR=onepool: the separate hash pool off) on what they move: the C5 end-to-end line (pinned host
+# Round 6: library task pool A/Bs (VAR=p12: pool size; VAR=hashpool / joinpool: the second pool for piece copies + ids / host-only joins, measured as variants before they became the product) on what they move: the C5 end-to-end line (pinned host
 # memory, the host joins beside the zero-copy kernels) and the 1 GiB piece streams.  This build
 # against build/variants/libstorbec_${VAR}.so, alternating, twice.
 set -o pipefail
