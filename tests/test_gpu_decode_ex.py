@@ -401,21 +401,23 @@ def test_fuzz_host_reassembly_join(mode):
         eng.close()
 
 
+@pytest.mark.parametrize("B,nch", [(256 << 10, 6), (1 << 20, 8)])
 @pytest.mark.parametrize("staged_flag", [False, True])
-def test_scattered_blocks_read_back_from_out(staged_flag):
+def test_scattered_blocks_read_back_from_out(staged_flag, B, nch):
     """A host reassembly whose blocks are too scattered to page-lock (256 KiB blocks 5 MiB apart:
     the library stages them) but whose output is one large range (api.cpp join_staged): the
     present primaries are copied into `out` first and the rows-only call reads them from there
     with `out` locked (host path counts: one locked call, nothing staged).  With staged=True
     nothing may be locked: the rows-only call stages the caller's blocks while the copies run.
-    Chunks with every primary present, one lost, and block k-1 lost or short in place."""
+    Chunks with every primary present, one lost, and block k-1 lost or short in place; 12 MiB and
+    64 MiB of output (the second read back in groups of chunks when SEC_JOIN_GROUPS > 1, still
+    one host path per call)."""
     from storb_amd.engine import Engine
 
     eng = Engine(0)
     try:
         rng = random.Random(5)
-        k, m, B, gap = 8, 12, 256 << 10, 5 << 20
-        nch = 6
+        k, m, gap = 8, 12, 5 << 20
         sizes = [k * B - rng.randrange(0, 3) for _ in range(nch)]
         arena = np.empty(nch * k * gap + B, np.uint8)  # untouched pages cost nothing
         src = [rng.randbytes(n) for n in sizes]
@@ -424,7 +426,7 @@ def test_scattered_blocks_read_back_from_out(staged_flag):
         sn = np.zeros(nch * k, np.int32)
         offs = np.zeros(nch * k, np.uint64)
         avail = np.zeros(nch * k, np.uint64)
-        lost_sets = [(), (3,), (k - 1,), (0, 5), (), (2, k - 1)]
+        lost_sets = [(), (3,), (k - 1,), (0, 5), (), (2, k - 1), (1,), (0,)][:nch]
         for i, (n, data) in enumerate(zip(sizes, src)):
             blocks = cfec.easy_encode(data, k, m)
             dd["out_off"][i], dd["B"][i], dd["padlen"][i] = i * k * B, B, k * B - n
