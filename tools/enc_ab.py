@@ -29,6 +29,15 @@ CASES = [
     ("zfec(64,96) 64MiB x16 (ragged)", 64, 96, (64 << 20) - 12345, 16),
     ("zfec(32,48) 1MiB x1024", 32, 48, 1 << 20, 1024),
     ("zfec(16,24) 8MiB x128", 16, 24, 8 << 20, 128),
+    # the block stride (B) question of DESIGN §8 item 3: power-of-two B at several spans, and
+    # non-power-of-two B at the 256 MiB span
+    ("stride: zfec(64,96) 16MiB x64 (B 256 KiB)", 64, 96, 16 << 20, 64),
+    ("stride: zfec(64,96) 64MiB x16 (B 1 MiB)", 64, 96, 64 << 20, 16),
+    ("stride: zfec(64,96) 128MiB x8 (B 2 MiB)", 64, 96, 128 << 20, 8),
+    ("stride: zfec(64,96) 256MiB x4 (B 4 MiB)", 64, 96, 256 << 20, 4),
+    ("stride: zfec(64,96) 252MiB x4 (B 4032 KiB)", 64, 96, 252 << 20, 4),
+    ("stride: zfec(64,96) 260MiB x4 (B 4160 KiB)", 64, 96, 260 << 20, 4),
+    ("stride: zfec(64,96) 256MiB-4KiB x4 (B 4 MiB - 64)", 64, 96, (256 << 20) - 4096, 4),
 ]
 
 
