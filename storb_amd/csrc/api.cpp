@@ -507,6 +507,9 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
 // group, (32,48) in 8-row groups, the interleaved launch, LDS-staged small chunks -- are
 // archived: tools/archive/.)
 constexpr int kBsPair = 98;       // Group::U of a two-wave launch, both row groups of a span per workgroup
+#ifndef SEC_PAIR_XCD_MIN_B
+#define SEC_PAIR_XCD_MIN_B (3u << 20)  // the pair encode's XCD order from this block size (see flatten)
+#endif
 constexpr int kSolveLds = 1 << 16;  // phase-2 tile map keys of sec_solve_bs_lds_kernel launches
 constexpr int kSynWg2 = 1 << 16;    // phase-1 tile map keys of sec_syndrome_bs_pair_kernel launches
 
@@ -528,7 +531,8 @@ int bs_shape(const Options &o, int k, int m, uint64_t B)
 void add_bs_work(const Options &o, Bins &bins, uint32_t chunk, uint64_t B, int shape)
 {
     if (sec_bs_groups(shape) > 1) {  // (64,96): one two-wave workgroup per span
-        auto &bin = bins[{3, shape, kBsPair, 128, 0}];
+        // (chunks of B >= SEC_PAIR_XCD_MIN_B in their own group, launched in XCD order: see flatten)
+        auto &bin = bins[{3, shape, kBsPair, 128, B >= (uint64_t)SEC_PAIR_XCD_MIN_B ? 1 : 0}];
         for (uint64_t t0 = 0; t0 < B; t0 += sec_bs_span())
             bin.push_back(sec::Tile{chunk, (uint32_t)t0, 0, 0});
         return;
@@ -551,6 +555,15 @@ void add_bs_work(const Options &o, Bins &bins, uint32_t chunk, uint64_t B, int s
 #ifndef SEC_XCD_ORDER
 #define SEC_XCD_ORDER 0
 #endif
+
+// The zfec(64,96) pair encode of chunks with blocks of B >= 3 MiB runs its tiles in XCD order.
+// In chunk order the ~512 resident workgroups cover about 1 MiB of each block row (2 KiB spans),
+// so with 4 MiB blocks (storb's 256 MiB chunks) the 64 rows a span reads are 1 MiB windows at a
+// 4 MiB stride and the concurrent addresses never vary the bits between: 3.82-4.01 TB/s, against
+// 4.26 for B = 4032 KiB.  In XCD order each XCD walks its own eighth of the tiles, and 256 MiB
+// chunks run 4.25-4.35 (+9-11 %); for 1 MiB-block (64 MiB) chunks, whose resident workgroups
+// already cover whole rows, XCD order cost 4 %, so it stays off below 3 MiB
+// (profiles/r06_enc_order_ab.jsonl).  SEC_PAIR_XCD_MIN_B (build knob, A/B; defined above add_bs_work).
 
 bool use_xcd_order(bool, const Group &g) { return g.mfma < 3 && SEC_XCD_ORDER == 1; }
 
@@ -578,7 +591,7 @@ void flatten(const Bins &bins, std::vector<Group> &groups, std::vector<sec::Tile
         groups.push_back(Group{std::get<1>(kv.first), std::get<2>(kv.first), std::get<3>(kv.first),
                                std::get<4>(kv.first), (uint32_t)first, (uint32_t)(tiles.size() - first),
                                std::get<0>(kv.first)});
-        if (use_xcd_order(decode, groups.back())) {
+        if (use_xcd_order(decode, groups.back()) || (std::get<2>(kv.first) == kBsPair && std::get<4>(kv.first))) {
             std::vector<sec::Tile> g(tiles.begin() + first, tiles.end());
             xcd_order(g);
             std::copy(g.begin(), g.end(), tiles.begin() + first);
