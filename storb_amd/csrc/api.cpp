@@ -507,6 +507,9 @@ void add_work(Bins &bins, std::vector<sec::TailItem> &tail, uint32_t chunk, uint
 // group, (32,48) in 8-row groups, the interleaved launch, LDS-staged small chunks -- are
 // archived: tools/archive/.)
 constexpr int kBsPair = 98;       // Group::U of a two-wave launch, both row groups of a span per workgroup
+#ifndef SEC_DEC_XCD_BIG
+#define SEC_DEC_XCD_BIG 1  // the same order for the wide decodes' tiles (build knob, A/B; see build_decode_plan)
+#endif
 #ifndef SEC_PAIR_XCD_MIN_B
 #define SEC_PAIR_XCD_MIN_B (3u << 20)  // the pair encode's XCD order from this block size (see flatten)
 #endif
@@ -1339,6 +1342,26 @@ int build_decode_plan(sec_ctx *ctx, const sec_dec_chunk *chunks, int64_t nchunks
                 add_work(bins, tail, (uint32_t)(i - c0), c.B, valid, (int)e_of[i], c.k, true, false,
                          recover || nocopy ? dec_small_kb(c.k) : 0);
             }
+        }
+        // The two-kernel wide decode's tiles (phase 1 pairs, phase 2 LDS spans) in XCD order when
+        // their blocks are large, as the pair encode's (add_bs_work): zfec(64,96) on 256 MiB chunks,
+        // 32 lost 2.24 -> 2.39 TB/s, 24 random 2.51 -> 2.69; the one-wave fused path lost 8 % to it
+        // and keeps chunk order (profiles/r06_dec_order_ab.jsonl).
+        if (SEC_DEC_XCD_BIG) {
+            auto big = [&](const std::vector<sec::Tile> &t, auto B_of) {
+                for (const sec::Tile &x : t)
+                    if (B_of(x) >= (uint64_t)SEC_PAIR_XCD_MIN_B)
+                        return true;
+                return false;
+            };
+            auto sB = [&](const sec::Tile &x) { return (uint64_t)sdescs[x.chunk].B; };
+            auto vB = [&](const sec::Tile &x) { return (uint64_t)vdescs[x.chunk].B; };
+            for (auto &kv : stiles)
+                if (kv.first >= kSynWg2 && big(kv.second, sB))
+                    xcd_order(kv.second);
+            for (auto &kv : vtiles)
+                if (kv.first >= kSolveLds && big(kv.second, vB))
+                    xcd_order(kv.second);
         }
         std::vector<sec::Tile> tiles, stl, vtl;
         flatten(bins, sp.groups, tiles, true);

@@ -24,6 +24,7 @@ sys.path.insert(0, ROOT)
 # (name, k, m, chunk bytes, chunks, lost data blocks)
 CASES = [
     ("zfec(64,96) 256MiB x4, 16 lost", 64, 96, 256 << 20, 4, 16),
+    ("zfec(64,96) 256MiB x4, 32 lost (every parity row)", 64, 96, 256 << 20, 4, 32),
     ("zfec(64,96) 1MiB x1024, 16 lost", 64, 96, 1 << 20, 1024, 16),
     ("zfec(64,96) 1MiB x1024, 32 lost (every parity row)", 64, 96, 1 << 20, 1024, 32),
     ("zfec(32,48) 1MiB x1024, 16 lost (every parity row)", 32, 48, 1 << 20, 1024, 16),
@@ -34,6 +35,7 @@ CASES = [
     # random lost data blocks and random present parity rows (seeded): what retrievals see
     ("zfec(64,96) 1MiB x1024, 16 lost (random, parity random)", 64, 96, 1 << 20, 1024, 16, 1),
     ("zfec(64,96) 1MiB x1024, 24 lost (random, parity random)", 64, 96, 1 << 20, 1024, 24, 2),
+    ("zfec(64,96) 256MiB x4, 24 lost (random, parity random)", 64, 96, 256 << 20, 4, 24, 2),
     ("zfec(32,48) 1MiB x1024, 12 lost (random, parity random)", 32, 48, 1 << 20, 1024, 12, 3),
     ("zfec(32,48) 1MiB x1024, 16 lost (random)", 32, 48, 1 << 20, 1024, 16, 4),
     # every one of the m blocks fetched, a random 10-30 % of them lost (data and parity): the decode
